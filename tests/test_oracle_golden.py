@@ -1,0 +1,140 @@
+"""Pin the CPU oracle to the golden vectors produced by the real reference
+(tests/golden/make_golden.py). CPU only; no GPU, no libcapmi."""
+import numpy as np
+import pytest
+import torch
+
+import gen
+from oracle import decoder_ref as R
+from oracle.resnet_ref import build_resnet101, encoder_attention_forward
+
+
+def t(x):
+    return torch.from_numpy(np.ascontiguousarray(x))
+
+
+def check_samples(fx, prefix, x, rtol=1e-5, atol=1e-6):
+    x = np.asarray(x).ravel()
+    idx = fx[prefix + "__idx"]
+    np.testing.assert_allclose(x[idx], fx[prefix + "__val"], rtol=rtol, atol=atol)
+    d = gen.digest(x)
+    np.testing.assert_allclose(d, fx[prefix + "__digest"], rtol=max(rtol, 1e-6) * 10, atol=atol * x.size ** 0.5)
+
+
+@pytest.mark.parametrize("tag", ["prod", "small"])
+def test_soft_attention(golden, tag):
+    fx = golden(f"soft_attention_{tag}")
+    m = fx["meta"]
+    B, P, E, D, A, s = m["B"], m["P"], m["E"], m["D"], m["A"], m["seed"]
+    p = {"attention.enc_att.weight": gen.uniform(s, "ea.w", (A, E), -E ** -.5, E ** -.5),
+         "attention.enc_att.bias": gen.uniform(s, "ea.b", (A,), -E ** -.5, E ** -.5),
+         "attention.dec_att.weight": gen.uniform(s, "da.w", (A, D), -D ** -.5, D ** -.5),
+         "attention.dec_att.bias": gen.uniform(s, "da.b", (A,), -D ** -.5, D ** -.5),
+         "attention.full_att.weight": gen.uniform(s, "fa.w", (1, A), -A ** -.5, A ** -.5),
+         "attention.full_att.bias": gen.uniform(s, "fa.b", (1,), -A ** -.5, A ** -.5)}
+    p = {k: t(v) for k, v in p.items()}
+    awe, alpha = R.soft_attention(p, t(gen.uniform(s, "enc", (B, P, E), 0, 1)),
+                                  t(gen.uniform(s, "h", (B, D), -1, 1)))
+    np.testing.assert_allclose(awe.numpy(), fx["awe"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(alpha.numpy(), fx["alpha"], rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("tag", ["small_ragged", "small_full", "prod"])
+def test_decoder_forward(golden, tag):
+    fx = golden(f"decoder_forward_{tag}")
+    m = fx["meta"]
+    p = {k: t(v) for k, v in gen.decoder_params(m["seed"], m["A"], m["D"], m["M"], m["V"]).items()}
+    enc = t(gen.encoder_features(m["seed"], m["B"]))
+    caps = t(fx["captions"])
+    with torch.no_grad():
+        h0, c0 = R.init_hidden_state(p, enc.view(m["B"], -1, 2048))
+        preds, _, dl, alphas = R.decoder_forward(p, enc, caps, m["lengths"])
+    assert dl == m["decode_lengths"]
+    np.testing.assert_allclose(h0.numpy(), fx["h0"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(c0.numpy(), fx["c0"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(alphas.numpy(), fx["alphas"], rtol=1e-5, atol=1e-7)
+    if "predictions" in fx:
+        np.testing.assert_allclose(preds.numpy(), fx["predictions"], rtol=1e-5, atol=1e-6)
+    else:
+        check_samples(fx, "predictions", preds.numpy())
+
+
+def oracle_encoder(resnet_seed, order, seed, train=True):
+    net = build_resnet101(gen.resnet101_params(resnet_seed))
+    net.train(train)
+    imgs = np.concatenate([gen.images(seed, 1, name=f"img{i}") for i in order])
+    with torch.no_grad():
+        feats = encoder_attention_forward(net, t(imgs))
+    return net, imgs, feats
+
+
+@pytest.mark.parametrize("tag", ["small", "glove_small", "prod"])
+def test_train_step(golden, tag):
+    fx = golden(f"train_step_{tag}")
+    m = fx["meta"]
+    net, imgs, feats = oracle_encoder(m["resnet_seed"], fx["order"], m["seed"])
+    np.testing.assert_allclose(gen.digest(imgs), fx["imgs_digest"], rtol=1e-9)
+    # encoder (restated resnet inside the reference wrapper, BN train mode)
+    check_samples(fx, "enc", feats.numpy(), rtol=1e-4, atol=1e-5)
+    for k in ("layer4.2.bn3.running_mean", "layer1.0.bn1.running_var"):
+        check_samples(fx, "enc_post.resnet." + _resnet_child_key(k), net.state_dict()[k].numpy(),
+                      rtol=1e-4, atol=1e-6)
+    # decoder step on the golden's own encoder output samples would need the full
+    # tensor; use the oracle's (checked above) features.
+    emb_dt = np.float64 if m["glove"] else np.float32
+    p = {k: t(v) for k, v in gen.decoder_params(m["seed"], m["A"], m["D"], m["M"], m["V"],
+                                                 emb_dtype=emb_dt).items()}
+    assert m["caption_lengths_seen"] == [fx["captions"].shape[1]] * m["B"]  # Q1
+    loss, preds, alphas, raw, grads, new_p, _ = R.train_step(
+        p, set(m["trainable"]), feats, t(fx["captions"]), m["caption_lengths_seen"])
+    np.testing.assert_allclose(loss.item(), float(fx["loss"]), rtol=1e-5)
+    np.testing.assert_allclose(alphas.numpy(), fx["alphas"], rtol=1e-4, atol=1e-6)
+    full = "predictions" in fx
+    if full:
+        np.testing.assert_allclose(preds.numpy(), fx["predictions"], rtol=1e-4, atol=1e-5)
+    else:
+        check_samples(fx, "predictions", preds.numpy(), rtol=1e-4, atol=1e-5)
+    for k in m["trainable"]:
+        g = raw[k].numpy()
+        if full:
+            np.testing.assert_allclose(g, fx["grad." + k], rtol=1e-3, atol=1e-6, err_msg=k)
+            np.testing.assert_allclose(new_p[k].numpy(), fx["post." + k], rtol=1e-5, atol=1e-6, err_msg=k)
+        else:
+            check_samples(fx, "grad." + k, g, rtol=1e-3, atol=1e-6)
+            check_samples(fx, "post." + k, new_p[k].numpy(), rtol=1e-5, atol=1e-6)
+
+
+def _resnet_child_key(k):
+    # EncoderAttention.resnet = Sequential(children()[:-2]) -> numeric child names
+    names = ["conv1", "bn1", "relu", "maxpool", "layer1", "layer2", "layer3", "layer4"]
+    head, rest = k.split(".", 1)
+    return f"{names.index(head)}.{rest}"
+
+
+def test_baseline_forward(golden):
+    fx = golden("baseline_forward")
+    m = fx["meta"]
+    B, L, M, H, V, s = m["B"], m["L"], m["M"], m["H"], m["V"], m["seed"]
+    shapes = {"embedding.weight": (V, M), "lstm.weight_ih_l0": (4 * H, M), "lstm.weight_hh_l0": (4 * H, H),
+              "lstm.bias_ih_l0": (4 * H,), "lstm.bias_hh_l0": (4 * H,), "linear.weight": (V, H),
+              "linear.bias": (V,)}
+    p = {k: t(gen.uniform(s, k, v, -0.2, 0.2)) for k, v in shapes.items()}
+    feats = t(gen.uniform(s, "feats", (B, M), -1, 1))
+    with torch.no_grad():
+        scores = R.baseline_forward(p, feats, t(fx["captions"]))
+        loss = R.baseline_loss(scores, t(fx["captions"]))
+    np.testing.assert_allclose(scores.numpy(), fx["scores"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(loss.item(), float(fx["loss"]), rtol=1e-6)
+
+
+@pytest.mark.parametrize("case", ["eval_1x160", "train_1x160"])
+def test_encoder_wrapper(golden, case):
+    fx = golden(f"encoder_{case}")
+    m = fx["meta"]
+    net = build_resnet101(gen.resnet101_params(m["resnet_seed"]))
+    net.train(m["mode"] == "train")
+    x = gen.images(m["resnet_seed"], m["B"], m["H"], m["H"], name=f"img_{m['mode']}_{m['H']}")
+    with torch.no_grad():
+        y = encoder_attention_forward(net, t(x))
+    assert list(y.shape) == list(fx["shape"])
+    check_samples(fx, "features", y.numpy(), rtol=1e-4, atol=1e-5)
