@@ -1,0 +1,196 @@
+"""Headline benchmark: 'attention' captioner training images/sec on MI355X.
+
+python bench.py --gpus N --steps K --warmup W     (N > 1: launched by torchrun, one rank per GPU)
+
+One step = the reference's training step (models/attention.py:386-430) on a resident
+synthetic batch of 64 (image 3x224x224, 25-token caption, V = 8100) per GPU: ResNet-101
+encoder forward (frozen, BatchNorm in train mode), 24-step soft-attention decoder
+forward + backward, CE + doubly-stochastic loss, (DP: gradient all-reduce over RCCL),
+clamp + Adam. fp32 throughout (the reference's precision). Weights: torch.manual_seed(0)
+random init of the reference architecture (no checkpoints offline).
+
+Rank 0 prints ONE JSON line. ``roofline`` is for the dominant kernel (the conv implicit-
+GEMM family, 86% of the step's FLOPs): achieved = conv FLOPs / summed conv kernel time,
+timed with HIP events on the launch stream around every conv launch of the timed steps.
+``cpu_baseline`` times the CPU oracle (op-for-op restatement of the reference step) on
+the host cores, rank 0 at N = 1 only, on a small bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "image-captioning-with-different-decoders_amd")
+for _p in (PKG, REPO):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+FP32_MFMA_PEAK_TF = 157.3   # MI355X fp32 matrix peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
+    ap.add_argument("--caption-len", type=int, default=25)
+    ap.add_argument("--vocab", type=int, default=8100)
+    ap.add_argument("--no-roofline", action="store_true", help="skip per-conv event timing")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+class ConvTimer:
+    """HIP-event bracket around every conv GEMM launch (on the launch stream)."""
+
+    def __init__(self):
+        self.events = []
+        self.flops = 0.0
+        self.enabled = False
+
+    def __call__(self, tag, flops, launch):
+        if not self.enabled:
+            launch()
+            return
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        launch()
+        e.record()
+        self.events.append((s, e))
+        self.flops += flops
+
+    def result(self):
+        ms = sum(s.elapsed_time(e) for s, e in self.events)
+        return ms, self.flops, len(self.events)
+
+
+def cpu_baseline(args, seconds):
+    """Oracle (CPU restatement of the reference step) on a bounded sample: B=2, full
+    ResNet-101 encoder forward + the unhoisted 24-step decoder fwd/bwd + clamp + Adam."""
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    import gen
+    from oracle import decoder_ref as R
+    from oracle.resnet_ref import build_resnet101, encoder_attention_forward
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    B, L, V = 2, args.caption_len, args.vocab
+    net = build_resnet101(gen.resnet101_params(5)).train()
+    p = {k: torch.from_numpy(v) for k, v in gen.decoder_params(5, 512, 512, 512, V).items()}
+    trainable = set(k for k in p if k != "embedding.weight")
+    imgs = torch.from_numpy(gen.images(5, B))
+    caps = torch.from_numpy(gen.captions(5, B, L, V))
+    state, n, t0 = {}, 0, None
+    while True:
+        with torch.no_grad():
+            feats = encoder_attention_forward(net, imgs)
+        out = R.train_step(p, trainable, feats, caps, [L] * B, state=state)
+        p.update(out[5])
+        state = out[6]
+        n += 1
+        if t0 is None:          # first step is warm-up
+            t0, n = time.perf_counter(), 0
+        elif time.perf_counter() - t0 > seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(B * n / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} oracle train steps at B={B} (ResNet-101 fwd + unhoisted decoder fwd/bwd + "
+                      f"clamp/Adam, L={L}, V={V}), torch CPU fp32, {threads} threads, {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    from capmi import dist as cdist
+    ctx = cdist.init_from_env("cuda")
+    dev = ctx.device
+    from capmi.data import synthetic_batch
+    from capmi.optim import Adam
+    from capmi.resnet import conv_flops_per_image
+    from capmi.train_step import AttentionTrainStep
+    from models.attention import AttentionDecoder, AttentionDecoderParams
+    from models.encoder import EncoderAttention
+    from vocabulary import synthetic_vocab
+
+    torch.manual_seed(0)
+    encoder = EncoderAttention().to(dev).train()
+    prm = AttentionDecoderParams()
+    prm.vocab = synthetic_vocab(args.vocab)
+    decoder = AttentionDecoder(dev, prm).to(dev).train()
+    decoder.fine_tune_embeddings(False)  # reference default (--fine_tune_embedding False, Q8)
+    cdist.broadcast_module(decoder, ctx)
+    opt = Adam(filter(lambda q: q.requires_grad, decoder.parameters()), lr=1e-4)
+    opt.set_clip(5.0)
+    step = AttentionTrainStep(encoder, decoder, opt, ctx, alpha_c=1.0)
+    timer = ConvTimer()
+    encoder._runner.conv_hook = None if args.no_roofline else timer
+    B = args.batch
+    imgs, caps, lens = synthetic_batch(B, args.caption_len, args.vocab, dev, seed=1234 + ctx.rank)
+
+    for _ in range(args.warmup):
+        step(imgs, caps, lens)
+    step.flush()
+    torch.cuda.synchronize()
+    cdist.barrier(ctx)
+    torch.cuda.synchronize()
+    timer.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step(imgs, caps, lens)
+    step.flush()
+    torch.cuda.synchronize()
+    cdist.barrier(ctx)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    timer.enabled = False
+    dt = cdist.max_over_ranks(dt, ctx)
+    loss_v = float(loss.item())
+
+    N = ctx.world
+    value = N * B * args.steps / dt
+    roof = None
+    if not args.no_roofline and timer.events:
+        ms, flops, launches = timer.result()
+        ach = flops / (ms * 1e-3) / 1e12
+        per_img = conv_flops_per_image(_view(encoder))
+        roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                "frac": round(ach / FP32_MFMA_PEAK_TF, 4), "traffic": None,
+                "kernel": "gemm_kernel<128,128,...> (ResNet-101 implicit-GEMM convs)",
+                "flops_per_launch": round(flops / launches), "avg_launch_us": round(ms * 1e3 / launches, 2),
+                "conv_gflop_per_image": round(per_img / 1e9, 3),
+                "conv_ms_per_step": round(ms / args.steps, 3)}
+    cpu = None
+    if ctx.rank == 0 and N == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, args.cpu_seconds)
+    if ctx.rank == 0:
+        line = {
+            "metric": "training images/sec (whole node), 'attention' decoder, at 1/2/4/8 MI355X",
+            "value": round(value, 2), "unit": "images/s", "n_gpus": N, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (resident in HBM; random-init weights, torch.manual_seed(0))",
+            "config": {"workload": "'attention' decoder + frozen ResNet-101 encoder (BN train mode), "
+                                   "one training step per batch", "per_gpu_batch": B, "global_batch": B * N,
+                       "caption_len": args.caption_len, "decode_steps": args.caption_len - 1,
+                       "vocab": args.vocab, "attention_dim": 512, "decoder_dim": 512, "embed_size": 512,
+                       "parallelism": f"dp{N}"},
+            "loss_last_step": round(loss_v, 5),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+
+
+def _view(enc):
+    from models.encoder import _ResNetView
+    return _ResNetView(enc.resnet)
+
+
+if __name__ == "__main__":
+    main()

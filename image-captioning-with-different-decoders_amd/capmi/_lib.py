@@ -1,0 +1,120 @@
+"""ctypes binding of libcapmi.so (C ABI declared in include/capmi.h).
+
+The library is the only compute path for CUDA(HIP) tensors: there is no
+fallback. If it is missing this module raises at import time.
+
+``import torch`` happens first on purpose: torch's bundled libamdhip64.so
+(SONAME libamdhip64.so.7) must be the HIP runtime libcapmi binds to, so both
+share one runtime (streams, allocations, graph capture).
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before libcapmi)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcapmi.so")
+
+c_int, c_ll, c_float, c_double, c_vp = ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
+c_ull = ctypes.c_ulonglong
+
+CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_A_CONV_NHWC, CAPMI_A_CONV_NCHW = 0, 1, 2, 3
+CAPMI_B_NMAJOR_W, CAPMI_B_KROWS = 0, 1
+CAPMI_TILE_128, CAPMI_TILE_64 = 0, 1
+CAPMI_MAX_GROUP = 4
+CAPMI_COLSUM_ROWS = 256
+ABI_VERSION = 1
+
+
+class GemmProblem(ctypes.Structure):
+    """Mirror of ``capmi_gemm_problem`` (include/capmi.h)."""
+    _fields_ = [
+        ("M", c_int), ("N", c_int), ("K", c_int), ("ksplit", c_int),
+        ("A", c_vp), ("lda", c_ll), ("a_r1", c_ll), ("a_s2", c_ll),
+        ("B", c_vp), ("ldb", c_ll),
+        ("C", c_vp), ("ldc", c_ll), ("c_r1", c_ll), ("c_s2", c_ll), ("c_split_stride", c_ll),
+        ("bias", c_vp), ("bias2", c_vp), ("alpha_ptr", c_vp),
+        ("alpha", c_float), ("beta", c_float), ("relu", c_int),
+        ("stats", c_vp),
+        ("cN", c_int), ("cH", c_int), ("cW", c_int), ("cCin", c_int), ("cKH", c_int),
+        ("cKW", c_int), ("cStride", c_int), ("cPad", c_int), ("cHo", c_int), ("cWo", c_int),
+        ("in_scale", c_vp), ("in_shift", c_vp),
+    ]
+
+
+# name -> argtypes (restype is int unless listed in _RESTYPES)
+_SIGS = {
+    "capmi_gemm": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_int, c_vp],
+    "capmi_gemm_stat_tiles": [c_int, c_int],
+    "capmi_splitk_reduce": [c_vp, c_int, c_ll, c_int, c_int, c_ll, c_vp, c_vp, c_ll, c_vp],
+    "capmi_colsum": [c_vp, c_int, c_int, c_ll, c_float, c_vp, c_vp, c_int, c_vp],
+    "capmi_conv_weight_pack": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
+    "capmi_bn_finalize": [c_vp, c_int, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_float, c_float,
+                          c_vp, c_vp, c_vp, c_vp, c_vp],
+    "capmi_bn_eval_params": [c_vp, c_vp, c_vp, c_vp, c_int, c_float, c_vp, c_vp, c_vp],
+    "capmi_bn_add_relu": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_vp],
+    "capmi_bn_relu_maxpool": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
+    "capmi_adaptive_avgpool_nhwc": [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp],
+    "capmi_embed_gather": [c_vp, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp, c_ll, c_vp],
+    "capmi_mean_rows": [c_vp, c_int, c_int, c_int, c_vp, c_vp],
+    "capmi_att_score_fwd": [c_vp, c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp,
+                            c_vp, c_vp],
+    "capmi_att_softmax_ctx_fwd": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_ll, c_vp, c_vp,
+                                  c_int, c_ll, c_vp, c_vp, c_vp, c_ll, c_vp],
+    "capmi_lstm_cell_fwd": [c_vp, c_int, c_ll, c_vp, c_vp, c_int, c_ll, c_vp, c_int, c_int, c_vp,
+                            c_vp, c_vp, c_vp],
+    "capmi_dropout": [c_vp, c_ll, c_float, c_ull, c_vp, c_vp],
+    "capmi_mask_rows_tb": [c_vp, c_vp, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_vp],
+    "capmi_ce_fwd_bwd": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp,
+                         c_int, c_vp, c_vp],
+    "capmi_alpha_reg": [c_vp, c_int, c_int, c_int, c_float, c_vp, c_vp, c_vp],
+    "capmi_loss_finalize": [c_vp, c_int, c_int, c_vp, c_vp, c_vp],
+    "capmi_lstm_cell_bwd": [c_vp, c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int,
+                            c_vp, c_vp, c_vp],
+    "capmi_att_ctx_bwd": [c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp],
+    "capmi_att_score_bwd": [c_vp, c_vp, c_ll, c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_int,
+                            c_int, c_vp, c_vp, c_vp],
+    "capmi_att_enc_grad": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,
+                           ctypes.POINTER(c_int), c_vp],
+    "capmi_adam_clamp": [c_vp, c_vp, c_vp, c_vp, c_ll, c_float, c_float, c_float, c_float, c_float,
+                         c_float, c_float, c_vp],
+    "capmi_adam_clamp_f64": [c_vp, c_vp, c_vp, c_vp, c_ll, c_double, c_double, c_double, c_double,
+                             c_double, c_double, c_double, c_vp],
+    "capmi_embed_scatter_add": [c_vp, c_ll, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp],
+    "capmi_strerror": [c_int],
+    "capmi_abi_version": [],
+}
+_RESTYPES = {"capmi_strerror": ctypes.c_char_p}
+EXPORTS = tuple(_SIGS)
+
+
+class CapmiError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libcapmi.so not found at {LIB_PATH}: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (the HIP kernels are the only "
+            "compute path; there is no fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPES.get(name, c_int)
+    if lib.capmi_abi_version() != ABI_VERSION:
+        raise ImportError("libcapmi.so ABI version mismatch; rebuild it")
+    return lib
+
+
+lib = _load()
+
+
+def check(code, what=""):
+    if code != 0:
+        raise CapmiError(f"{what}: {lib.capmi_strerror(code).decode()} (code {code})")
+
+
+def call(name, *args):
+    check(getattr(lib, name)(*args), name)

@@ -1,0 +1,331 @@
+"""Forward and backward-through-time of the soft-attention LSTM decoder on libcapmi.
+
+Restates models/attention.py:218-284 (AttentionDecoder.forward) and, for the
+backward pass, what autograd does through it, with the loop-invariant work
+hoisted out of the 24-step recurrence:
+
+  * ``enc_att(encoder_out)`` (:54, recomputed every step by the reference, Q5)
+    is one GEMM before the loop; its weight gradient is one GEMM after it,
+    over d(att_enc) summed over t (exact in math, different fp32 sum order);
+  * the embedding half of ``W_ih`` (teacher forcing) is one GEMM for all t;
+  * ``fc`` (:279) is one (T*B) x D x V GEMM after the loop, dW_fc one GEMM;
+  * every weight gradient of the recurrent GEMMs is one GEMM over the stacked
+    per-step gradients after the loop.
+
+Per timestep there remain 5 launches forward (grouped h-GEMM, score, softmax +
+context + gate, x-GEMM, LSTM pointwise) and 5 backward. Per-step state is
+time-major ([t][b][...]); the returned predictions/alphas keep the reference's
+batch-major (B,T,V)/(B,T,P) layouts.
+
+Ragged captions follow the reference's ``batch_size_t = sum(l > t)`` rule
+(:261): rows b >= bt[t] produce zero predictions/alphas and no gradient.
+"""
+import math
+
+import torch
+
+from . import kernels as K
+from ._lib import CAPMI_A_KMAJOR as AK, CAPMI_A_MMAJOR as AMM, CAPMI_B_KROWS as BKR
+from ._lib import CAPMI_B_NMAJOR_W as BW
+
+E_DIM = 2048
+PNAMES = ["attention.enc_att.weight", "attention.enc_att.bias", "attention.dec_att.weight",
+          "attention.dec_att.bias", "attention.full_att.weight", "attention.full_att.bias",
+          "decode_step.weight_ih", "decode_step.weight_hh", "decode_step.bias_ih",
+          "decode_step.bias_hh", "h_lin.weight", "h_lin.bias", "c_lin.weight", "c_lin.bias",
+          "f_beta.weight", "f_beta.bias", "fc.weight", "fc.bias", "embedding.weight"]
+
+
+def _split(M, N, K_, tile, target=256, min_k=128):
+    """K-split so that tiles*split ~ target workgroups (each split keeps >= min_k of K)."""
+    t = K.tiles_for(M, N, tile)
+    if t >= target:
+        return 1
+    s = max(1, min(math.ceil(target / t), K_ // min_k))
+    return s
+
+
+class DecoderDims:
+    def __init__(self, B, T, L, P, A, D, M, V, E=E_DIM):
+        self.B, self.T, self.L, self.P, self.A, self.D, self.M, self.V, self.E = B, T, L, P, A, D, M, V, E
+        self.X = M + E
+        for name, v in (("A", A), ("D", D), ("M", M), ("E", E)):
+            if v % 4:
+                raise ValueError(f"capmi decoder needs {name} % 4 == 0 (got {v})")
+        if A > 1024:
+            raise ValueError("capmi decoder supports attention_dim <= 1024")
+        # split-K factors of the per-step (M = B) GEMMs
+        self.s_h = (_split(B, A, D, K.TILE_64), _split(B, E, D, K.TILE_64), _split(B, 4 * D, D, K.TILE_64))
+        self.s_x = _split(B, 4 * D, E, K.TILE_64)
+        self.s_dx = _split(B, E, 4 * D, K.TILE_64)
+        self.s_dh = (_split(B, D, 4 * D, K.TILE_64, 96), _split(B, D, E, K.TILE_64, 96),
+                     _split(B, D, A, K.TILE_64, 64))
+
+    def key(self):
+        return (self.B, self.T, self.L, self.P, self.A, self.D, self.M, self.V, self.E)
+
+
+class Workspace:
+    """All decoder buffers for one shape, allocated once (graph-capture friendly)."""
+
+    def __init__(self, dm, device):
+        B, T, P, A, D, M, V, E, X = dm.B, dm.T, dm.P, dm.A, dm.D, dm.M, dm.V, dm.E, dm.X
+        f = dict(device=device, dtype=torch.float32)
+        e = torch.empty
+        self.X = e(T, B, X, **f)
+        self.mean = e(B, E, **f)
+        self.H = e(T + 1, B, D, **f)
+        self.C = e(T + 1, B, D, **f)
+        self.ACT = e(T, B, 4 * D, **f)
+        self.AD = e(T, B, A, **f)
+        self.AWE = e(T, B, E, **f)
+        self.GATE = e(T, B, E, **f)
+        self.XEMB = e(T, B, 4 * D, **f)
+        self.ATT_ENC = e(B, P, A, **f)
+        self.score = e(B, P, **f)
+        s_a, s_g, s_hh = dm.s_h
+        self.P_ad = e(s_a, B, A, **f)
+        self.P_gate = e(s_g, B, E, **f)
+        self.P_hh = e(s_hh, B, 4 * D, **f)
+        self.P_x = e(dm.s_x, B, 4 * D, **f)
+        # backward
+        self.DHD = e(T, B, D, **f)
+        self.DG = e(T, B, 4 * D, **f)
+        self.DGP = e(T, B, E, **f)
+        self.DAD = e(T, B, A, **f)
+        self.DE = e(T, B, P, **f)
+        self.DALPHA = e(B, P, **f)
+        self.DC = e(2, B, D, **f)
+        self.P_dx = e(dm.s_dx, B, E, **f)
+        self.P_dh = e(sum(dm.s_dh), B, D, **f)
+        self.DH0 = e(B, D, **f)
+        self.DATT = e(B, P, A, **f)
+        nblk = K.att_enc_grad_blocks(B, P)
+        self.WF_PART = e(nblk, A, **f)
+        self.BF_PART = e(nblk, 1, **f)
+        # generic scratch: split-K slabs of the hoisted GEMMs and colsum work
+        self.scratch = e(max(8 * T * B * D, 32 * B * D, T * B * M, 256 * 128 * 128), **f)
+        self.work = e(max(K.colsum_work_size(T * B, V), K.colsum_work_size(B * P, A),
+                          K.colsum_work_size(T * B, 4 * D), K.colsum_work_size(T * B, E), 64), **f)
+
+
+class DecoderCore:
+    """Stateless apart from the per-shape workspace cache."""
+
+    def __init__(self):
+        self._ws = {}
+
+    def workspace(self, dm, device):
+        key = (dm.key(), str(device))
+        ws = self._ws.get(key)
+        if ws is None:
+            self._ws.clear()  # one live shape at a time keeps HBM use bounded
+            ws = Workspace(dm, device)
+            self._ws[key] = ws
+        return ws
+
+    # ------------------------------------------------------------------ helpers
+    @staticmethod
+    def _gemm_into(ws, out, ld_out, M, N, Kd, A, lda, B, ldb, amode, bmode, bias=None, bias2=None,
+                   tile=K.TILE_128, target=256, **kw):
+        """C = op(A) op(B) (+bias); split-K through ws.scratch + reduce when the tile grid is small."""
+        s = _split(M, N, Kd, tile, target, min_k=256)
+        if s > 1 and s * M * N > ws.scratch.numel():
+            s = max(1, ws.scratch.numel() // (M * N))
+        if s == 1:
+            K.gemm(K.problem(M, N, Kd, A, lda, B, ldb, out, ld_out, bias=bias, bias2=bias2, **kw),
+                   amode, bmode, tile)
+            return
+        K.gemm(K.problem(M, N, Kd, A, lda, B, ldb, ws.scratch, N, ksplit=s, c_split_stride=M * N, **kw),
+               amode, bmode, tile)
+        if bias2 is not None:
+            raise NotImplementedError
+        K.splitk_reduce(ws.scratch, s, M * N, M, N, N, out, ld_out, bias=bias)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, p, enc, caps, decode_lengths, *, dropout_p=0.0, training=False, seed=0):
+        """p: dict name->tensor (PNAMES). enc: (B,P,E) contiguous fp32. caps: (B,L) int64.
+        Returns (predictions (B,T,V), alphas (B,T,P), state)."""
+        B, P, E = enc.shape
+        L = caps.shape[1]
+        T = max(decode_lengths)
+        A = p["attention.enc_att.weight"].shape[0]
+        D = p["decode_step.weight_hh"].shape[1]
+        M = p["embedding.weight"].shape[1]
+        V = p["fc.weight"].shape[0]
+        dm = DecoderDims(B, T, L, P, A, D, M, V, E)
+        ws = self.workspace(dm, enc.device)
+        X = dm.X
+        bt = [sum(1 for l in decode_lengths if l > t) for t in range(T)]
+        ragged = any(b != B for b in bt)
+        bt_dev = torch.tensor(bt, dtype=torch.int32).to(enc.device, non_blocking=True) if ragged else None
+
+        W_ih = p["decode_step.weight_ih"]
+        # embeddings of the caption tokens -> X[:, :, :M]      (:247, :273)
+        K.embed_gather(p["embedding.weight"], caps, B, L, T, ws.X, X)
+        # init_hidden_state (:151-164)
+        K.mean_rows(enc, B, P, E, ws.mean)
+        sh = min(8, max(1, E // 256))
+        slab = ws.scratch[:2 * sh * B * D]
+        K.gemm([K.problem(B, D, E, ws.mean, E, p["h_lin.weight"], E, slab, D, ksplit=sh, c_split_stride=B * D),
+                K.problem(B, D, E, ws.mean, E, p["c_lin.weight"], E, slab[sh * B * D:], D, ksplit=sh,
+                          c_split_stride=B * D)], AK, BW, K.TILE_64)
+        K.splitk_reduce(slab, sh, B * D, B, D, D, ws.H[0], D, bias=p["h_lin.bias"])
+        K.splitk_reduce(slab[sh * B * D:], sh, B * D, B, D, D, ws.C[0], D, bias=p["c_lin.bias"])
+        # hoisted enc_att (:54) and the embedding half of the LSTM input GEMM
+        K.gemm(K.problem(B * P, A, E, enc, E, p["attention.enc_att.weight"], E, ws.ATT_ENC, A,
+                         bias=p["attention.enc_att.bias"]), AK, BW, K.TILE_128)
+        K.gemm(K.problem(T * B, 4 * D, M, ws.X, X, W_ih, X, ws.XEMB, 4 * D, bias=p["decode_step.bias_ih"],
+                         bias2=p["decode_step.bias_hh"]), AK, BW, K.TILE_128)
+
+        alphas = torch.empty(B, T, P, device=enc.device, dtype=torch.float32)
+        s_a, s_g, s_hh = dm.s_h
+        W_ih_awe = W_ih[:, M:]
+        wf = p["attention.full_att.weight"]
+        for t in range(T):
+            h = ws.H[t]
+            # att_dec (:55), f_beta (:270) and W_hh h (:277) share the input h: one grouped launch
+            K.gemm([K.problem(B, A, D, h, D, p["attention.dec_att.weight"], D, ws.P_ad, A, ksplit=s_a,
+                              c_split_stride=B * A),
+                    K.problem(B, E, D, h, D, p["f_beta.weight"], D, ws.P_gate, E, ksplit=s_g,
+                              c_split_stride=B * E),
+                    K.problem(B, 4 * D, D, h, D, p["decode_step.weight_hh"], D, ws.P_hh, 4 * D, ksplit=s_hh,
+                              c_split_stride=B * 4 * D)], AK, BW, K.TILE_64)
+            K.att_score_fwd(ws.ATT_ENC, ws.P_ad, s_a, B * A, p["attention.dec_att.bias"], wf,
+                            p["attention.full_att.bias"], B, P, A, ws.score, ws.AD[t])
+            K.att_softmax_ctx_fwd(ws.score, enc, B, P, E, bt[t], alphas[:, t], T * P, ws.AWE[t],
+                                  ws.P_gate, s_g, B * E, p["f_beta.bias"], ws.GATE[t], ws.X[t, :, M:], X)
+            K.gemm(K.problem(B, 4 * D, E, ws.X[t, :, M:], X, W_ih_awe, X, ws.P_x, 4 * D, ksplit=dm.s_x,
+                             c_split_stride=B * 4 * D), AK, BW, K.TILE_64)
+            K.lstm_cell_fwd(ws.P_x, dm.s_x, B * 4 * D, ws.XEMB[t], ws.P_hh, s_hh, B * 4 * D, ws.C[t], B, D,
+                            ws.H[t + 1], ws.C[t + 1], ws.ACT[t])
+
+        # dropout (:107,279) then the hoisted fc over all (t, b) rows
+        Hcur = ws.H[1:]
+        if training and dropout_p > 0:
+            Hd = torch.empty_like(Hcur)
+            K.dropout(Hcur, Hcur.numel(), dropout_p, seed, Hd)
+        else:
+            Hd = Hcur
+        preds = torch.empty(B, T, V, device=enc.device, dtype=torch.float32)
+        K.gemm(K.problem(T * B, V, D, Hd, D, p["fc.weight"], D, preds, T * V, c_r1=B, c_s2=V,
+                         bias=p["fc.bias"]), AK, BW, K.TILE_128)
+        if ragged:
+            K.mask_rows_tb(preds, bt_dev, T, B, V, T * V, B, V)
+        state = dict(dm=dm, ws=ws, enc=enc, caps=caps, bt=bt, bt_dev=bt_dev, ragged=ragged, alphas=alphas,
+                     Hd=Hd, dropout_p=dropout_p if training else 0.0, seed=seed)
+        return preds, alphas, state
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, p, st, grads, dpred, dpred_time_major=False, dreg=None, dalphas=None,
+                 need=None):
+        """Writes parameter gradients into ``grads`` (dict name->tensor, pre-allocated).
+
+        dpred: gradient of the (B,T,V) predictions (batch-major), or time-major (T*B, V)
+        when ``dpred_time_major``. dreg: (B,P) gradient added to every alphas[:, t]
+        (the fused regulariser). dalphas: (B,T,P) gradient of the alphas output
+        (generic autograd path). ``need``: names whose gradient is wanted (default: all
+        present in ``grads``)."""
+        dm, ws = st["dm"], st["ws"]
+        B, T, L, P, A, D, M, V, E, X = dm.B, dm.T, dm.L, dm.P, dm.A, dm.D, dm.M, dm.V, dm.E, dm.X
+        enc, bt = st["enc"], st["bt"]
+        need = set(grads) if need is None else set(need)
+        W_ih = p["decode_step.weight_ih"]
+        TB = T * B
+        if dpred_time_major:
+            ar = dict(a_r1=0, a_s2=0)
+            lda_p = V
+        else:
+            ar = dict(a_r1=B, a_s2=V)
+            lda_p = T * V
+        if st["ragged"] and not dpred_time_major:
+            # reference semantics: predictions of finished rows are constants (no gradient)
+            dpred = dpred.clone()
+            K.mask_rows_tb(dpred, st["bt_dev"], T, B, V, T * V, B, V)
+
+        # ---- fc (:279): dHd = dpred W_fc ; dW_fc = dpred^T Hd ; db_fc = colsum(dpred)
+        self._gemm_into(ws, ws.DHD, D, TB, D, V, dpred, lda_p, p["fc.weight"], D, AK, BKR, **ar)
+        if "fc.weight" in need:
+            K.gemm(K.problem(V, D, TB, dpred, lda_p, st["Hd"], D, grads["fc.weight"], D, **ar), AMM, BKR,
+                   K.TILE_128)
+        if "fc.bias" in need:
+            K.colsum(dpred, TB, V, V, grads["fc.bias"], ws.work)
+        if st["dropout_p"] > 0:
+            K.dropout(ws.DHD, ws.DHD.numel(), st["dropout_p"], st["seed"], ws.DHD)
+
+        # ---- backward through time
+        s_dh = dm.s_dh
+        S_dh = sum(s_dh)
+        W_ih_awe = W_ih[:, M:]
+        wf = p["attention.full_att.weight"]
+        cur = 0
+        for t in range(T - 1, -1, -1):
+            K.lstm_cell_bwd(ws.DHD[t], ws.P_dh, S_dh if t < T - 1 else 0, B * D,
+                            ws.DC[cur] if t < T - 1 else None, ws.ACT[t], ws.C[t], ws.C[t + 1], B, D, bt[t],
+                            ws.DG[t], ws.DC[cur ^ 1])
+            cur ^= 1
+            K.gemm(K.problem(B, E, 4 * D, ws.DG[t], 4 * D, W_ih_awe, X, ws.P_dx, E, ksplit=dm.s_dx,
+                             c_split_stride=B * E), AK, BKR, K.TILE_64)
+            K.att_ctx_bwd(ws.P_dx, dm.s_dx, B * E, ws.GATE[t], ws.AWE[t], enc, B, P, E, ws.DGP[t], ws.DALPHA)
+            if dalphas is not None:
+                dr, dr_ld = dalphas[:, t], T * P
+            elif dreg is not None:
+                dr, dr_ld = dreg, P
+            else:
+                dr, dr_ld = None, 0
+            K.att_score_bwd(ws.DALPHA, dr, dr_ld, st["alphas"][:, t], T * P, ws.ATT_ENC, ws.AD[t], wf, B, P,
+                            A, bt[t], ws.DE[t], ws.DAD[t])
+            o1, o2 = s_dh[0] * B * D, (s_dh[0] + s_dh[1]) * B * D
+            K.gemm([K.problem(B, D, 4 * D, ws.DG[t], 4 * D, p["decode_step.weight_hh"], D, ws.P_dh, D,
+                              ksplit=s_dh[0], c_split_stride=B * D),
+                    K.problem(B, D, E, ws.DGP[t], E, p["f_beta.weight"], D, ws.P_dh.view(-1)[o1:], D,
+                              ksplit=s_dh[1], c_split_stride=B * D),
+                    K.problem(B, D, A, ws.DAD[t], A, p["attention.dec_att.weight"], D,
+                              ws.P_dh.view(-1)[o2:], D, ksplit=s_dh[2], c_split_stride=B * D)],
+                   AK, BKR, K.TILE_64)
+        # dh0 / dc0 -> h_lin / c_lin (:162-163)
+        K.splitk_reduce(ws.P_dh, S_dh, B * D, B, D, D, ws.DH0, D)
+        dc0 = ws.DC[cur]
+        for nm, dd in (("h_lin", ws.DH0), ("c_lin", dc0)):
+            if nm + ".weight" in need:
+                K.gemm(K.problem(D, E, B, dd, D, ws.mean, E, grads[nm + ".weight"], E), AMM, BKR, K.TILE_128)
+            if nm + ".bias" in need:
+                K.colsum(dd, B, D, D, grads[nm + ".bias"], ws.work)
+
+        # ---- hoisted weight gradients over all t
+        Hprev = ws.H[:T]
+        if "decode_step.weight_ih" in need:
+            self._gemm_into(ws, grads["decode_step.weight_ih"], X, 4 * D, X, TB, ws.DG, 4 * D, ws.X, X, AMM, BKR)
+        if "decode_step.weight_hh" in need:
+            self._gemm_into(ws, grads["decode_step.weight_hh"], D, 4 * D, D, TB, ws.DG, 4 * D, Hprev, D, AMM, BKR)
+        if "decode_step.bias_ih" in need or "decode_step.bias_hh" in need:
+            tgt = grads.get("decode_step.bias_ih", grads.get("decode_step.bias_hh"))
+            K.colsum(ws.DG, TB, 4 * D, 4 * D, tgt, ws.work)
+            for nm in ("decode_step.bias_ih", "decode_step.bias_hh"):
+                if nm in need and grads[nm] is not tgt:
+                    grads[nm].copy_(tgt)
+        if "f_beta.weight" in need:
+            self._gemm_into(ws, grads["f_beta.weight"], D, E, D, TB, ws.DGP, E, Hprev, D, AMM, BKR)
+        if "f_beta.bias" in need:
+            K.colsum(ws.DGP, TB, E, E, grads["f_beta.bias"], ws.work)
+        if "attention.dec_att.weight" in need:
+            self._gemm_into(ws, grads["attention.dec_att.weight"], D, A, D, TB, ws.DAD, A, Hprev, D, AMM, BKR)
+        if "attention.dec_att.bias" in need:
+            K.colsum(ws.DAD, TB, A, A, grads["attention.dec_att.bias"], ws.work)
+        # d(att_enc) summed over t, full_att grads (:56-57), then enc_att grads (:54)
+        nblk = K.att_enc_grad(ws.DE, ws.ATT_ENC, ws.AD, wf, T, B, P, A, ws.DATT, ws.WF_PART, ws.BF_PART)
+        if "attention.full_att.weight" in need:
+            K.colsum(ws.WF_PART, nblk, A, A, grads["attention.full_att.weight"], ws.work)
+        if "attention.full_att.bias" in need:
+            K.colsum(ws.BF_PART, nblk, 1, 1, grads["attention.full_att.bias"], ws.work)
+        if "attention.enc_att.weight" in need:
+            self._gemm_into(ws, grads["attention.enc_att.weight"], E, A, E, B * P, ws.DATT, A, enc, E, AMM, BKR)
+        if "attention.enc_att.bias" in need:
+            K.colsum(ws.DATT, B * P, A, A, grads["attention.enc_att.bias"], ws.work)
+        # embedding (only when fine-tuned, Q8): dX_emb = DG W_ih[:, :M] -> scatter-add by token
+        if "embedding.weight" in need:
+            demb = grads["embedding.weight"]
+            demb.zero_()
+            dxe = ws.scratch[:TB * M].view(TB, M)
+            K.gemm(K.problem(TB, M, 4 * D, ws.DG, 4 * D, W_ih, X, dxe, M), AK, BKR, K.TILE_128)
+            K.embed_scatter_add(dxe, M, st["caps"], B, L, T, st["bt_dev"], M, demb)

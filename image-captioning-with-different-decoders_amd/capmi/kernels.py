@@ -1,0 +1,252 @@
+"""Thin Python wrappers over libcapmi's C ABI (one function per entry point).
+
+Shape/dtype/device validation happens here, before the call (include/capmi.h
+contract); every launch goes on ``torch.cuda.current_stream()``.
+"""
+import ctypes
+
+import torch
+
+from ._lib import (CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W, CAPMI_COLSUM_ROWS, CAPMI_TILE_128, CAPMI_TILE_64,
+                   GemmProblem, call, lib)
+
+F32 = torch.float32
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _cuda(*ts, dtype=F32):
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise ValueError("capmi kernels need device (HIP) tensors")
+        if dtype is not None and t.dtype != dtype:
+            raise TypeError(f"expected {dtype}, got {t.dtype}")
+
+
+# --------------------------------------------------------------------------------------
+# GEMM
+# --------------------------------------------------------------------------------------
+def problem(M, N, K, A, lda, B, ldb, C, ldc, *, a_r1=0, a_s2=0, c_r1=0, c_s2=0, ksplit=1,
+            c_split_stride=0, bias=None, bias2=None, alpha=1.0, alpha_ptr=None, beta=0.0,
+            relu=False, stats=None, conv=None, in_scale=None, in_shift=None):
+    """Build one ``capmi_gemm_problem``. A/B/C are tensors (or views) whose data_ptr is the
+    operand origin; ld* are element strides. ``conv`` = dict(N,H,W,Cin,KH,KW,stride,pad,Ho,Wo)."""
+    _cuda(A, B, C, bias, bias2, stats, in_scale, in_shift)
+    p = GemmProblem()
+    p.M, p.N, p.K, p.ksplit = int(M), int(N), int(K), int(ksplit)
+    p.A, p.lda, p.a_r1, p.a_s2 = ptr(A), int(lda), int(a_r1), int(a_s2)
+    p.B, p.ldb = ptr(B), int(ldb)
+    p.C, p.ldc, p.c_r1, p.c_s2, p.c_split_stride = ptr(C), int(ldc), int(c_r1), int(c_s2), int(c_split_stride)
+    p.bias, p.bias2 = ptr(bias), ptr(bias2)
+    p.alpha_ptr = ptr(alpha_ptr)
+    p.alpha, p.beta, p.relu = float(alpha), float(beta), int(bool(relu))
+    p.stats = ptr(stats)
+    if conv is not None:
+        p.cN, p.cH, p.cW, p.cCin = conv["N"], conv["H"], conv["W"], conv["Cin"]
+        p.cKH, p.cKW, p.cStride, p.cPad = conv["KH"], conv["KW"], conv["stride"], conv["pad"]
+        p.cHo, p.cWo = conv["Ho"], conv["Wo"]
+    p.in_scale, p.in_shift = ptr(in_scale), ptr(in_shift)
+    return p
+
+
+def gemm(problems, amode=CAPMI_A_KMAJOR, bmode=CAPMI_B_NMAJOR_W, tile=CAPMI_TILE_128):
+    if isinstance(problems, GemmProblem):
+        problems = [problems]
+    arr = (GemmProblem * len(problems))(*problems)
+    call("capmi_gemm", arr, len(problems), amode, bmode, tile, stream())
+
+
+def stat_tiles(M, tile=CAPMI_TILE_128):
+    return lib.capmi_gemm_stat_tiles(int(M), int(tile))
+
+
+def tiles_for(M, N, tile):
+    bm = 128 if tile == CAPMI_TILE_128 else 64
+    return ((M + bm - 1) // bm) * ((N + bm - 1) // bm)
+
+
+def splitk_reduce(inp, S, slab, rows, cols, ld_in, out, ld_out, bias=None):
+    _cuda(inp, out, bias)
+    call("capmi_splitk_reduce", ptr(inp), S, slab, rows, cols, ld_in, ptr(bias), ptr(out), ld_out,
+         stream())
+
+
+def colsum_work_size(rows, cols):
+    return max(1, (rows + CAPMI_COLSUM_ROWS - 1) // CAPMI_COLSUM_ROWS) * cols
+
+
+def colsum(inp, rows, cols, ld, out, work, scale=1.0, accumulate=False):
+    _cuda(inp, out, work)
+    assert work.numel() >= colsum_work_size(rows, cols)
+    call("capmi_colsum", ptr(inp), rows, cols, ld, scale, ptr(work), ptr(out), int(accumulate), stream())
+
+
+# --------------------------------------------------------------------------------------
+# encoder
+# --------------------------------------------------------------------------------------
+def conv_weight_pack(w, out):
+    _cuda(w, out)
+    co, ci, kh, kw = w.shape
+    assert w.is_contiguous() and out.numel() == w.numel()
+    call("capmi_conv_weight_pack", ptr(w), co, ci, kh, kw, ptr(out), stream())
+
+
+def bn_finalize(stats, tiles, C, count, gamma, beta, running_mean, running_var, momentum, eps,
+                scale, shift, save_mean=None, save_var=None):
+    _cuda(stats, gamma, beta, running_mean, running_var, scale, shift, save_mean, save_var)
+    call("capmi_bn_finalize", ptr(stats), tiles, C, count, ptr(gamma), ptr(beta), ptr(running_mean),
+         ptr(running_var), momentum, eps, ptr(scale), ptr(shift), ptr(save_mean), ptr(save_var),
+         stream())
+
+
+def bn_eval_params(gamma, beta, rm, rv, C, eps, scale, shift):
+    _cuda(gamma, beta, rm, rv, scale, shift)
+    call("capmi_bn_eval_params", ptr(gamma), ptr(beta), ptr(rm), ptr(rv), C, eps, ptr(scale), ptr(shift),
+         stream())
+
+
+def bn_add_relu(y, s, b, res, out, rows, C, res_scale=None, res_shift=None):
+    _cuda(y, s, b, res, out, res_scale, res_shift)
+    call("capmi_bn_add_relu", ptr(y), ptr(s), ptr(b), ptr(res), ptr(res_scale), ptr(res_shift),
+         ptr(out), rows, C, stream())
+
+
+def bn_relu_maxpool(y, s, b, out, N, H, W, C, Ho, Wo):
+    _cuda(y, s, b, out)
+    call("capmi_bn_relu_maxpool", ptr(y), ptr(s), ptr(b), ptr(out), N, H, W, C, Ho, Wo, stream())
+
+
+def adaptive_avgpool_nhwc(inp, N, H, W, C, OH, OW, out):
+    _cuda(inp, out)
+    call("capmi_adaptive_avgpool_nhwc", ptr(inp), N, H, W, C, OH, OW, ptr(out), stream())
+
+
+# --------------------------------------------------------------------------------------
+# decoder
+# --------------------------------------------------------------------------------------
+def embed_gather(emb, caps, B, L, T, out, ld_out):
+    _cuda(emb, dtype=None)
+    _cuda(out)
+    _cuda(caps, dtype=torch.int64)
+    assert emb.dtype in (torch.float32, torch.float64) and emb.is_contiguous() and caps.is_contiguous()
+    call("capmi_embed_gather", ptr(emb), int(emb.dtype == torch.float64), emb.shape[1], ptr(caps), B, L,
+         T, ptr(out), ld_out, stream())
+
+
+def mean_rows(enc, B, P, E, out):
+    _cuda(enc, out)
+    call("capmi_mean_rows", ptr(enc), B, P, E, ptr(out), stream())
+
+
+def att_score_fwd(att_enc, dec_part, S, dec_slab, bias_da, wf, bf, B, P, A, e, att_dec_out=None):
+    _cuda(att_enc, dec_part, bias_da, wf, bf, e, att_dec_out)
+    call("capmi_att_score_fwd", ptr(att_enc), ptr(dec_part), S, dec_slab, ptr(bias_da), ptr(wf),
+         ptr(bf), B, P, A, ptr(e), ptr(att_dec_out), stream())
+
+
+def att_softmax_ctx_fwd(e, enc, B, P, E, bt, alpha_out, alpha_ld_b, awe_out, gate_part=None, S=0,
+                        gate_slab=0, bias_fb=None, gate_out=None, x_out=None, ld_x=0):
+    _cuda(e, enc, alpha_out, awe_out, gate_part, bias_fb, gate_out, x_out)
+    call("capmi_att_softmax_ctx_fwd", ptr(e), ptr(enc), B, P, E, bt, ptr(alpha_out), alpha_ld_b,
+         ptr(awe_out), ptr(gate_part), S, gate_slab, ptr(bias_fb), ptr(gate_out), ptr(x_out), ld_x,
+         stream())
+
+
+def lstm_cell_fwd(part, S, slab, xemb, hh_part, S2, slab2, c_prev, B, D, h_out, c_out, act_out):
+    _cuda(part, xemb, hh_part, c_prev, h_out, c_out, act_out)
+    call("capmi_lstm_cell_fwd", ptr(part), S, slab, ptr(xemb), ptr(hh_part), S2, slab2, ptr(c_prev), B,
+         D, ptr(h_out), ptr(c_out), ptr(act_out), stream())
+
+
+def dropout(inp, n, p, seed, out):
+    _cuda(inp, out)
+    call("capmi_dropout", ptr(inp), n, float(p), int(seed) & ((1 << 64) - 1), ptr(out), stream())
+
+
+def mask_rows_tb(x, bt_dev, T, B, cols, ld, r1=0, s2=0):
+    _cuda(x)
+    _cuda(bt_dev, dtype=torch.int32)
+    call("capmi_mask_rows_tb", ptr(x), ptr(bt_dev), T, B, cols, ld, r1, s2, stream())
+
+
+def ce_fwd_bwd(logits, caps, B, T, L, V, bt_dev, nrows, loss_rows, lse=None, dlogits=None,
+               dl_time_major=False, gscale=None):
+    _cuda(logits, loss_rows, lse, dlogits, gscale)
+    _cuda(caps, dtype=torch.int64)
+    _cuda(bt_dev, dtype=torch.int32)
+    call("capmi_ce_fwd_bwd", ptr(logits), ptr(caps), B, T, L, V, ptr(bt_dev), nrows, ptr(loss_rows),
+         ptr(lse), ptr(dlogits), int(dl_time_major), ptr(gscale), stream())
+
+
+def alpha_reg(alphas, B, T, P, alpha_c, reg, dreg):
+    _cuda(alphas, reg, dreg)
+    call("capmi_alpha_reg", ptr(alphas), B, T, P, float(alpha_c), ptr(reg), ptr(dreg), stream())
+
+
+def loss_finalize(loss_rows, n, nrows, reg, out):
+    _cuda(loss_rows, reg, out)
+    call("capmi_loss_finalize", ptr(loss_rows), n, nrows, ptr(reg), ptr(out), stream())
+
+
+def lstm_cell_bwd(dhd, dh_part, S, slab, dc_in, act, c_prev, c_cur, B, D, bt, dgates, dc_out):
+    _cuda(dhd, dh_part, dc_in, act, c_prev, c_cur, dgates, dc_out)
+    call("capmi_lstm_cell_bwd", ptr(dhd), ptr(dh_part), S, slab, ptr(dc_in), ptr(act), ptr(c_prev),
+         ptr(c_cur), B, D, bt, ptr(dgates), ptr(dc_out), stream())
+
+
+def att_ctx_bwd(part, S, slab, gate, awe, enc, B, P, E, dgp, dalpha):
+    _cuda(part, gate, awe, enc, dgp, dalpha)
+    call("capmi_att_ctx_bwd", ptr(part), S, slab, ptr(gate), ptr(awe), ptr(enc), B, P, E, ptr(dgp),
+         ptr(dalpha), stream())
+
+
+def att_score_bwd(dalpha, dreg, dreg_ld_b, alpha, alpha_ld_b, att_enc, att_dec, wf, B, P, A, bt, de,
+                  dad):
+    _cuda(dalpha, dreg, alpha, att_enc, att_dec, wf, de, dad)
+    call("capmi_att_score_bwd", ptr(dalpha), ptr(dreg), dreg_ld_b, ptr(alpha), alpha_ld_b, ptr(att_enc),
+         ptr(att_dec), ptr(wf), B, P, A, bt, ptr(de), ptr(dad), stream())
+
+
+def att_enc_grad(de, att_enc, att_dec, wf, T, B, P, A, datt_enc, wf_part, bf_part):
+    _cuda(de, att_enc, att_dec, wf, datt_enc, wf_part, bf_part)
+    n = ctypes.c_int(0)
+    call("capmi_att_enc_grad", ptr(de), ptr(att_enc), ptr(att_dec), ptr(wf), T, B, P, A, ptr(datt_enc),
+         ptr(wf_part), ptr(bf_part), ctypes.byref(n), stream())
+    return n.value
+
+
+def att_enc_grad_blocks(B, P):
+    return ((P + 27) // 28) * B
+
+
+# --------------------------------------------------------------------------------------
+# optimiser
+# --------------------------------------------------------------------------------------
+def adam_clamp(p, g, m, v, lr, beta1, beta2, eps, bc1, bc2_sqrt, clip):
+    if p.dtype == torch.float64:
+        _cuda(p, g, m, v, dtype=torch.float64)
+        call("capmi_adam_clamp_f64", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, beta1, beta2, eps,
+             bc1, bc2_sqrt, clip, stream())
+    else:
+        _cuda(p, g, m, v)
+        call("capmi_adam_clamp", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, beta1, beta2, eps, bc1,
+             bc2_sqrt, clip, stream())
+
+
+def embed_scatter_add(dx, ld_dx, caps, B, L, T, bt_dev, M, demb):
+    _cuda(dx)
+    _cuda(caps, dtype=torch.int64)
+    _cuda(demb, dtype=None)
+    call("capmi_embed_scatter_add", ptr(dx), ld_dx, ptr(caps), B, L, T, ptr(bt_dev), M, ptr(demb),
+         int(demb.dtype == torch.float64), stream())
+
+
+TILE_128, TILE_64 = CAPMI_TILE_128, CAPMI_TILE_64

@@ -1,0 +1,102 @@
+"""Adam with the reference's element-wise gradient clamp fused in (one kernel per dtype).
+
+Drop-in for ``torch.optim.Adam(params, lr=...)`` as used at models/attention.py:352-355
+(defaults: betas (0.9, 0.999), eps 1e-8, no weight decay) followed by
+``clip_gradient(optimizer, grad_clip)`` (train_utils.py:2-12): ``clip_gradient``
+records the bound, ``step()`` clamps and updates in one pass.
+
+Parameters (and their ``.grad``) are re-homed into one flat buffer per dtype
+(fp32, plus fp64 for a GloVe table, Q7), so the data-parallel all-reduce and the
+update each touch one contiguous buffer. The modules keep their Parameters
+(same objects, same names/shapes); only their storage moves.
+"""
+import math
+
+import torch
+
+from . import kernels as K
+
+
+class Adam:
+    fused_clamp = True
+
+    def __init__(self, params, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0):
+        if weight_decay:
+            raise ValueError("capmi Adam: weight decay is not used by the reference")
+        params = [p for p in params]
+        if not params:
+            raise ValueError("optimizer got an empty parameter list")  # same as torch (Q9)
+        self.param_groups = [{"params": params, "lr": lr, "betas": betas, "eps": eps,
+                              "weight_decay": 0, "amsgrad": False}]
+        self.clip = math.inf
+        self.step_count = 0
+        self.flats = []  # (dtype, p_flat, g_flat, m, v, [(param, offset, numel)])
+        for dt in sorted({p.dtype for p in params}, key=str):
+            ps = [p for p in params if p.dtype == dt]
+            n = sum(p.numel() for p in ps)
+            dev = ps[0].device
+            pf = torch.empty(n, device=dev, dtype=dt)
+            gf = torch.zeros(n, device=dev, dtype=dt)
+            layout, off = [], 0
+            for p in ps:
+                k = p.numel()
+                pf[off:off + k].copy_(p.detach().reshape(-1))
+                p.data = pf[off:off + k].view_as(p)
+                p.grad = gf[off:off + k].view_as(p)
+                layout.append((p, off, k))
+                off += k
+            self.flats.append([dt, pf, gf, torch.zeros_like(pf), torch.zeros_like(pf), layout])
+
+    # ------------------------------------------------------------------
+    def set_clip(self, c):
+        self.clip = float(c)
+
+    def grad_buffers(self):
+        return [f[2] for f in self.flats]
+
+    def zero_grad(self, set_to_none=False):
+        for f in self.flats:
+            f[2].zero_()
+            for p, off, k in f[5]:
+                p.grad = f[2][off:off + k].view_as(p)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        self.step_count += 1
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        t = self.step_count
+        bc1 = 1 - b1 ** t
+        bc2s = math.sqrt(1 - b2 ** t)
+        clip = self.clip if math.isfinite(self.clip) else 3.0e38
+        for dt, pf, gf, m, v, _ in self.flats:
+            K.adam_clamp(pf, gf, m, v, g["lr"], b1, b2, g["eps"], bc1, bc2s, clip)
+
+    # ---- torch.optim.Adam-compatible state dict --------------------------
+    def state_dict(self):
+        state = {}
+        i = 0
+        for dt, pf, gf, m, v, layout in self.flats:
+            for p, off, k in layout:
+                state[i] = {"step": torch.tensor(float(self.step_count)),
+                            "exp_avg": m[off:off + k].view_as(p).clone(),
+                            "exp_avg_sq": v[off:off + k].view_as(p).clone()}
+                i += 1
+        g = dict(self.param_groups[0])
+        g["params"] = list(range(i))
+        return {"state": state, "param_groups": [g]}
+
+    def load_state_dict(self, sd):
+        i = 0
+        for dt, pf, gf, m, v, layout in self.flats:
+            for p, off, k in layout:
+                st = sd["state"].get(i)
+                if st is not None:
+                    m[off:off + k].copy_(st["exp_avg"].reshape(-1))
+                    v[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+                    self.step_count = int(float(st["step"]))
+                i += 1
+        pg = sd["param_groups"][0]
+        for key in ("lr", "betas", "eps"):
+            if key in pg:
+                self.param_groups[0][key] = pg[key]

@@ -1,0 +1,258 @@
+"""ResNet-101 (torchvision layout) with a fused MI355X forward.
+
+The module tree mirrors torchvision.models.resnet101 exactly (names, children()
+order: conv1, bn1, relu, maxpool, layer1..4, avgpool, fc), so the reference's
+``list(resnet.children())[:-2]`` / ``[:-1]`` slicing (models/encoder.py:38,90)
+and its state-dict keys (a local ``resnet101.pth``) mean the same thing here.
+
+On a HIP device, ``fused_forward`` runs the conv stack through libcapmi:
+every Conv2d is an implicit GEMM on fp32 MFMA over NHWC activations; the
+BatchNorm that follows it is split into (a) batch statistics accumulated in
+the conv GEMM's epilogue, (b) a tiny finalize kernel (mean/var -> scale/shift,
+running-stat update in train mode) and (c) the apply+ReLU, fused into the next
+conv's A-tile load or into the bottleneck tail kernel (BN + residual + ReLU).
+On CPU tensors the modules run their ordinary nn forward (config 1 plumbing).
+"""
+import torch
+import torch.nn as nn
+
+from . import kernels as K
+from ._lib import CAPMI_A_CONV_NCHW, CAPMI_A_CONV_NHWC, CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, width, stride=1, downsample=False):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = nn.Conv2d(width, width * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(width * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = None
+        if downsample:
+            self.downsample = nn.Sequential(nn.Conv2d(cin, width * 4, 1, stride=stride, bias=False),
+                                            nn.BatchNorm2d(width * 4))
+        self.stride = stride
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        y = self.relu(self.bn1(self.conv1(x)))
+        y = self.relu(self.bn2(self.conv2(y)))
+        return self.relu(self.bn3(self.conv3(y)) + idt)
+
+
+class ResNet101(nn.Module):
+    def __init__(self, layers=(3, 4, 23, 3), num_classes=1000):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        cin = 64
+        for i, (n, w, s) in enumerate(zip(layers, (64, 128, 256, 512), (1, 2, 2, 2))):
+            blocks = []
+            for b in range(n):
+                blocks.append(Bottleneck(cin, w, s if b == 0 else 1, downsample=(b == 0)))
+                cin = w * 4
+            setattr(self, f"layer{i + 1}", nn.Sequential(*blocks))
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(2048, num_classes)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        """torchvision's init: kaiming_normal_(fan_out, relu) convs, BN weight 1 / bias 0."""
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+
+    def forward(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        return self.fc(torch.flatten(self.avgpool(x), 1))
+
+
+def resnet101(weights_path=None):
+    """Seeded-random ResNet-101 (torch RNG), or the weights of a local torchvision
+    checkpoint (``weights_path``, loaded with weights_only=True). Never downloads."""
+    m = ResNet101()
+    if weights_path is not None:
+        m.load_state_dict(torch.load(weights_path, map_location="cpu", weights_only=True))
+    return m
+
+
+# ======================================================================================
+# fused forward
+# ======================================================================================
+class _Packed:
+    """Conv weights in the GEMM's B layout: [Cout][KH][KW][Cin] (K-contiguous)."""
+
+    def __init__(self):
+        self.cache = {}
+
+    def get(self, conv):
+        w = conv.weight
+        co, ci, kh, kw = w.shape
+        if kh == 1 and kw == 1:
+            return w  # [Cout][Cin] already
+        if ci % 16:  # conv1 (Cin = 3): consumed in its native [Cout][Cin][KH][KW] order
+            return w
+        key = id(conv)
+        ent = self.cache.get(key)
+        if ent is None or ent[0] != w._version or ent[1] != w.data_ptr():
+            packed = torch.empty(co, kh, kw, ci, device=w.device, dtype=w.dtype)
+            K.conv_weight_pack(w.detach().contiguous(), packed)
+            ent = (w._version, w.data_ptr(), packed)
+            self.cache[key] = ent
+        return ent[2]
+
+
+class EncoderRunner:
+    """Launch plan for the frozen ResNet-101 conv stack (children()[:-2] of torchvision's
+    resnet101) on NHWC fp32 activations. Buffers are cached per input shape."""
+
+    def __init__(self):
+        self.packed = _Packed()
+        self._ws = None
+        self._ws_key = None
+        self.conv_hook = None  # optional callable(tag, fn) wrapping each conv launch (bench timing)
+
+    def _workspace(self, N, H, W, device):
+        key = (N, H, W, str(device))
+        if self._ws_key != key:
+            H1, W1 = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+            big = N * H1 * W1 * 64  # conv1 output; layer1 outputs are N*(H1/2)^2*256 = same
+            big = max(big, N * ((H1 + 1) // 2) * ((W1 + 1) // 2) * 256)
+            f = dict(device=device, dtype=torch.float32)
+            ws = {n: torch.empty(big, **f) for n in ("x", "y1", "y2", "y3", "yd", "out")}
+            ws["stats"] = torch.empty(2 * ((N * H1 * W1 + 127) // 128) * 256, **f)
+            ws["ss"] = {}
+            self._ws, self._ws_key = ws, key
+        return self._ws
+
+    def _ss(self, ws, bn):
+        ent = ws["ss"].get(id(bn))
+        if ent is None:
+            C = bn.num_features
+            ent = torch.empty(2, C, device=bn.weight.device, dtype=torch.float32)
+            ws["ss"][id(bn)] = ent
+        return ent[0], ent[1]
+
+    def _bn(self, ws, bn, rows, train):
+        """BatchNorm params for the conv output just produced: batch stats (train) or running."""
+        s, b = self._ss(ws, bn)
+        C = bn.num_features
+        if train:
+            tiles = K.stat_tiles(rows, K.TILE_128)
+            mom = 0.1 if bn.momentum is None else bn.momentum
+            K.bn_finalize(ws["stats"], tiles, C, rows, bn.weight, bn.bias,
+                          bn.running_mean if bn.track_running_stats else None,
+                          bn.running_var if bn.track_running_stats else None, mom, bn.eps, s, b)
+        else:
+            K.bn_eval_params(bn.weight, bn.bias, bn.running_mean, bn.running_var, C, bn.eps, s, b)
+        return s, b
+
+    def _conv(self, tag, x, conv, out, N, H, W, train, in_ss=None, nchw=False):
+        co, ci, kh, kw = conv.weight.shape
+        st, pd = conv.stride[0], conv.padding[0]
+        Ho, Wo = (H + 2 * pd - kh) // st + 1, (W + 2 * pd - kw) // st + 1
+        rows = N * Ho * Wo
+        Kd = ci * kh * kw
+        w = self.packed.get(conv)
+        geo = dict(N=N, H=H, W=W, Cin=ci, KH=kh, KW=kw, stride=st, pad=pd, Ho=Ho, Wo=Wo)
+        stats = ws_stats = self._ws["stats"] if train else None
+        kw_ = dict(stats=ws_stats)
+        if nchw:
+            prob = K.problem(rows, co, Kd, x, 0, w, Kd, out, co, conv=geo, **kw_)
+            mode = CAPMI_A_CONV_NCHW
+        elif kh == 1 and st == 1 and in_ss is None:
+            prob = K.problem(rows, co, Kd, x, ci, w, Kd, out, co, **kw_)
+            mode = CAPMI_A_KMAJOR
+        else:
+            sc, sh = in_ss if in_ss is not None else (None, None)
+            prob = K.problem(rows, co, Kd, x, 0, w, Kd, out, co, conv=geo, in_scale=sc, in_shift=sh, **kw_)
+            mode = CAPMI_A_CONV_NHWC
+        launch = lambda: K.gemm(prob, mode, CAPMI_B_NMAJOR_W, K.TILE_128)  # noqa: E731
+        if self.conv_hook is not None:
+            self.conv_hook(tag, 2.0 * rows * co * Kd, launch)
+        else:
+            launch()
+        del stats
+        return Ho, Wo, rows
+
+    @torch.no_grad()
+    def forward(self, net, imgs, out_hw=(14, 14), train=True, out=None):
+        """imgs (N,3,H,W) fp32 contiguous on the device -> (N, OH, OW, 2048) NHWC (= the
+        reference's adaptive_pool + permute(0,2,3,1), models/encoder.py:107-110)."""
+        if imgs.dtype != torch.float32 or not imgs.is_contiguous():
+            raise TypeError("encoder input must be contiguous float32 (N,3,H,W)")
+        N, C0, H, W = imgs.shape
+        ws = self._workspace(N, H, W, imgs.device)
+        # conv1 7x7/2 -> bn1 -> relu -> maxpool (children 0-3)
+        H1, W1, rows = self._conv("conv1", imgs, net.conv1, ws["y1"], N, H, W, train, nchw=True)
+        s, b = self._bn(ws, net.bn1, rows, train)
+        Hp, Wp = (H1 + 2 - 3) // 2 + 1, (W1 + 2 - 3) // 2 + 1
+        K.bn_relu_maxpool(ws["y1"], s, b, ws["x"], N, H1, W1, 64, Hp, Wp)
+        x, xo = ws["x"], ws["out"]
+        H, W, Cx = Hp, Wp, 64
+        bns = []
+        for li in range(1, 5):
+            for bi, blk in enumerate(getattr(net, f"layer{li}")):
+                tag = f"layer{li}.{bi}"
+                _, _, r1 = self._conv(tag + ".conv1", x, blk.conv1, ws["y1"], N, H, W, train)
+                ss1 = self._bn(ws, blk.bn1, r1, train)
+                H2, W2, r2 = self._conv(tag + ".conv2", ws["y1"], blk.conv2, ws["y2"], N, H, W, train, in_ss=ss1)
+                ss2 = self._bn(ws, blk.bn2, r2, train)
+                _, _, r3 = self._conv(tag + ".conv3", ws["y2"], blk.conv3, ws["y3"], N, H2, W2, train, in_ss=ss2)
+                s3, b3 = self._bn(ws, blk.bn3, r3, train)
+                Cout = blk.conv3.out_channels
+                if blk.downsample is not None:
+                    self._conv(tag + ".downsample", x, blk.downsample[0], ws["yd"], N, H, W, train)
+                    sd, bd = self._bn(ws, blk.downsample[1], r3, train)
+                    K.bn_add_relu(ws["y3"], s3, b3, ws["yd"], xo, r3, Cout, res_scale=sd, res_shift=bd)
+                    bns.append(blk.downsample[1])
+                else:
+                    K.bn_add_relu(ws["y3"], s3, b3, x, xo, r3, Cout)
+                bns += [blk.bn1, blk.bn2, blk.bn3]
+                x, xo = xo, x
+                H, W, Cx = H2, W2, Cout
+        if train:
+            bns.append(net.bn1)
+            nbt = [m.num_batches_tracked for m in bns if m.num_batches_tracked is not None]
+            if nbt:
+                torch._foreach_add_(nbt, 1)
+        OH, OW = out_hw
+        if out is None:
+            out = torch.empty(N, OH, OW, Cx, device=imgs.device, dtype=torch.float32)
+        K.adaptive_avgpool_nhwc(x, N, H, W, Cx, OH, OW, out)
+        return out
+
+
+def conv_flops_per_image(net, H=224, W=224):
+    """Algorithmic FLOPs of the conv stack for one image (2*Ho*Wo*Cout*Cin*KH*KW summed)."""
+    tot = 0
+    h, w = H, W
+    convs = [net.conv1]
+    c = net.conv1
+    h, w = (h + 6 - 7) // 2 + 1, (w + 6 - 7) // 2 + 1
+    tot += 2 * h * w * c.out_channels * c.in_channels * 49
+    h, w = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1
+    for li in range(1, 5):
+        for blk in getattr(net, f"layer{li}"):
+            tot += 2 * h * w * blk.conv1.out_channels * blk.conv1.in_channels
+            s = blk.conv2.stride[0]
+            h2, w2 = (h + 2 - 3) // s + 1, (w + 2 - 3) // s + 1
+            tot += 2 * h2 * w2 * blk.conv2.out_channels * blk.conv2.in_channels * 9
+            tot += 2 * h2 * w2 * blk.conv3.out_channels * blk.conv3.in_channels
+            if blk.downsample is not None:
+                d = blk.downsample[0]
+                tot += 2 * h2 * w2 * d.out_channels * d.in_channels
+            h, w = h2, w2
+    del convs
+    return tot

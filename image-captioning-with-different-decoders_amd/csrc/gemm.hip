@@ -1,0 +1,494 @@
+// fp32 MFMA GEMM and implicit-GEMM convolution for gfx950.
+//
+// One kernel template serves every dense contraction of the training step:
+//   * nn.Linear forward / dX / dW (models/attention.py:33-35,54-55,110-114,162-163,270,279)
+//   * LSTMCell gate GEMMs (models/attention.py:108-109,277-278)
+//   * all 104 Conv2d of torchvision ResNet-101 (models/encoder.py:88-91,107) as implicit
+//     GEMMs over NHWC activations (k = (kh, kw, ci)), with the previous layer's
+//     BatchNorm-apply + ReLU fused into the A-tile load and the BatchNorm(train)
+//     batch statistics fused into the epilogue.
+//
+// Exact fp32: v_mfma_f32_32x32x2_f32 (gfx950 has no xf32); each 32x32 accumulator is a
+// k-ordered fmaf chain. Tiles: 128x128x16 (4 waves of 64x64) for large problems,
+// 64x64x16 (4 waves of 32x32) for the per-timestep decoder GEMMs (M = batch), which
+// rely on split-K for parallelism; split partial slabs are summed by the consumer.
+// Global->LDS staging is register-double-buffered: tile t+1 is loaded into registers
+// while tile t is multiplied out of LDS, one barrier per K-tile.
+#include "common.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct GemmArgs {
+  capmi_gemm_problem p[CAPMI_MAX_GROUP];
+  int tiles_begin[CAPMI_MAX_GROUP + 1];
+  int tiles_m[CAPMI_MAX_GROUP];
+  int tiles_n[CAPMI_MAX_GROUP];
+  int kchunk[CAPMI_MAX_GROUP];
+  int nprob;
+};
+
+constexpr int BK = 16;
+
+__device__ __forceinline__ long long remap(long long r, long long r1, long long ld, long long s2) {
+  return r1 > 0 ? (r % r1) * ld + (r / r1) * s2 : r * ld;
+}
+
+template <int AMODE> struct APad { static constexpr int v = 2; };
+template <> struct APad<1> { static constexpr int v = 4; };
+template <> struct APad<3> { static constexpr int v = 4; };
+template <int BMODE> struct BPad { static constexpr int v = 2; };
+template <> struct BPad<1> { static constexpr int v = 4; };
+
+// load 4 consecutive elements p[0..3] of which `n` (0..4) are in bounds
+template <bool VEC>
+__device__ __forceinline__ float4 load4(const float* p, int n) {
+  if (VEC) {
+    return n > 0 ? *reinterpret_cast<const float4*>(p) : make_float4(0.f, 0.f, 0.f, 0.f);
+  } else {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (n > 0) v.x = p[0];
+    if (n > 1) v.y = p[1];
+    if (n > 2) v.z = p[2];
+    if (n > 3) v.w = p[3];
+    return v;
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int AMODE, int BMODE, bool VEC>
+__global__ void __launch_bounds__(256) gemm_kernel(const GemmArgs args) {
+  constexpr int NWN = BN / WN;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int SA = BM + APad<AMODE>::v;
+  constexpr int SB = BN + BPad<BMODE>::v;
+  // A slots per thread per K-tile: float4 slots for modes 0-2, scalars for mode 3
+  constexpr int NA = (AMODE == 3) ? (BM * BK / 256) : (BM * BK / 4 / 256);
+  constexpr int NB = BN * BK / 4 / 256;
+  static_assert(NA >= 1 && NB >= 1, "tile too small");
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
+
+  __shared__ __attribute__((aligned(16))) float As[2][BK][SA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][SB];
+  __shared__ float red[4][2][32 * TN];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm0 = (wid / NWN) * WM, wn0 = (wid % NWN) * WN;
+
+  int bid = blockIdx.x, pi = 0;
+  while (pi + 1 < args.nprob && bid >= args.tiles_begin[pi + 1]) ++pi;
+  const capmi_gemm_problem& P = args.p[pi];
+  const int local = bid - args.tiles_begin[pi];
+  const int tiles_n = args.tiles_n[pi], tiles_m = args.tiles_m[pi];
+  const int tn = local % tiles_n;
+  const int tm = (local / tiles_n) % tiles_m;
+  const int z = local / (tiles_n * tiles_m);
+  const int M = P.M, N = P.N, K = P.K;
+  const int k_begin = z * args.kchunk[pi];
+  const int k_end = min(K, k_begin + args.kchunk[pi]);
+  const int nkt = k_end > k_begin ? (k_end - k_begin + BK - 1) / BK : 0;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- per-thread A-row precompute --------------------------------------------------
+  const float* a_ptr[NA];
+  int a_ih0[NA], a_iw0[NA];
+  bool a_ok[NA];
+  int a_kk[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int f = tid + i * 256;
+    if (AMODE == 0 || AMODE == 2) {
+      const int row = m0 + (f >> 2);
+      a_kk[i] = (f & 3) * 4;
+      a_ok[i] = row < M;
+      if (AMODE == 0) {
+        a_ptr[i] = P.A + (a_ok[i] ? remap(row, P.a_r1, P.lda, P.a_s2) : 0);
+      } else {
+        const int hw = P.cHo * P.cWo;
+        const int n = row / hw, rem = row - n * hw;
+        const int oh = rem / P.cWo, ow = rem - oh * P.cWo;
+        a_ih0[i] = oh * P.cStride - P.cPad;
+        a_iw0[i] = ow * P.cStride - P.cPad;
+        a_ptr[i] = P.A + (long long)n * P.cH * P.cW * P.cCin;
+      }
+    } else if (AMODE == 1) {
+      a_kk[i] = f / (BM / 4);
+      const int m = m0 + (f % (BM / 4)) * 4;
+      a_ok[i] = m < M;
+      a_ptr[i] = P.A + m;
+      a_ih0[i] = min(4, M - m);
+    } else {  // AMODE 3: scalar gather, r = f % BM, kk = f / BM
+      const int row = m0 + (f % BM);
+      a_kk[i] = f / BM;
+      a_ok[i] = row < M;
+      const int hw = P.cHo * P.cWo;
+      const int n = row / hw, rem = row - n * hw;
+      const int oh = rem / P.cWo, ow = rem - oh * P.cWo;
+      a_ih0[i] = oh * P.cStride - P.cPad;
+      a_iw0[i] = ow * P.cStride - P.cPad;
+      a_ptr[i] = P.A + (long long)n * P.cCin * P.cH * P.cW;
+    }
+  }
+  // ---- per-thread B precompute ----------------------------------------------------
+  const float* b_ptr[NB];
+  int b_kk[NB], b_nv[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int f = tid + i * 256;
+    if (BMODE == 0) {
+      const int n = n0 + (f >> 2);
+      b_kk[i] = (f & 3) * 4;
+      b_nv[i] = n < N;
+      b_ptr[i] = P.B + (n < N ? (long long)n * P.ldb : 0);
+    } else {
+      b_kk[i] = f / (BN / 4);
+      const int n = n0 + (f % (BN / 4)) * 4;
+      b_nv[i] = max(0, min(4, N - n));
+      b_ptr[i] = P.B + (n < N ? n : 0);
+    }
+  }
+
+  float4 ra[NA];
+  float rs[NA];  // scalar staging for AMODE 3
+  float4 rb[NB];
+
+  auto load_tile = [&](int kt) {
+    const int k0 = k_begin + kt * BK;
+    if (AMODE == 0) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int k = k0 + a_kk[i];
+        const int nv = a_ok[i] ? max(0, min(4, k_end - k)) : 0;
+        ra[i] = load4<VEC>(a_ptr[i] + k, nv);
+      }
+    } else if (AMODE == 1) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int k = k0 + a_kk[i];
+        const bool ok = a_ok[i] && k < k_end;
+        ra[i] = load4<VEC>(a_ptr[i] + (ok ? remap(k, P.a_r1, P.lda, P.a_s2) : 0), ok ? a_ih0[i] : 0);
+      }
+    } else if (AMODE == 2) {
+      const int kpos = k0 / P.cCin;
+      const int ci0 = k0 - kpos * P.cCin;
+      const int kh = kpos / P.cKW, kw = kpos - kh * P.cKW;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
+        const bool ok = a_ok[i] && k0 < k_end && ih >= 0 && ih < P.cH && iw >= 0 && iw < P.cW;
+        const int ci = ci0 + a_kk[i];
+        float4 v = load4<true>(a_ptr[i] + ((long long)ih * P.cW + iw) * P.cCin + ci, ok ? 4 : 0);
+        if (P.in_scale != nullptr && ok) {
+          const float4 sc = *reinterpret_cast<const float4*>(P.in_scale + ci);
+          const float4 sh = *reinterpret_cast<const float4*>(P.in_shift + ci);
+          v = relu4(fma4(v, sc, sh));
+        }
+        ra[i] = v;
+      }
+    } else {  // AMODE 3
+      const int khw = P.cKH * P.cKW;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int k = k0 + a_kk[i];
+        float v = 0.f;
+        if (a_ok[i] && k < k_end) {
+          const int ci = k / khw, rem = k - ci * khw;
+          const int kh = rem / P.cKW, kw = rem - kh * P.cKW;
+          const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
+          if (ih >= 0 && ih < P.cH && iw >= 0 && iw < P.cW) {
+            v = a_ptr[i][((long long)ci * P.cH + ih) * P.cW + iw];
+            if (P.in_scale != nullptr) v = fmaxf(fmaf(v, P.in_scale[ci], P.in_shift[ci]), 0.f);
+          }
+        }
+        rs[i] = v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int k = k0 + b_kk[i];
+      if (BMODE == 0) {
+        const int nv = b_nv[i] ? max(0, min(4, k_end - k)) : 0;
+        rb[i] = load4<VEC>(b_ptr[i] + k, nv);
+      } else {
+        const bool ok = k < k_end;
+        rb[i] = load4<VEC>(b_ptr[i] + (ok ? (long long)k * P.ldb : 0), ok ? b_nv[i] : 0);
+      }
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int f = tid + i * 256;
+      if (AMODE == 0 || AMODE == 2) {
+        const int r = f >> 2, kq = a_kk[i];
+        As[buf][kq + 0][r] = ra[i].x;
+        As[buf][kq + 1][r] = ra[i].y;
+        As[buf][kq + 2][r] = ra[i].z;
+        As[buf][kq + 3][r] = ra[i].w;
+      } else if (AMODE == 1) {
+        *reinterpret_cast<float4*>(&As[buf][a_kk[i]][(f % (BM / 4)) * 4]) = ra[i];
+      } else {
+        As[buf][a_kk[i]][f % BM] = rs[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int f = tid + i * 256;
+      if (BMODE == 0) {
+        const int r = f >> 2, kq = b_kk[i];
+        Bs[buf][kq + 0][r] = rb[i].x;
+        Bs[buf][kq + 1][r] = rb[i].y;
+        Bs[buf][kq + 2][r] = rb[i].z;
+        Bs[buf][kq + 3][r] = rb[i].w;
+      } else {
+        *reinterpret_cast<float4*>(&Bs[buf][b_kk[i]][(f % (BN / 4)) * 4]) = rb[i];
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int lr = lane & 31, lk = lane >> 5;
+  if (nkt > 0) {
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nkt) load_tile(kt + 1);
+#pragma unroll
+      for (int kk = 0; kk < BK / 2; ++kk) {
+        float a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = As[buf][2 * kk + lk][wm0 + 32 * i + lr];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = Bs[buf][2 * kk + lk][wn0 + 32 * j + lr];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+      if (kt + 1 < nkt) store_tile(buf ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue ---------------------------------------------------------------------
+  const float alpha = P.alpha * (P.alpha_ptr ? *P.alpha_ptr : 1.f);
+  float* Cz = P.C + (long long)z * P.c_split_stride;
+  const bool want_stats = P.stats != nullptr;
+  float csum[TN], csq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    csum[j] = 0.f;
+    csq[j] = 0.f;
+    const int col = n0 + wn0 + 32 * j + lr;
+    const bool cok = col < N;
+    float bias = 0.f;
+    if (z == 0 && cok) {
+      if (P.bias) bias += P.bias[col];
+      if (P.bias2) bias += P.bias2[col];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (cok && row < M) {
+          float* cp = Cz + remap(row, P.c_r1, P.ldc, P.c_s2) + col;
+          float v = fmaf(acc[i][j][r], alpha, bias);
+          if (P.beta != 0.f) v = fmaf(P.beta, *cp, v);
+          if (P.relu) v = fmaxf(v, 0.f);
+          *cp = v;
+          csum[j] += v;
+          csq[j] = fmaf(v, v, csq[j]);
+        }
+      }
+    }
+  }
+  if (want_stats) {
+    // reduce over the two half-waves, then over the waves that share these columns
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      csum[j] += __shfl_xor(csum[j], 32, 64);
+      csq[j] += __shfl_xor(csq[j], 32, 64);
+    }
+    if (lk == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        red[wid][0][32 * j + lr] = csum[j];
+        red[wid][1][32 * j + lr] = csq[j];
+      }
+    }
+    __syncthreads();
+    constexpr int NWM = BM / WM;
+    for (int c = tid; c < BN; c += 256) {
+      const int wn = c / WN, cc = c % WN;
+      float s = 0.f, q = 0.f;
+      for (int w = 0; w < NWM; ++w) {
+        s += red[w * NWN + wn][0][cc];
+        q += red[w * NWN + wn][1][cc];
+      }
+      const int col = n0 + c;
+      if (col < N) {
+        P.stats[((long long)tm * N + col) * 2 + 0] = s;
+        P.stats[((long long)tm * N + col) * 2 + 1] = q;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int AMODE, int BMODE>
+static int launch_t(const GemmArgs& a, bool vec, int blocks, hipStream_t s) {
+  if (vec)
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AMODE, BMODE, true>), dim3(blocks), dim3(256), 0,
+                       s, a);
+  else
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AMODE, BMODE, false>), dim3(blocks), dim3(256),
+                       0, s, a);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
+template <int BM, int BN, int WM, int WN>
+static int launch_mode(const GemmArgs& a, int amode, int bmode, bool vec, int blocks, hipStream_t s) {
+  if (amode == 0 && bmode == 0) return launch_t<BM, BN, WM, WN, 0, 0>(a, vec, blocks, s);
+  if (amode == 0 && bmode == 1) return launch_t<BM, BN, WM, WN, 0, 1>(a, vec, blocks, s);
+  if (amode == 1 && bmode == 0) return launch_t<BM, BN, WM, WN, 1, 0>(a, vec, blocks, s);
+  if (amode == 1 && bmode == 1) return launch_t<BM, BN, WM, WN, 1, 1>(a, vec, blocks, s);
+  if (amode == 2 && bmode == 0) return launch_t<BM, BN, WM, WN, 2, 0>(a, true, blocks, s);
+  if (amode == 3 && bmode == 0) return launch_t<BM, BN, WM, WN, 3, 0>(a, vec, blocks, s);
+  return CAPMI_EINVAL;
+}
+
+extern "C" int capmi_gemm_stat_tiles(int M, int tile) {
+  const int BM = tile == CAPMI_TILE_128 ? 128 : 64;
+  return (M + BM - 1) / BM;
+}
+
+extern "C" int capmi_gemm(const capmi_gemm_problem* probs, int nprob, int amode, int bmode,
+                          int tile, void* stream) {
+  CAPMI_REQUIRE(nprob >= 1 && nprob <= CAPMI_MAX_GROUP, CAPMI_EINVAL);
+  CAPMI_REQUIRE(amode >= 0 && amode <= 3 && bmode >= 0 && bmode <= 1, CAPMI_EINVAL);
+  CAPMI_REQUIRE(tile == CAPMI_TILE_128 || tile == CAPMI_TILE_64, CAPMI_EINVAL);
+  const int BM = tile == CAPMI_TILE_128 ? 128 : 64, BN = BM;
+  GemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.nprob = nprob;
+  bool vec = true;
+  long long total = 0;
+  for (int i = 0; i < nprob; ++i) {
+    const capmi_gemm_problem& p = probs[i];
+    CAPMI_REQUIRE(p.M >= 0 && p.N >= 0 && p.K >= 0 && p.ksplit >= 1, CAPMI_EINVAL);
+    CAPMI_REQUIRE(p.A && p.B && p.C, CAPMI_EINVAL);
+    CAPMI_REQUIRE(p.ksplit == 1 || p.c_split_stride > 0, CAPMI_EINVAL);
+    CAPMI_REQUIRE(p.stats == nullptr || p.ksplit == 1, CAPMI_EINVAL);
+    if (amode == 2) {
+      CAPMI_REQUIRE(p.cCin % BK == 0 && p.cCin % 4 == 0, CAPMI_EALIGN);
+      CAPMI_REQUIRE(p.K == p.cKH * p.cKW * p.cCin && p.M == p.cN * p.cHo * p.cWo, CAPMI_EINVAL);
+      CAPMI_REQUIRE(aligned16(p.A), CAPMI_EALIGN);
+      CAPMI_REQUIRE(p.in_scale == nullptr || (aligned16(p.in_scale) && aligned16(p.in_shift)),
+                    CAPMI_EALIGN);
+    }
+    if (amode == 3) {
+      CAPMI_REQUIRE(p.K == p.cKH * p.cKW * p.cCin && p.M == p.cN * p.cHo * p.cWo, CAPMI_EINVAL);
+    }
+    if (amode == 0) {
+      vec = vec && aligned16(p.A) && p.lda % 4 == 0 && p.K % 4 == 0 && (p.a_r1 <= 0 || p.a_s2 % 4 == 0);
+    } else if (amode == 1) {
+      vec = vec && aligned16(p.A) && p.lda % 4 == 0 && p.M % 4 == 0 && (p.a_r1 <= 0 || p.a_s2 % 4 == 0);
+    }
+    if (bmode == 0)
+      vec = vec && aligned16(p.B) && p.ldb % 4 == 0 && p.K % 4 == 0;
+    else
+      vec = vec && aligned16(p.B) && p.ldb % 4 == 0 && p.N % 4 == 0;
+    if (amode == 2) CAPMI_REQUIRE(aligned16(p.B) && p.ldb % 4 == 0, CAPMI_EALIGN);
+    a.p[i] = p;
+    a.tiles_m[i] = (p.M + BM - 1) / BM;
+    a.tiles_n[i] = (p.N + BN - 1) / BN;
+    int kc = (p.K + p.ksplit - 1) / p.ksplit;
+    kc = ((kc + BK - 1) / BK) * BK;
+    a.kchunk[i] = kc > 0 ? kc : BK;
+    a.tiles_begin[i] = (int)total;
+    total += (long long)a.tiles_m[i] * a.tiles_n[i] * p.ksplit;
+  }
+  a.tiles_begin[nprob] = (int)total;
+  CAPMI_REQUIRE(total < (1LL << 31), CAPMI_ERANGE);
+  if (total == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  if (tile == CAPMI_TILE_128) return launch_mode<128, 128, 64, 64>(a, amode, bmode, vec, (int)total, s);
+  return launch_mode<64, 64, 32, 32>(a, amode, bmode, vec, (int)total, s);
+}
+
+// ------------------------------------------------------------------------------------
+// split-K slab reduction and column sums (bias gradients)
+// ------------------------------------------------------------------------------------
+__global__ void splitk_reduce_kernel(const float* __restrict__ in, int S, long long slab, int rows,
+                                     int cols, long long ld_in, const float* __restrict__ bias,
+                                     float* __restrict__ out, long long ld_out) {
+  const long long n = (long long)rows * cols;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / cols), c = (int)(i - (long long)r * cols);
+    const float* p = in + r * ld_in + c;
+    float s = bias ? bias[c] : 0.f;
+    for (int z = 0; z < S; ++z) s += p[z * slab];
+    out[r * ld_out + c] = s;
+  }
+}
+
+extern "C" int capmi_splitk_reduce(const float* in, int S, long long slab, int rows, int cols,
+                                   long long ld_in, const float* bias, float* out,
+                                   long long ld_out, void* stream) {
+  CAPMI_REQUIRE(S >= 1 && rows >= 0 && cols >= 0, CAPMI_EINVAL);
+  const long long n = (long long)rows * cols;
+  if (n == 0) return 0;
+  const unsigned blocks = (unsigned)std::min<long long>(cdiv(n, 256), 4096);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), in, S,
+                     slab, rows, cols, ld_in, bias, out, ld_out);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
+// stage 1: work[blk_r][c] = sum over rows [blk_r*R, blk_r*R+R) ; stage 2: out[c] = scale*sum work
+__global__ void colsum_stage1(const float* __restrict__ in, int rows, int cols, long long ld,
+                              float* __restrict__ work) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  const int r0 = blockIdx.y * CAPMI_COLSUM_ROWS;
+  const int r1 = min(rows, r0 + CAPMI_COLSUM_ROWS);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += in[(long long)r * ld + c];
+  work[(long long)blockIdx.y * cols + c] = s;
+}
+
+__global__ void colsum_stage2(const float* __restrict__ work, int nb, int cols, float scale,
+                              float* __restrict__ out, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += work[(long long)b * cols + c];
+  s *= scale;
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+extern "C" int capmi_colsum(const float* in, int rows, int cols, long long ld, float scale,
+                            float* work, float* out, int accumulate, void* stream) {
+  CAPMI_REQUIRE(rows >= 0 && cols >= 0, CAPMI_EINVAL);
+  if (cols == 0) return 0;
+  const int nb = rows > 0 ? (int)cdiv(rows, CAPMI_COLSUM_ROWS) : 0;
+  hipStream_t s = as_stream(stream);
+  if (nb > 0)
+    hipLaunchKernelGGL(colsum_stage1, dim3(cdiv(cols, 256), nb), dim3(256), 0, s, in, rows, cols,
+                       ld, work);
+  hipLaunchKernelGGL(colsum_stage2, dim3(cdiv(cols, 256)), dim3(256), 0, s, work, nb, cols, scale,
+                     out, accumulate);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,229 @@
+"""Soft-attention captioning decoder with the reference surface
+(models/attention.py of SarahAlkhateeb/Image-Captioning-with-Different-Decoders).
+
+Same classes, constructor arguments, sub-module attributes and state-dict keys
+(``attention.{enc_att,dec_att,full_att}``, ``decode_step``, ``h_lin``, ``c_lin``,
+``f_beta``, ``fc``, ``embedding``), same forward signatures and outputs. The
+compute runs on libcapmi's HIP kernels (capmi.decoder_core): forward,
+backward-through-time, fused CE + regulariser and the clamp+Adam update.
+"""
+import os
+import time
+
+import torch
+import torch.nn as nn
+
+from capmi import decoder_fn as DF
+from capmi.optim import Adam as FusedAdam
+from checkpoint import load_checkpoint, save_checkpoint, unpack_checkpoint
+from metric import AccumulatingMetric
+from models.encoder import EncoderAttention
+from train_utils import clip_gradient
+from vocabulary import PAD_TOKEN, Vocabulary
+
+
+class SoftAttention(nn.Module):
+    """Attention network (reference :18-61). ReLU score (the reference's, not tanh)."""
+
+    def __init__(self, encoder_dim=2048, decoder_dim=512, attention_dim=512):
+        super(SoftAttention, self).__init__()
+        self.enc_att = nn.Linear(encoder_dim, attention_dim)
+        self.dec_att = nn.Linear(decoder_dim, attention_dim)
+        self.full_att = nn.Linear(attention_dim, 1)
+        self.relu = nn.ReLU()
+        self.softmax = nn.Softmax(dim=1)
+
+    def forward(self, encoder_out, decoder_hidden):
+        """(B,P,E), (B,D) -> attention-weighted encoding (B,E), weights (B,P)."""
+        return DF.soft_attention_forward(self, encoder_out, decoder_hidden)
+
+
+class AttentionDecoderParams:
+    attention_dim = 512
+    decoder_dim = 512
+    embed_size = 512  # Use 300 if glove and 768 if BERT.
+    dropout = 0.5
+    use_bert = False
+    vocab = None  # Must override.
+
+
+class AttentionDecoder(nn.Module):
+    """Reference :72-284."""
+
+    def __init__(self, device, params):
+        super(AttentionDecoder, self).__init__()
+        assert isinstance(params, AttentionDecoderParams)
+        assert isinstance(params.vocab, Vocabulary)
+        self.device = device
+        self.encoder_dim = 2048  # Set in stone.
+        self.attention_dim = params.attention_dim
+        self.embed_size = params.embed_size
+        self.decoder_dim = params.decoder_dim
+        self.vocab = params.vocab
+        self.vocab_size = len(self.vocab)
+        self.dropout = params.dropout
+        self.use_bert = params.use_bert
+        if self.use_bert:
+            # reference :96-100 fetches bert-base-uncased by name (network); not available offline
+            raise NotImplementedError("BERT embeddings need bert-base-uncased (not available offline)")
+
+        self.attention = SoftAttention(self.encoder_dim, self.decoder_dim, self.attention_dim)
+        self.dropout = nn.Dropout(p=self.dropout)
+        self.decode_step = nn.LSTMCell(self.embed_size + self.encoder_dim, self.decoder_dim, bias=True)
+        self.h_lin = nn.Linear(self.encoder_dim, self.decoder_dim)
+        self.c_lin = nn.Linear(self.encoder_dim, self.decoder_dim)
+        self.f_beta = nn.Linear(self.decoder_dim, self.encoder_dim)
+        self.sigmoid = nn.Sigmoid()
+        self.fc = nn.Linear(self.decoder_dim, self.vocab_size)
+        self.embedding = nn.Embedding(self.vocab_size, self.embed_size)
+
+        # reference :119-126
+        self.fc.bias.data.fill_(0)
+        self.fc.weight.data.uniform_(-0.1, 0.1)
+        self.embedding.weight.data.uniform_(-0.1, 0.1)
+        self.fine_tune_embeddings(on=True)
+
+    def load_pretrained_embeddins(self, embeddings):
+        """Reference :128-136 (name kept, typo included). GloVe tables stay fp64 (Q7)."""
+        self.embedding.weight = nn.Parameter(embeddings)
+
+    def fine_tune_embeddings(self, on=True):
+        for param in self.embedding.parameters():
+            param.requires_grad = on
+
+    def init_hidden_state(self, encoder_out):
+        """(B,P,E) -> h, c (B,D) (reference :151-164)."""
+        return DF.init_hidden_forward(self, encoder_out)
+
+    def forward(self, encoder_out, encoded_captions, caption_lengths):
+        """(B,14,14,E), (B,L) int64, list[int] -> predictions (B,T,V), captions,
+        decode_lengths, alphas (B,T,P)   (reference :218-284)."""
+        return DF.decoder_forward(self, encoder_out, encoded_captions, caption_lengths)
+
+
+# ======================================================================================
+# training (reference :287-452)
+# ======================================================================================
+def _train_dataset(args):
+    from capmi.data import SyntheticCOCO, synthetic_requested
+    if synthetic_requested(args):
+        return SyntheticCOCO.from_args(args)
+    from dataset import COCODataset  # real COCO path (needs pycocotools, nltk, images)
+    return COCODataset(mode='train', caption_max_len=args.max_caption_length)
+
+
+def train(device, args):
+    """Trains the attention model (reference :287-452), same loop and log line.
+
+    Differences, all deliberate: the step runs the fused capmi path (hoisted
+    GEMMs, fused CE + regulariser, gradients written in place, clamp fused into
+    Adam); ``loss.item()`` syncs only every ``print_freq`` batches; data-parallel
+    over torchrun ranks when WORLD_SIZE > 1 (gradient all-reduce over RCCL);
+    checkpoints hold state_dicts (Q13)."""
+    from capmi import dist as cdist
+    from capmi.train_step import AttentionTrainStep
+
+    ctx = cdist.init_from_env(device)
+    device = ctx.device
+    dataset = _train_dataset(args)
+    pad_idx = dataset.vocab(PAD_TOKEN)
+
+    def collate_fn(data):
+        from torch.nn.utils.rnn import pad_sequence
+        imgs, captions = zip(*data)
+        imgs = torch.stack(imgs, dim=0)
+        captions = pad_sequence(captions, batch_first=True, padding_value=pad_idx)
+        caption_lengths = [len(caption) for caption in captions]  # after padding (Q1)
+        return imgs, captions, caption_lengths
+
+    sampler = cdist.sampler_for(dataset, ctx)
+    train_loader = torch.utils.data.DataLoader(
+        dataset=dataset, batch_size=args.batch_size, shuffle=sampler is None, sampler=sampler,
+        num_workers=args.workers, collate_fn=collate_fn, pin_memory=True)
+
+    if args.checkpoint is None:
+        encoder = EncoderAttention()
+        if args.fine_tune_encoder:
+            raise NotImplementedError("capmi: encoder fine-tuning is not built yet (config 4)")
+        decoder_params = AttentionDecoderParams()
+        decoder_params.attention_dim = args.attention_dim
+        decoder_params.decoder_dim = args.decoder_dim
+        decoder_params.embed_size = args.embed_size
+        decoder_params.dropout = args.decoder_dropout
+        decoder_params.vocab = dataset.vocab
+        decoder_params.use_bert = args.use_bert
+        decoder = AttentionDecoder(device, decoder_params)
+        if args.use_glove:
+            from embed import load_glove_vectors
+            decoder.load_pretrained_embeddins(load_glove_vectors())
+        decoder.fine_tune_embeddings(args.fine_tune_embedding)
+        start_epoch, metrics, opt_state = 0, {}, None
+    else:
+        chkpt = load_checkpoint(device, args)
+        start_epoch, enc_sd, dec_sd, _, opt_state, metrics = unpack_checkpoint(chkpt)
+        start_epoch += 1
+        encoder = EncoderAttention()
+        encoder.load_state_dict(enc_sd)
+        decoder_params = AttentionDecoderParams()
+        decoder_params.attention_dim, decoder_params.decoder_dim = args.attention_dim, args.decoder_dim
+        decoder_params.embed_size, decoder_params.dropout = args.embed_size, args.decoder_dropout
+        decoder_params.vocab = dataset.vocab
+        decoder = AttentionDecoder(device, decoder_params)
+        if dec_sd["embedding.weight"].dtype == torch.float64:
+            decoder.load_pretrained_embeddins(dec_sd["embedding.weight"].clone())
+        decoder.load_state_dict(dec_sd)
+        decoder.fine_tune_embeddings(args.fine_tune_embedding)
+
+    encoder = encoder.to(device)
+    decoder = decoder.to(device)
+    cdist.broadcast_module(decoder, ctx)
+    decoder_optimizer = FusedAdam(filter(lambda p: p.requires_grad, decoder.parameters()),
+                                  lr=args.decoder_lr)
+    if opt_state is not None:
+        decoder_optimizer.load_state_dict(opt_state)
+    step = AttentionTrainStep(encoder, decoder, decoder_optimizer, ctx, alpha_c=args.alpha_c)
+
+    decoder.train()
+    encoder.train()
+    num_batches = len(train_loader)
+    epoch_losses = metrics.get('epoch_losses', [])
+    for epoch in range(start_epoch, args.epochs):
+        if sampler is not None:
+            sampler.set_epoch(epoch)
+        batch_losses = []
+        accum_loss = AccumulatingMetric()
+        accum_time = AccumulatingMetric()
+        start = time.time()
+        pending = []
+        for batch_idx, (imgs, captions, caption_lengths) in enumerate(train_loader):
+            imgs = imgs.to(device, non_blocking=True)
+            captions = captions.to(device, non_blocking=True)
+            clip_gradient(decoder_optimizer, args.grad_clip)
+            loss = step(imgs, captions, caption_lengths)
+            pending.append(loss.detach().clone())
+            if batch_idx % args.print_freq == 0 or batch_idx == num_batches - 1:
+                for l in torch.stack(pending).view(-1).tolist():   # one sync per print
+                    batch_losses.append(l)
+                    accum_loss.update(l)
+                pending = []
+                accum_time.update(time.time() - start)
+                if ctx.rank == 0:
+                    print(f'Epoch {epoch+1}/{args.epochs}, Batch {batch_idx+1}/{num_batches}, '
+                          f'Loss {accum_loss.avg():.4f}, Time: {accum_time.val:.4f}')
+            start = time.time()
+        epoch_losses.append(batch_losses)
+        metrics = {'epoch_losses': epoch_losses}
+        if ctx.rank == 0:
+            save_checkpoint(args, epoch, encoder, decoder, None, decoder_optimizer, metrics)
+    if ctx.rank == 0:
+        print(f'Model {args.model_name} finished training for {args.epochs} epochs.')
+
+
+def evaluate(device, args, encoder, decoder):
+    """Reference :454-567 (teacher-forced validation + caption metrics): evaluation is
+    outside the training hot path this round builds."""
+    raise NotImplementedError("evaluation / caption scoring is not part of the training path")
+
+
+__all__ = ["SoftAttention", "AttentionDecoderParams", "AttentionDecoder", "train", "evaluate"]
+_ = os

@@ -1,0 +1,107 @@
+"""ResNet-101 encoders with the reference surface (models/encoder.py of
+SarahAlkhateeb/Image-Captioning-with-Different-Decoders).
+
+``EncoderAttention`` (reference :72-121) and ``Encoder`` (:22-69) keep their
+constructor, ``forward`` and ``fine_tune`` signatures, the ``resnet`` /
+``adaptive_pool`` / ``embed`` attributes and the state-dict keys
+(``resnet.<i>...`` over torchvision's children()). On HIP tensors the conv
+stack runs through libcapmi (capmi.resnet.EncoderRunner); on CPU tensors the
+ordinary nn modules run, as the reference does on its CPU config.
+"""
+import os
+
+import torch
+from torch import nn
+
+from capmi import kernels as K
+from capmi.resnet import EncoderRunner, resnet101
+
+_LOCAL_WEIGHTS = os.path.join("models", "resnet101.pth")
+
+
+def _load_resnet101_model():
+    """Reference :9-20 loads torchvision weights (a local models/resnet101.pth, or a download).
+    Offline, this loads $CAPMI_RESNET101_WEIGHTS or models/resnet101.pth when present
+    (weights_only=True), else keeps torchvision's random init (seeded by the caller)."""
+    path = os.environ.get("CAPMI_RESNET101_WEIGHTS")
+    if path is None and os.path.exists(_LOCAL_WEIGHTS):
+        path = _LOCAL_WEIGHTS
+    return resnet101(path)
+
+
+class _ResNetView:
+    """Attribute view of Sequential(children()[:-2 or -1]) for the fused runner."""
+
+    def __init__(self, seq):
+        self.conv1, self.bn1 = seq[0], seq[1]
+        self.layer1, self.layer2, self.layer3, self.layer4 = seq[4], seq[5], seq[6], seq[7]
+
+
+def _check_frozen(module):
+    if torch.is_grad_enabled() and any(p.requires_grad for p in module.parameters()):
+        raise NotImplementedError(
+            "capmi: encoder fine-tuning (conv dgrad/wgrad, BASELINE config 4) is not built yet; "
+            "the frozen-encoder forward is")
+
+
+class Encoder(nn.Module):
+    """CNN encoder of the baseline model (reference :22-69)."""
+
+    def __init__(self, embed_size):
+        super().__init__()
+        resnet = _load_resnet101_model()
+        modules = list(resnet.children())[:-1]
+        self.resnet = nn.Sequential(*modules)
+        self.embed = nn.Linear(resnet.fc.in_features, embed_size)
+        for param in self.resnet.parameters():
+            param.requires_grad = False
+        self._runner = EncoderRunner()
+
+    def forward(self, imgs):
+        if not imgs.is_cuda:
+            features = self.resnet(imgs)
+            return self.embed(features.view(features.size(0), -1))
+        _check_frozen(self.resnet)
+        feats = self._runner.forward(_ResNetView(self.resnet), imgs.contiguous(), (1, 1),
+                                     train=self.training)
+        N = feats.shape[0]
+        out = torch.empty(N, self.embed.out_features, device=imgs.device, dtype=torch.float32)
+        if torch.is_grad_enabled() and self.embed.weight.requires_grad:
+            return torch.nn.functional.linear(feats.view(N, -1), self.embed.weight, self.embed.bias)
+        K.gemm(K.problem(N, self.embed.out_features, 2048, feats, 2048, self.embed.weight, 2048, out,
+                         self.embed.out_features, bias=self.embed.bias), 0, 0, K.TILE_64)
+        return out
+
+    def fine_tune(self, on=True):
+        for conv_block in list(self.resnet.children())[5:]:
+            for param in conv_block.parameters():
+                param.requires_grad = on
+
+
+class EncoderAttention(nn.Module):
+    """CNN encoder of the attention model (reference :72-121): (B,3,H,W) -> (B,14,14,2048)."""
+
+    def __init__(self):
+        super().__init__()
+        resnet = _load_resnet101_model()
+        modules = list(resnet.children())[:-2]
+        self.resnet = nn.Sequential(*modules)
+        self.adaptive_pool = nn.AdaptiveAvgPool2d((14, 14))
+        for param in self.resnet.parameters():
+            param.requires_grad = False
+        self._runner = EncoderRunner()
+
+    def forward(self, imgs):
+        if not imgs.is_cuda:
+            features = self.adaptive_pool(self.resnet(imgs))
+            return features.permute(0, 2, 3, 1)
+        _check_frozen(self.resnet)
+        out_hw = self.adaptive_pool.output_size
+        out_hw = (out_hw, out_hw) if isinstance(out_hw, int) else tuple(out_hw)
+        return self._runner.forward(_ResNetView(self.resnet), imgs.contiguous(), out_hw,
+                                    train=self.training)
+
+    def fine_tune(self, on=True):
+        for conv_block in list(self.resnet.children())[5:]:
+            for param in conv_block.parameters():
+                param.requires_grad = on

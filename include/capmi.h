@@ -1,0 +1,211 @@
+/*
+ * capmi.h -- C ABI of libcapmi.so, the MI355X (gfx950) kernels behind the
+ * 'attention' captioning training step of
+ * SarahAlkhateeb/Image-Captioning-with-Different-Decoders.
+ *
+ * The reference has no native boundary: every device op is a PyTorch library
+ * op called from Python. Each entry point below replaces the reference op(s)
+ * cited next to it (file:line into the reference). Conventions:
+ *   - plain device pointers (fp32 unless the name says f64), sizes as ints,
+ *     the HIP stream as an opaque `void*` (hipStream_t), no torch types;
+ *   - every call returns 0 on success, else a CAPMI_E* code or a hipError_t
+ *     (>= 1000 is capmi's own, see capmi_strerror);
+ *   - the library never allocates or frees device memory: every output and
+ *     workspace is passed in by the caller (PyTorch's caching allocator);
+ *   - launches only, no synchronisation: every call is safe inside a
+ *     hipStreamBeginCapture / hipGraph.
+ * Layouts: activations are NHWC (channels innermost); decoder per-step state
+ * is time-major (T, B, ...); weights stay in their nn.Module layout except
+ * the conv weights, which are packed once to [Cout][KH][KW][Cin].
+ */
+#ifndef CAPMI_H
+#define CAPMI_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CAPMI_ABI_VERSION 1
+
+#define CAPMI_OK 0
+#define CAPMI_EINVAL 1001   /* bad shape / argument */
+#define CAPMI_EALIGN 1002   /* pointer or stride not aligned as required */
+#define CAPMI_ERANGE 1003   /* size outside what the kernel supports */
+
+#define CAPMI_MAX_GROUP 4
+
+/* ------------------------------------------------------------------------
+ * GEMM / implicit-GEMM convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32).
+ * C[M,N] = alpha * op(A)[M,K] * op(B)[K,N] (+ bias) (+ beta*C) (relu)
+ * Replaces: nn.Linear forward/backward (models/attention.py:33-35,54-55,
+ * 110-114,162-163,270,279), the LSTMCell gate GEMMs (:108-109,277-278) and
+ * every Conv2d of torchvision's ResNet-101 (models/encoder.py:88-91,107).
+ * ---------------------------------------------------------------------- */
+enum capmi_amode {
+  CAPMI_A_KMAJOR = 0,   /* A[m][k]: off(m) + k, off(r) = (r % a_r1)*lda + (r / a_r1)*a_s2 */
+  CAPMI_A_MMAJOR = 1,   /* A[k][m]: off(k) + m  (i.e. A^T of a row-major matrix)          */
+  CAPMI_A_CONV_NHWC = 2,/* implicit im2col of an NHWC input, k = (kh, kw, ci), Cin % 16 == 0 */
+  CAPMI_A_CONV_NCHW = 3 /* implicit im2col of an NCHW input, k = (ci, kh, kw) (conv1)    */
+};
+enum capmi_bmode {
+  CAPMI_B_NMAJOR_W = 0, /* B[k][n] = W[n][k] (nn.Linear weight / packed conv weight), ldb = row stride of W */
+  CAPMI_B_KROWS = 1     /* B[k][n] row-major, ldb = row stride */
+};
+enum capmi_tile { CAPMI_TILE_128 = 0, CAPMI_TILE_64 = 1 };
+
+typedef struct capmi_gemm_problem {
+  int M, N, K;
+  int ksplit;            /* >= 1. split z writes C + z*c_split_stride (raw partials, bias only on z = 0) */
+  const float* A; long long lda, a_r1, a_s2;   /* a_r1 <= 0 means "no 2-level row remap" */
+  const float* B; long long ldb;
+  float* C; long long ldc, c_r1, c_s2, c_split_stride;
+  const float* bias;     /* [N] or NULL */
+  const float* bias2;    /* [N] or NULL (added as well: LSTM b_ih + b_hh) */
+  const float* alpha_ptr;/* device scalar multiplying A*B, or NULL */
+  float alpha, beta;     /* host scalars; beta != 0 reads C */
+  int relu;
+  float* stats;          /* NULL or [ceil(M/BM)][N][2] per-tile (sum, sumsq) of the stored C (BN-train stats) */
+  /* implicit-GEMM conv geometry (A = input activation, modes 2/3) */
+  int cN, cH, cW, cCin, cKH, cKW, cStride, cPad, cHo, cWo;
+  const float* in_scale; /* NULL or [Cin]: A element := relu(x*in_scale[ci] + in_shift[ci]) in-bounds (BN-apply+ReLU prologue) */
+  const float* in_shift;
+} capmi_gemm_problem;
+
+int capmi_gemm(const capmi_gemm_problem* problems, int nprob, int amode, int bmode, int tile,
+               void* stream);
+/* rows of the per-tile statistics buffer capmi_gemm writes for a given M and tile */
+int capmi_gemm_stat_tiles(int M, int tile);
+
+/* sum of S partial slabs: out[r][c] = sum_s in[s*slab + r*ld_in + c] (+ bias[c]); rows x cols */
+int capmi_splitk_reduce(const float* in, int S, long long slab, int rows, int cols, long long ld_in,
+                        const float* bias, float* out, long long ld_out, void* stream);
+/* column sums of a rows x cols row-major matrix (bias gradients): out[c] = scale * sum_r in[r*ld + c].
+ * work must hold ceil(rows/CAPMI_COLSUM_ROWS) * cols floats. accumulate != 0 adds into out. */
+#define CAPMI_COLSUM_ROWS 256
+int capmi_colsum(const float* in, int rows, int cols, long long ld, float scale, float* work,
+                 float* out, int accumulate, void* stream);
+
+/* ------------------------------------------------------------------------
+ * ResNet-101 encoder pieces (models/encoder.py:88-110, BatchNorm in train
+ * mode because the reference calls encoder.train(): models/attention.py:374).
+ * ---------------------------------------------------------------------- */
+/* [Cout][Cin][KH][KW] -> [Cout][KH][KW][Cin] */
+int capmi_conv_weight_pack(const float* w, int Cout, int Cin, int KH, int KW, float* out, void* stream);
+/* BatchNorm2d(train) finalize from capmi_gemm stats: mean/var over `count` rows, then
+ * scale = gamma*rsqrt(var+eps), shift = beta - mean*scale; running stats updated in place
+ * (momentum, unbiased var) when running_mean != NULL. mean/var out (may be NULL). */
+int capmi_bn_finalize(const float* stats, int tiles, int C, long long count, const float* gamma,
+                      const float* beta, float* running_mean, float* running_var, float momentum,
+                      float eps, float* scale, float* shift, float* save_mean, float* save_var,
+                      void* stream);
+/* BatchNorm2d(eval): scale/shift from running statistics */
+int capmi_bn_eval_params(const float* gamma, const float* beta, const float* running_mean,
+                         const float* running_var, int C, float eps, float* scale, float* shift,
+                         void* stream);
+/* Bottleneck tail: out = relu(y*s + b + (res_scale ? res*rs + rb : res)), NHWC, C % 4 == 0 */
+int capmi_bn_add_relu(const float* y, const float* s, const float* b, const float* res,
+                      const float* res_scale, const float* res_shift, float* out, long long rows,
+                      int C, void* stream);
+/* conv1 tail: out = maxpool3x3/2/p1(relu(y*s + b)), NHWC (models/encoder.py:90 children 1-3) */
+int capmi_bn_relu_maxpool(const float* y, const float* s, const float* b, float* out, int N, int H,
+                          int W, int C, int Ho, int Wo, void* stream);
+/* AdaptiveAvgPool2d to (OH,OW) on NHWC, output NHWC (models/encoder.py:92,108-109) */
+int capmi_adaptive_avgpool_nhwc(const float* in, int N, int H, int W, int C, int OH, int OW,
+                                float* out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Attention decoder (models/attention.py:43-61, 151-164, 218-284).
+ * Per-step state is time-major: X[t][b][M+E], H[t][b][D], ...
+ * ---------------------------------------------------------------------- */
+/* out[t][b][0:M] (row stride ld_out) = emb[caps[b*L + t]] for t < T; emb fp32 or fp64 (emb_is_f64) */
+int capmi_embed_gather(const void* emb, int emb_is_f64, int M, const long long* caps, int B, int L,
+                       int T, float* out, long long ld_out, void* stream);
+/* out[b][e] = mean_p enc[b][p][e]  (encoder_out.mean(dim=1), :161) */
+int capmi_mean_rows(const float* enc, int B, int P, int E, float* out, void* stream);
+/* Soft-attention score (:54-58 without the softmax): ad = sum_s dec_part[s][b][:] + bias_da;
+ * e[b][p] = relu(att_enc[b][p][:] + ad) . wf + bf. Writes ad to att_dec_out[b][:] if non-NULL. */
+int capmi_att_score_fwd(const float* att_enc, const float* dec_part, int S, long long dec_slab,
+                        const float* bias_da, const float* wf, const float* bf, int B, int P, int A,
+                        float* e, float* att_dec_out, void* stream);
+/* softmax over P (:58) + context (:59-60) + optional f_beta gate (:270-271).
+ * alpha -> alpha_out[b*alpha_ld_b + p] (zeros for rows b >= bt); awe (ungated) -> awe_out[b][E];
+ * gate = sigmoid(sum_s gate_part[s][b][:] + bias_fb) -> gate_out[b][E];
+ * gated awe -> x_out[b*ld_x + e] (if x_out). gate_part == NULL: no gate. */
+int capmi_att_softmax_ctx_fwd(const float* e, const float* enc, int B, int P, int E, int bt,
+                              float* alpha_out, long long alpha_ld_b, float* awe_out,
+                              const float* gate_part, int S, long long gate_slab,
+                              const float* bias_fb, float* gate_out, float* x_out, long long ld_x,
+                              void* stream);
+/* LSTMCell (:108-109,277-278), gate order i,f,g,o. pre = sum_s part[s] + xemb + sum_s hh_part[s].
+ * writes h_out, c_out [B][D], act_out [B][4D] = (sig i, sig f, tanh g, sig o) */
+int capmi_lstm_cell_fwd(const float* part, int S, long long slab, const float* xemb,
+                        const float* hh_part, int S2, long long slab2, const float* c_prev, int B,
+                        int D, float* h_out, float* c_out, float* act_out, void* stream);
+/* Dropout before fc (:107,279): out = in * keep/(1-p), keep = hash(seed, index) >= p */
+int capmi_dropout(const float* in, long long n, float p, unsigned long long seed, float* out,
+                  void* stream);
+/* zero rows r of a (rows x cols) matrix, row r = t*B + b, where b >= bt[t] (ragged decode, :261) */
+int capmi_mask_rows_tb(float* x, const int* bt, int T, int B, int cols, long long ld, long long r1,
+                       long long s2, void* stream);
+
+/* Loss (:401-414). rows r = b*T + t of logits (B,T,V); target = caps[b*L + t + 1].
+ * loss_rows[r] = lse - x[target]; dlogits (if non-NULL) = (softmax - onehot) * (*gscale) / nrows,
+ * written at row t*B + b (time-major) when dl_time_major else b*T + t. Rows with t >= T_b skipped. */
+int capmi_ce_fwd_bwd(const float* logits, const long long* caps, int B, int T, int L, int V,
+                     const int* bt, int nrows, float* loss_rows, float* lse, float* dlogits,
+                     int dl_time_major, const float* gscale, void* stream);
+/* alpha regulariser ((alpha_c - sum_t alpha)^2).mean() over (B,P), alphas (B,T,P):
+ * writes reg (1 float) and dreg[b][p] = -2 (alpha_c - sum_t alpha) / (B*P). */
+int capmi_alpha_reg(const float* alphas, int B, int T, int P, float alpha_c, float* reg,
+                    float* dreg, void* stream);
+/* loss = sum(loss_rows[0:n]) / nrows + (reg ? reg[0] : 0) -> out[0] (single block, deterministic) */
+int capmi_loss_finalize(const float* loss_rows, int n, int nrows, const float* reg, float* out,
+                        void* stream);
+
+/* ---- backward through time ---- */
+/* dh = dhd[b][:] (already dropout-masked, may be NULL) + sum_s dh_part[s][b][:]; dc = dc_in (NULL=0)
+ * -> dgates [B][4D] (pre-activation) and dc_out [B][D]; rows b >= bt produce zeros. */
+int capmi_lstm_cell_bwd(const float* dhd, const float* dh_part, int S, long long slab,
+                        const float* dc_in, const float* act, const float* c_prev,
+                        const float* c_cur, int B, int D, int bt, float* dgates, float* dc_out,
+                        void* stream);
+/* d(awe_g) = sum_s part[s]; dawe = d*gate; dgp = d*awe*gate*(1-gate) (if gate != NULL)
+ * dalpha[b][p] = dawe . enc[b][p][:] */
+int capmi_att_ctx_bwd(const float* part, int S, long long slab, const float* gate,
+                      const float* awe, const float* enc, int B, int P, int E, float* dgp,
+                      float* dalpha, void* stream);
+/* softmax backward with an extra dalpha term (dreg[b*dreg_ld_b + p], may be NULL: the alphas
+ * output's own gradient) and the ReLU score backward:
+ *   da = dalpha + dreg; de = alpha*(da - sum_p alpha*da); dad[b][a] = wf[a] sum_p de[p] [att_enc+ad > 0]
+ * alpha read at alpha[b*alpha_ld_b + p]. rows b >= bt produce zeros. */
+int capmi_att_score_bwd(const float* dalpha, const float* dreg, long long dreg_ld_b,
+                        const float* alpha, long long alpha_ld_b, const float* att_enc,
+                        const float* att_dec, const float* wf, int B, int P, int A, int bt,
+                        float* de, float* dad, void* stream);
+/* hoisted: datt_enc[b][p][a] = wf[a] sum_t de[t][b][p] [att_enc+ad_t > 0];
+ * wf_part[blk][a] += sum de*relu(.) ; bf_part[blk] = sum de  (blk = one per (b, p-chunk)) */
+int capmi_att_enc_grad(const float* de, const float* att_enc, const float* att_dec,
+                       const float* wf, int T, int B, int P, int A, float* datt_enc,
+                       float* wf_part, float* bf_part, int* nblk_out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Optimiser (train_utils.py:2-12 clamp + torch.optim.Adam, models/attention.py:352-355,423-430)
+ * p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps) with g clamped to +-clip first.
+ * ---------------------------------------------------------------------- */
+int capmi_adam_clamp(float* p, const float* g, float* m, float* v, long long n, float lr,
+                     float beta1, float beta2, float eps, float bc1, float bc2_sqrt, float clip,
+                     void* stream);
+int capmi_adam_clamp_f64(double* p, const double* g, double* m, double* v, long long n, double lr,
+                         double beta1, double beta2, double eps, double bc1, double bc2_sqrt,
+                         double clip, void* stream);
+/* embedding gradient: demb[caps[b*L+t]][:] += dx[t][b][0:M] (atomic; fp32 or fp64 table) */
+int capmi_embed_scatter_add(const float* dx, long long ld_dx, const long long* caps, int B, int L,
+                            int T, const int* bt, int M, void* demb, int demb_is_f64, void* stream);
+
+const char* capmi_strerror(int code);
+int capmi_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CAPMI_H */

@@ -1,0 +1,144 @@
+"""GPU: libcapmi GEMM / implicit-GEMM conv vs fp64 CPU references.
+
+Tolerance: |C - C64| <= 4e-6 * (|A| |B|)_ij + 1e-6, i.e. a few fp32 roundings
+of the row-by-column sum of magnitudes (the MFMA result is an exact fp32 fmaf
+chain in a different k order than any CPU library)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _K():
+    from capmi import kernels as K
+    return K
+
+
+def check(C, ref, ref_abs, what):
+    err = (C.double().cpu() - ref).abs()
+    tol = 4e-6 * ref_abs + 1e-6
+    assert bool((err <= tol).all()), f"{what}: max err {float(err.max()):.3g}, worst ratio {float((err / tol).max()):.3g}"
+
+
+def rnd(*shape, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(*shape, generator=g, dtype=torch.float64) * 2 - 1
+
+
+@pytest.mark.parametrize("tile", [0, 1])
+@pytest.mark.parametrize("M,N,Kd", [(300, 200, 96), (64, 2048, 512), (129, 65, 50), (1, 7, 3)])
+def test_linear_fwd(tile, M, N, Kd):
+    K = _K()
+    X, W, b, b2 = rnd(M, Kd, seed=1), rnd(N, Kd, seed=2), rnd(N, seed=3), rnd(N, seed=4)
+    C = torch.empty(M, N, device=DEV)
+    K.gemm(K.problem(M, N, Kd, X.float().to(DEV), Kd, W.float().to(DEV), Kd, C, N,
+                     bias=b.float().to(DEV), bias2=b2.float().to(DEV)), 0, 0, tile)
+    ref = X @ W.T + b + b2
+    check(C, ref, X.abs() @ W.abs().T + b.abs() + b2.abs(), "linear")
+
+
+@pytest.mark.parametrize("tile", [0, 1])
+def test_transposed_modes_and_remap(tile):
+    K = _K()
+    # dW = dY^T X with dY stored batch-major (B,T,N) and read time-major through the 2-level remap
+    B, T, N, Kx = 5, 7, 36, 44
+    dY = rnd(B, T, N, seed=5)
+    Xt = rnd(T * B, Kx, seed=6)  # time-major rows r = t*B + b
+    C = torch.empty(N, Kx, device=DEV)
+    K.gemm(K.problem(N, Kx, T * B, dY.float().to(DEV), T * N, Xt.float().to(DEV), Kx, C, Kx,
+                     a_r1=B, a_s2=N), 1, 1, tile)
+    dY_tm = dY.permute(1, 0, 2).reshape(T * B, N)
+    check(C, dY_tm.T @ Xt, dY_tm.abs().T @ Xt.abs(), "MMAJOR x KROWS with remap")
+    # dX = dY W (B operand row-major [K][N]) with output row remap to batch-major
+    W = rnd(N, Kx, seed=7)
+    out = torch.zeros(B, T, Kx, device=DEV)
+    K.gemm(K.problem(T * B, Kx, N, dY.float().to(DEV), T * N, W.float().to(DEV), Kx, out, T * Kx,
+                     a_r1=B, a_s2=N, c_r1=B, c_s2=Kx), 0, 1, tile)
+    ref = (dY_tm @ W).view(T, B, Kx).permute(1, 0, 2)
+    check(out, ref, (dY_tm.abs() @ W.abs()).view(T, B, Kx).permute(1, 0, 2), "KMAJOR x KROWS, C remap")
+
+
+def test_splitk_grouped_and_reduce():
+    K = _K()
+    B, D, N1, N2 = 64, 512, 512, 2048
+    h = rnd(B, D, seed=8)
+    W1, W2 = rnd(N1, D, seed=9), rnd(N2, D, seed=10)
+    s1, s2 = 4, 2
+    P1 = torch.empty(s1, B, N1, device=DEV)
+    P2 = torch.empty(s2, B, N2, device=DEV)
+    hd = h.float().to(DEV)
+    K.gemm([K.problem(B, N1, D, hd, D, W1.float().to(DEV), D, P1, N1, ksplit=s1, c_split_stride=B * N1),
+            K.problem(B, N2, D, hd, D, W2.float().to(DEV), D, P2, N2, ksplit=s2, c_split_stride=B * N2)],
+           0, 0, 1)
+    out = torch.empty(B, N1, device=DEV)
+    bias = rnd(N1, seed=11)
+    K.splitk_reduce(P1, s1, B * N1, B, N1, N1, out, N1, bias=bias.float().to(DEV))
+    check(out, h @ W1.T + bias, h.abs() @ W1.abs().T + bias.abs(), "split-K + reduce")
+    check(P2.sum(0), h @ W2.T, h.abs() @ W2.abs().T, "grouped problem 2")
+
+
+def test_colsum():
+    K = _K()
+    x = rnd(1000, 77, seed=12)
+    out = torch.empty(77, device=DEV)
+    work = torch.empty(K.colsum_work_size(1000, 77), device=DEV)
+    K.colsum(x.float().to(DEV), 1000, 77, 77, out, work)
+    check(out, x.sum(0), x.abs().sum(0), "colsum")
+
+
+def test_bn_stats_epilogue():
+    K = _K()
+    M, N, Kd = 1000, 96, 64
+    X, W = rnd(M, Kd, seed=13), rnd(N, Kd, seed=14)
+    C = torch.empty(M, N, device=DEV)
+    tiles = K.stat_tiles(M)
+    stats = torch.empty(tiles, N, 2, device=DEV)
+    K.gemm(K.problem(M, N, Kd, X.float().to(DEV), Kd, W.float().to(DEV), Kd, C, N, stats=stats), 0, 0, 0)
+    Cd = C.double().cpu()
+    s = stats.double().cpu().sum(0)
+    torch.testing.assert_close(s[:, 0], Cd.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(s[:, 1], (Cd * Cd).sum(0), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("k,stride,cin,cout,hw,prologue", [
+    (3, 1, 64, 64, 14, True), (3, 2, 128, 128, 15, True), (1, 2, 64, 256, 14, False),
+    (1, 1, 64, 256, 9, True)])
+def test_conv_nhwc(k, stride, cin, cout, hw, prologue):
+    K = _K()
+    N = 3
+    x = rnd(N, cin, hw, hw, seed=15)
+    w = rnd(cout, cin, k, k, seed=16) * 0.1
+    sc, sh = rnd(cin, seed=17), rnd(cin, seed=18)
+    pad = k // 2
+    xin = torch.relu(x * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)) if prologue else x
+    ref = F.conv2d(xin, w, stride=stride, padding=pad)
+    ref_abs = F.conv2d(xin.abs(), w.abs(), stride=stride, padding=pad)
+    Ho = ref.shape[2]
+    x_nhwc = x.permute(0, 2, 3, 1).contiguous().float().to(DEV)
+    wp = torch.empty(cout, k, k, cin, device=DEV)
+    K.conv_weight_pack(w.float().to(DEV).contiguous(), wp)
+    out = torch.empty(N * Ho * Ho, cout, device=DEV)
+    geo = dict(N=N, H=hw, W=hw, Cin=cin, KH=k, KW=k, stride=stride, pad=pad, Ho=Ho, Wo=Ho)
+    K.gemm(K.problem(N * Ho * Ho, cout, k * k * cin, x_nhwc, 0, wp, k * k * cin, out, cout, conv=geo,
+                     in_scale=sc.float().to(DEV) if prologue else None,
+                     in_shift=sh.float().to(DEV) if prologue else None), 2, 0, 0)
+    got = out.view(N, Ho, Ho, cout).permute(0, 3, 1, 2)
+    check(got, ref, ref_abs, f"conv{k}x{k}/s{stride}")
+
+
+def test_conv1_nchw_gather():
+    K = _K()
+    N, H = 2, 40
+    x = rnd(N, 3, H, H, seed=19)
+    w = rnd(64, 3, 7, 7, seed=20) * 0.1
+    ref = F.conv2d(x, w, stride=2, padding=3)
+    ref_abs = F.conv2d(x.abs(), w.abs(), stride=2, padding=3)
+    Ho = ref.shape[2]
+    out = torch.empty(N * Ho * Ho, 64, device=DEV)
+    geo = dict(N=N, H=H, W=H, Cin=3, KH=7, KW=7, stride=2, pad=3, Ho=Ho, Wo=Ho)
+    K.gemm(K.problem(N * Ho * Ho, 64, 147, x.float().to(DEV).contiguous(), 0, w.float().to(DEV).contiguous(),
+                     147, out, 64, conv=geo), 3, 0, 0)
+    check(out.view(N, Ho, Ho, 64).permute(0, 3, 1, 2), ref, ref_abs, "conv1 NCHW gather")

