@@ -20,9 +20,9 @@ c_ull = ctypes.c_ulonglong
 
 CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_A_CONV_NHWC, CAPMI_A_CONV_NCHW = 0, 1, 2, 3
 CAPMI_B_NMAJOR_W, CAPMI_B_KROWS = 0, 1
-CAPMI_TILE_128, CAPMI_TILE_64 = 0, 1
+CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO = 0, 1, 2, 3
 CAPMI_MAX_GROUP = 4
-CAPMI_COLSUM_ROWS = 256
+CAPMI_COLSUM_GROUPS = 64
 ABI_VERSION = 1
 
 
@@ -50,7 +50,7 @@ _SIGS = {
     "capmi_colsum": [c_vp, c_int, c_int, c_ll, c_float, c_vp, c_vp, c_int, c_vp],
     "capmi_conv_weight_pack": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_bn_finalize": [c_vp, c_int, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_float, c_float,
-                          c_vp, c_vp, c_vp, c_vp, c_vp],
+                          c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "capmi_bn_eval_params": [c_vp, c_vp, c_vp, c_vp, c_int, c_float, c_vp, c_vp, c_vp],
     "capmi_bn_add_relu": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_vp],
     "capmi_bn_relu_maxpool": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
@@ -67,8 +67,9 @@ _SIGS = {
     "capmi_mask_rows_tb": [c_vp, c_vp, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_vp],
     "capmi_ce_fwd_bwd": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp,
                          c_int, c_vp, c_vp],
+    "capmi_alpha_reg_parts": [c_int, c_int],
     "capmi_alpha_reg": [c_vp, c_int, c_int, c_int, c_float, c_vp, c_vp, c_vp],
-    "capmi_loss_finalize": [c_vp, c_int, c_int, c_vp, c_vp, c_vp],
+    "capmi_loss_finalize": [c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp],
     "capmi_lstm_cell_bwd": [c_vp, c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int,
                             c_vp, c_vp, c_vp],
     "capmi_att_ctx_bwd": [c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp],

@@ -174,9 +174,9 @@ class DecoderCore:
         K.splitk_reduce(slab[sh * B * D:], sh, B * D, B, D, D, ws.C[0], D, bias=p["c_lin.bias"])
         # hoisted enc_att (:54) and the embedding half of the LSTM input GEMM
         K.gemm(K.problem(B * P, A, E, enc, E, p["attention.enc_att.weight"], E, ws.ATT_ENC, A,
-                         bias=p["attention.enc_att.bias"]), AK, BW, K.TILE_128)
+                         bias=p["attention.enc_att.bias"]), AK, BW, K.TILE_AUTO)
         K.gemm(K.problem(T * B, 4 * D, M, ws.X, X, W_ih, X, ws.XEMB, 4 * D, bias=p["decode_step.bias_ih"],
-                         bias2=p["decode_step.bias_hh"]), AK, BW, K.TILE_128)
+                         bias2=p["decode_step.bias_hh"]), AK, BW, K.TILE_AUTO)
 
         alphas = torch.empty(B, T, P, device=enc.device, dtype=torch.float32)
         s_a, s_g, s_hh = dm.s_h
@@ -209,7 +209,7 @@ class DecoderCore:
             Hd = Hcur
         preds = torch.empty(B, T, V, device=enc.device, dtype=torch.float32)
         K.gemm(K.problem(T * B, V, D, Hd, D, p["fc.weight"], D, preds, T * V, c_r1=B, c_s2=V,
-                         bias=p["fc.bias"]), AK, BW, K.TILE_128)
+                         bias=p["fc.bias"]), AK, BW, K.TILE_AUTO)
         if ragged:
             K.mask_rows_tb(preds, bt_dev, T, B, V, T * V, B, V)
         state = dict(dm=dm, ws=ws, enc=enc, caps=caps, bt=bt, bt_dev=bt_dev, ragged=ragged, alphas=alphas,

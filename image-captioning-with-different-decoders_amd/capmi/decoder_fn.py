@@ -100,7 +100,7 @@ class FusedStepState:
             f = dict(device=device, dtype=torch.float32)
             self.loss_rows = torch.empty(B * T, **f)
             self.dlogits = torch.empty(T * B, V, **f)
-            self.reg = torch.empty(1, **f)
+            self.reg = torch.empty(K.alpha_reg_parts(B, P), **f)
             self.dreg = torch.empty(B, P, **f)
             self.loss = torch.empty(1, **f)
             self.key = key

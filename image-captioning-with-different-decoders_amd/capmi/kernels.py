@@ -7,8 +7,8 @@ import ctypes
 
 import torch
 
-from ._lib import (CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W, CAPMI_COLSUM_ROWS, CAPMI_TILE_128, CAPMI_TILE_64,
-                   GemmProblem, call, lib)
+from ._lib import (CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W, CAPMI_COLSUM_GROUPS, CAPMI_TILE_128, CAPMI_TILE_64,
+                   CAPMI_TILE_128x64, CAPMI_TILE_AUTO, GemmProblem, call, lib)
 
 F32 = torch.float32
 
@@ -69,8 +69,9 @@ def stat_tiles(M, tile=CAPMI_TILE_128):
 
 
 def tiles_for(M, N, tile):
-    bm = 128 if tile == CAPMI_TILE_128 else 64
-    return ((M + bm - 1) // bm) * ((N + bm - 1) // bm)
+    bm = 64 if tile == CAPMI_TILE_64 else 128
+    bn = 128 if tile == CAPMI_TILE_128 else 64
+    return ((M + bm - 1) // bm) * ((N + bn - 1) // bn)
 
 
 def splitk_reduce(inp, S, slab, rows, cols, ld_in, out, ld_out, bias=None):
@@ -80,7 +81,7 @@ def splitk_reduce(inp, S, slab, rows, cols, ld_in, out, ld_out, bias=None):
 
 
 def colsum_work_size(rows, cols):
-    return max(1, (rows + CAPMI_COLSUM_ROWS - 1) // CAPMI_COLSUM_ROWS) * cols
+    return CAPMI_COLSUM_GROUPS * cols
 
 
 def colsum(inp, rows, cols, ld, out, work, scale=1.0, accumulate=False):
@@ -99,12 +100,18 @@ def conv_weight_pack(w, out):
     call("capmi_conv_weight_pack", ptr(w), co, ci, kh, kw, ptr(out), stream())
 
 
+def bn_work_doubles(C):
+    return 128 * 2 * C
+
+
 def bn_finalize(stats, tiles, C, count, gamma, beta, running_mean, running_var, momentum, eps,
-                scale, shift, save_mean=None, save_var=None):
+                scale, shift, work, save_mean=None, save_var=None):
     _cuda(stats, gamma, beta, running_mean, running_var, scale, shift, save_mean, save_var)
+    _cuda(work, dtype=torch.float64)
+    assert work.numel() >= bn_work_doubles(C)
     call("capmi_bn_finalize", ptr(stats), tiles, C, count, ptr(gamma), ptr(beta), ptr(running_mean),
          ptr(running_var), momentum, eps, ptr(scale), ptr(shift), ptr(save_mean), ptr(save_var),
-         stream())
+         ptr(work), stream())
 
 
 def bn_eval_params(gamma, beta, rm, rv, C, eps, scale, shift):
@@ -186,14 +193,21 @@ def ce_fwd_bwd(logits, caps, B, T, L, V, bt_dev, nrows, loss_rows, lse=None, dlo
          ptr(lse), ptr(dlogits), int(dl_time_major), ptr(gscale), stream())
 
 
-def alpha_reg(alphas, B, T, P, alpha_c, reg, dreg):
-    _cuda(alphas, reg, dreg)
-    call("capmi_alpha_reg", ptr(alphas), B, T, P, float(alpha_c), ptr(reg), ptr(dreg), stream())
+def alpha_reg_parts(B, P):
+    return lib.capmi_alpha_reg_parts(B, P)
 
 
-def loss_finalize(loss_rows, n, nrows, reg, out):
-    _cuda(loss_rows, reg, out)
-    call("capmi_loss_finalize", ptr(loss_rows), n, nrows, ptr(reg), ptr(out), stream())
+def alpha_reg(alphas, B, T, P, alpha_c, reg_part, dreg):
+    """reg_part: alpha_reg_parts(B, P) floats whose sum is the regulariser value."""
+    _cuda(alphas, reg_part, dreg)
+    assert reg_part is None or reg_part.numel() >= alpha_reg_parts(B, P)
+    call("capmi_alpha_reg", ptr(alphas), B, T, P, float(alpha_c), ptr(reg_part), ptr(dreg), stream())
+
+
+def loss_finalize(loss_rows, n, nrows, reg_part, out):
+    _cuda(loss_rows, reg_part, out)
+    call("capmi_loss_finalize", ptr(loss_rows), n, nrows, ptr(reg_part),
+         0 if reg_part is None else reg_part.numel(), ptr(out), stream())
 
 
 def lstm_cell_bwd(dhd, dh_part, S, slab, dc_in, act, c_prev, c_cur, B, D, bt, dgates, dc_out):
@@ -249,4 +263,4 @@ def embed_scatter_add(dx, ld_dx, caps, B, L, T, bt_dev, M, demb):
          int(demb.dtype == torch.float64), stream())
 
 
-TILE_128, TILE_64 = CAPMI_TILE_128, CAPMI_TILE_64
+TILE_128, TILE_64, TILE_128x64, TILE_AUTO = CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO

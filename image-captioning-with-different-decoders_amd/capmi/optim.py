@@ -33,18 +33,23 @@ class Adam:
         self.flats = []  # (dtype, p_flat, g_flat, m, v, [(param, offset, numel)])
         for dt in sorted({p.dtype for p in params}, key=str):
             ps = [p for p in params if p.dtype == dt]
-            n = sum(p.numel() for p in ps)
-            dev = ps[0].device
-            pf = torch.empty(n, device=dev, dtype=dt)
-            gf = torch.zeros(n, device=dev, dtype=dt)
-            layout, off = [], 0
+            # every tensor starts on a 256-byte boundary (the kernels' 16-B vector loads and
+            # their coalescing need aligned operands); the gaps stay zero and are never read
+            al = 256 // torch.empty(0, dtype=dt).element_size()
+            offs, n = [], 0
             for p in ps:
+                offs.append(n)
+                n += (p.numel() + al - 1) // al * al
+            dev = ps[0].device
+            pf = torch.zeros(n, device=dev, dtype=dt)
+            gf = torch.zeros(n, device=dev, dtype=dt)
+            layout = []
+            for p, off in zip(ps, offs):
                 k = p.numel()
                 pf[off:off + k].copy_(p.detach().reshape(-1))
                 p.data = pf[off:off + k].view_as(p)
                 p.grad = gf[off:off + k].view_as(p)
                 layout.append((p, off, k))
-                off += k
             self.flats.append([dt, pf, gf, torch.zeros_like(pf), torch.zeros_like(pf), layout])
 
     # ------------------------------------------------------------------

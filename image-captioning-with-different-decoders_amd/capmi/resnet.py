@@ -131,7 +131,8 @@ class EncoderRunner:
             big = max(big, N * ((H1 + 1) // 2) * ((W1 + 1) // 2) * 256)
             f = dict(device=device, dtype=torch.float32)
             ws = {n: torch.empty(big, **f) for n in ("x", "y1", "y2", "y3", "yd", "out")}
-            ws["stats"] = torch.empty(2 * ((N * H1 * W1 + 127) // 128) * 256, **f)
+            ws["stats"] = torch.empty(2 * ((N * H1 * W1 + 63) // 64) * 256, **f)
+            ws["bnwork"] = torch.empty(K.bn_work_doubles(2048), device=device, dtype=torch.float64)
             ws["ss"] = {}
             self._ws, self._ws_key = ws, key
         return self._ws
@@ -149,11 +150,12 @@ class EncoderRunner:
         s, b = self._ss(ws, bn)
         C = bn.num_features
         if train:
-            tiles = K.stat_tiles(rows, K.TILE_128)
+            tiles = K.stat_tiles(rows)
             mom = 0.1 if bn.momentum is None else bn.momentum
             K.bn_finalize(ws["stats"], tiles, C, rows, bn.weight, bn.bias,
                           bn.running_mean if bn.track_running_stats else None,
-                          bn.running_var if bn.track_running_stats else None, mom, bn.eps, s, b)
+                          bn.running_var if bn.track_running_stats else None, mom, bn.eps, s, b,
+                          ws["bnwork"])
         else:
             K.bn_eval_params(bn.weight, bn.bias, bn.running_mean, bn.running_var, C, bn.eps, s, b)
         return s, b
@@ -178,7 +180,7 @@ class EncoderRunner:
             sc, sh = in_ss if in_ss is not None else (None, None)
             prob = K.problem(rows, co, Kd, x, 0, w, Kd, out, co, conv=geo, in_scale=sc, in_shift=sh, **kw_)
             mode = CAPMI_A_CONV_NHWC
-        launch = lambda: K.gemm(prob, mode, CAPMI_B_NMAJOR_W, K.TILE_128)  # noqa: E731
+        launch = lambda: K.gemm(prob, mode, CAPMI_B_NMAJOR_W, K.TILE_AUTO)  # noqa: E731
         if self.conv_hook is not None:
             self.conv_hook(tag, 2.0 * rows * co * Kd, launch)
         else:

@@ -42,24 +42,31 @@ extern "C" int capmi_embed_gather(const void* emb, int emb_is_f64, int M, const 
 }
 
 // --------------------------------------------------------------------------------------
-__global__ void mean_rows_kernel(const float* __restrict__ enc, int B, int P, int E,
-                                 float* __restrict__ out) {
-  const long long n = (long long)B * E;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int e = (int)(i % E), b = (int)(i / E);
-    const float* p = enc + (long long)b * P * E + e;
-    float s = 0.f;
-    for (int q = 0; q < P; ++q) s += p[(long long)q * E];
-    out[i] = s / (float)P;
+__global__ void __launch_bounds__(256) mean_rows_kernel(const float* __restrict__ enc, int B, int P,
+                                                        int E, float* __restrict__ out) {
+  __shared__ float4 part[4][64];
+  const int b = blockIdx.y, c4 = threadIdx.x & 63, pg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + c4 * 4;
+  float4 acc = f4(0.f);
+  if (c < E) {
+    const float* base = enc + (long long)b * P * E + c;
+    for (int p = pg; p < P; p += 4) acc = acc + *reinterpret_cast<const float4*>(base + (long long)p * E);
+  }
+  part[pg][c4] = acc;
+  __syncthreads();
+  if (pg == 0 && c < E) {
+    const float4 s = ((part[0][c4] + part[1][c4]) + part[2][c4]) + part[3][c4];
+    const float inv = (float)P;
+    *reinterpret_cast<float4*>(out + (long long)b * E + c) =
+        make_float4(s.x / inv, s.y / inv, s.z / inv, s.w / inv);
   }
 }
 
 extern "C" int capmi_mean_rows(const float* enc, int B, int P, int E, float* out, void* stream) {
   CAPMI_REQUIRE(enc && out && B > 0 && P > 0 && E > 0, CAPMI_EINVAL);
-  const long long n = (long long)B * E;
-  hipLaunchKernelGGL(mean_rows_kernel, dim3(std::min<long long>(cdiv(n, 256), 4096)), dim3(256), 0,
-                     as_stream(stream), enc, B, P, E, out);
+  CAPMI_REQUIRE(E % 4 == 0 && aligned16(enc) && aligned16(out), CAPMI_EALIGN);
+  hipLaunchKernelGGL(mean_rows_kernel, dim3(cdiv(E, 256), B), dim3(256), 0, as_stream(stream), enc, B,
+                     P, E, out);
   CAPMI_LAUNCH_CHECK();
   return 0;
 }
@@ -370,52 +377,59 @@ extern "C" int capmi_ce_fwd_bwd(const float* logits, const long long* caps, int 
 }
 
 // --------------------------------------------------------------------------------------
-// alpha regulariser ((alpha_c - sum_t alpha)^2).mean() and its gradient; single workgroup
+// alpha regulariser ((alpha_c - sum_t alpha)^2).mean() and its gradient; one thread per (b, p)
 // --------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(1024) alpha_reg_kernel(const float* __restrict__ alphas, int B,
-                                                         int T, int P, float alpha_c,
-                                                         float* __restrict__ reg,
-                                                         float* __restrict__ dreg) {
+__global__ void __launch_bounds__(256) alpha_reg_kernel(const float* __restrict__ alphas, int B,
+                                                        int T, int P, float alpha_c,
+                                                        float* __restrict__ reg_part,
+                                                        float* __restrict__ dreg) {
   __shared__ float red[16];
   const int n = B * P;
   const float inv = 1.f / (float)n;
+  const int i = blockIdx.x * 256 + threadIdx.x;
   float acc = 0.f;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+  if (i < n) {
     const int b = i / P, p = i - b * P;
+    const float* a = alphas + (long long)b * T * P + p;
     float s = 0.f;
-    for (int t = 0; t < T; ++t) s += alphas[((long long)b * T + t) * P + p];
+    for (int t = 0; t < T; ++t) s += a[(long long)t * P];
     const float d = alpha_c - s;
-    acc = fmaf(d, d, acc);
+    acc = d * d;
     if (dreg) dreg[i] = -2.f * d * inv;
   }
   acc = block_sum(acc, red);
-  if (threadIdx.x == 0 && reg) reg[0] = acc * inv;
+  if (threadIdx.x == 0 && reg_part) reg_part[blockIdx.x] = acc * inv;
 }
 
-extern "C" int capmi_alpha_reg(const float* alphas, int B, int T, int P, float alpha_c, float* reg,
-                               float* dreg, void* stream) {
+extern "C" int capmi_alpha_reg_parts(int B, int P) { return (int)cdiv((long long)B * P, 256); }
+
+extern "C" int capmi_alpha_reg(const float* alphas, int B, int T, int P, float alpha_c,
+                               float* reg_part, float* dreg, void* stream) {
   CAPMI_REQUIRE(alphas && B > 0 && T > 0 && P > 0, CAPMI_EINVAL);
-  hipLaunchKernelGGL(alpha_reg_kernel, dim3(1), dim3(1024), 0, as_stream(stream), alphas, B, T, P,
-                     alpha_c, reg, dreg);
+  hipLaunchKernelGGL(alpha_reg_kernel, dim3(cdiv((long long)B * P, 256)), dim3(256), 0,
+                     as_stream(stream), alphas, B, T, P, alpha_c, reg_part, dreg);
   CAPMI_LAUNCH_CHECK();
   return 0;
 }
 
 __global__ void __launch_bounds__(1024) loss_finalize_kernel(const float* __restrict__ rows, int n,
                                                              float inv_n, const float* __restrict__ reg,
-                                                             float* __restrict__ out) {
+                                                             int nreg, float* __restrict__ out) {
   __shared__ float red[16];
   float s = 0.f;
   for (int i = threadIdx.x; i < n; i += blockDim.x) s += rows[i];
   s = block_sum(s, red);
-  if (threadIdx.x == 0) out[0] = s * inv_n + (reg ? reg[0] : 0.f);
+  float r = 0.f;
+  for (int i = threadIdx.x; i < nreg; i += blockDim.x) r += reg[i];
+  r = block_sum(r, red);
+  if (threadIdx.x == 0) out[0] = s * inv_n + r;
 }
 
-extern "C" int capmi_loss_finalize(const float* loss_rows, int n, int nrows, const float* reg,
-                                   float* out, void* stream) {
-  CAPMI_REQUIRE(loss_rows && out && n > 0 && nrows > 0, CAPMI_EINVAL);
+extern "C" int capmi_loss_finalize(const float* loss_rows, int n, int nrows, const float* reg_part,
+                                   int nreg, float* out, void* stream) {
+  CAPMI_REQUIRE(loss_rows && out && n > 0 && nrows > 0 && (nreg == 0 || reg_part), CAPMI_EINVAL);
   hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), 0, as_stream(stream), loss_rows, n,
-                     1.f / (float)nrows, reg, out);
+                     1.f / (float)nrows, reg_part, nreg, out);
   CAPMI_LAUNCH_CHECK();
   return 0;
 }

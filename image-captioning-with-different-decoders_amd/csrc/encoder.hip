@@ -35,20 +35,20 @@ extern "C" int capmi_conv_weight_pack(const float* w, int Cout, int Cin, int KH,
 }
 
 // ---------------------------------------------------------------------------------
-// BN finalize: 16 channels x 16 tile-lanes per 256-thread block, fp64 combine.
+// BN finalize, two stages: (1) G slice-groups x 64 channels, fp64 partial sums per group;
+// (2) per channel: combine the G partials, mean/var -> scale/shift, running stats.
 // ---------------------------------------------------------------------------------
-__global__ void bn_finalize_kernel(const float* __restrict__ stats, int tiles, int C,
-                                   long long count, const float* __restrict__ gamma,
-                                   const float* __restrict__ beta, float* running_mean,
-                                   float* running_var, float momentum, float eps,
-                                   float* __restrict__ scale, float* __restrict__ shift,
-                                   float* save_mean, float* save_var) {
-  __shared__ double rs[16][17], rq[16][17];
-  const int cl = threadIdx.x & 15, tl = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
+constexpr int BNF_MAXG = 32;
+
+__global__ void bn_stats_stage1(const float* __restrict__ stats, int tiles, int C, int per_g,
+                                double* __restrict__ part) {
+  __shared__ double rs[4][64], rq[4][64];
+  const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int t0 = blockIdx.y * per_g, t1 = min(tiles, t0 + per_g);
   double s = 0.0, q = 0.0;
   if (c < C) {
-    for (int t = tl; t < tiles; t += 16) {
+    for (int t = t0 + tl; t < t1; t += 4) {
       const float2 v = *reinterpret_cast<const float2*>(stats + ((long long)t * C + c) * 2);
       s += v.x;
       q += v.y;
@@ -58,39 +58,59 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int tiles, i
   rq[tl][cl] = q;
   __syncthreads();
   if (tl == 0 && c < C) {
-    for (int i = 1; i < 16; ++i) {
-      s += rs[i][cl];
-      q += rq[i][cl];
-    }
-    const double n = (double)count;
-    const double mean = s / n;
-    double var = q / n - mean * mean;
-    if (var < 0) var = 0;
-    const double inv = 1.0 / sqrt(var + (double)eps);
-    const float sc = (float)((double)gamma[c] * inv);
-    scale[c] = sc;
-    shift[c] = (float)((double)beta[c] - mean * (double)sc);
-    if (save_mean) save_mean[c] = (float)mean;
-    if (save_var) save_var[c] = (float)var;
-    if (running_mean) {
-      const double unb = count > 1 ? var * n / (n - 1.0) : var;
-      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-      running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
-    }
+    s = rs[0][cl] + rs[1][cl] + rs[2][cl] + rs[3][cl];
+    q = rq[0][cl] + rq[1][cl] + rq[2][cl] + rq[3][cl];
+    part[((long long)blockIdx.y * C + c) * 2 + 0] = s;
+    part[((long long)blockIdx.y * C + c) * 2 + 1] = q;
+  }
+}
+
+__global__ void bn_stats_stage2(const double* __restrict__ part, int G, int C, long long count,
+                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                float* running_mean, float* running_var, float momentum, float eps,
+                                float* __restrict__ scale, float* __restrict__ shift,
+                                float* save_mean, float* save_var) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int g = 0; g < G; ++g) {
+    s += part[((long long)g * C + c) * 2 + 0];
+    q += part[((long long)g * C + c) * 2 + 1];
+  }
+  const double n = (double)count;
+  const double mean = s / n;
+  double var = q / n - mean * mean;
+  if (var < 0) var = 0;
+  const double inv = 1.0 / sqrt(var + (double)eps);
+  const float sc = (float)((double)gamma[c] * inv);
+  scale[c] = sc;
+  shift[c] = (float)((double)beta[c] - mean * (double)sc);
+  if (save_mean) save_mean[c] = (float)mean;
+  if (save_var) save_var[c] = (float)var;
+  if (running_mean) {
+    const double unb = count > 1 ? var * n / (n - 1.0) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
   }
 }
 
 extern "C" int capmi_bn_finalize(const float* stats, int tiles, int C, long long count,
                                  const float* gamma, const float* beta, float* running_mean,
                                  float* running_var, float momentum, float eps, float* scale,
-                                 float* shift, float* save_mean, float* save_var, void* stream) {
-  CAPMI_REQUIRE(stats && gamma && beta && scale && shift && tiles > 0 && C > 0 && count > 0,
+                                 float* shift, float* save_mean, float* save_var, void* work,
+                                 void* stream) {
+  CAPMI_REQUIRE(stats && gamma && beta && scale && shift && work && tiles > 0 && C > 0 && count > 0,
                 CAPMI_EINVAL);
   CAPMI_REQUIRE((running_mean == nullptr) == (running_var == nullptr), CAPMI_EINVAL);
-  CAPMI_REQUIRE(((uintptr_t)stats & 7) == 0, CAPMI_EALIGN);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 16)), dim3(256), 0, as_stream(stream), stats,
-                     tiles, C, count, gamma, beta, running_mean, running_var, momentum, eps, scale,
-                     shift, save_mean, save_var);
+  CAPMI_REQUIRE(((uintptr_t)stats & 7) == 0 && ((uintptr_t)work & 7) == 0, CAPMI_EALIGN);
+  const int G = std::min(BNF_MAXG, std::max(1, (tiles + 31) / 32));
+  const int per_g = (tiles + G - 1) / G;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(bn_stats_stage1, dim3(cdiv(C, 64), G), dim3(256), 0, s, stats, tiles, C, per_g,
+                     (double*)work);
+  hipLaunchKernelGGL(bn_stats_stage2, dim3(cdiv(C, 256)), dim3(256), 0, s, (const double*)work, G, C,
+                     count, gamma, beta, running_mean, running_var, momentum, eps, scale, shift,
+                     save_mean, save_var);
   CAPMI_LAUNCH_CHECK();
   return 0;
 }

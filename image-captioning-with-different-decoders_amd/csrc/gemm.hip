@@ -16,22 +16,9 @@
 // while tile t is multiplied out of LDS, one barrier per K-tile.
 #include "common.h"
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-struct GemmArgs {
-  capmi_gemm_problem p[CAPMI_MAX_GROUP];
-  int tiles_begin[CAPMI_MAX_GROUP + 1];
-  int tiles_m[CAPMI_MAX_GROUP];
-  int tiles_n[CAPMI_MAX_GROUP];
-  int kchunk[CAPMI_MAX_GROUP];
-  int nprob;
-};
+#include "gemm_args.h"
 
 constexpr int BK = 16;
-
-__device__ __forceinline__ long long remap(long long r, long long r1, long long ld, long long s2) {
-  return r1 > 0 ? (r % r1) * ld + (r / r1) * s2 : r * ld;
-}
 
 template <int AMODE> struct APad { static constexpr int v = 2; };
 template <> struct APad<1> { static constexpr int v = 4; };
@@ -313,32 +300,46 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmArgs args) {
     }
   }
   if (want_stats) {
-    // reduce over the two half-waves, then over the waves that share these columns
+    // per-channel (sum, sumsq) per 64-row slice, as gemm_nt.hip
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       csum[j] += __shfl_xor(csum[j], 32, 64);
       csq[j] += __shfl_xor(csq[j], 32, 64);
     }
-    if (lk == 0) {
+    if (WM == 64) {
+      if (lk == 0) {
+        const long long sl = (m0 + wm0) >> 6;
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        red[wid][0][32 * j + lr] = csum[j];
-        red[wid][1][32 * j + lr] = csq[j];
+        for (int j = 0; j < TN; ++j) {
+          const int col = n0 + wn0 + 32 * j + lr;
+          if (col < N && m0 + wm0 < M) {
+            P.stats[(sl * N + col) * 2 + 0] = csum[j];
+            P.stats[(sl * N + col) * 2 + 1] = csq[j];
+          }
+        }
       }
-    }
-    __syncthreads();
-    constexpr int NWM = BM / WM;
-    for (int c = tid; c < BN; c += 256) {
-      const int wn = c / WN, cc = c % WN;
-      float s = 0.f, q = 0.f;
-      for (int w = 0; w < NWM; ++w) {
-        s += red[w * NWN + wn][0][cc];
-        q += red[w * NWN + wn][1][cc];
+    } else {
+      if (lk == 0) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          red[wid][0][32 * j + lr] = csum[j];
+          red[wid][1][32 * j + lr] = csq[j];
+        }
       }
-      const int col = n0 + c;
-      if (col < N) {
-        P.stats[((long long)tm * N + col) * 2 + 0] = s;
-        P.stats[((long long)tm * N + col) * 2 + 1] = q;
+      __syncthreads();
+      constexpr int NWM = BM / WM;
+      for (int c = tid; c < BN; c += 256) {
+        const int wn = c / WN, cc = c % WN;
+        float s = 0.f, q = 0.f;
+        for (int w = 0; w < NWM; ++w) {
+          s += red[w * NWN + wn][0][cc];
+          q += red[w * NWN + wn][1][cc];
+        }
+        const int col = n0 + c;
+        if (col < N) {
+          P.stats[((long long)tm * N + col) * 2 + 0] = s;
+          P.stats[((long long)tm * N + col) * 2 + 1] = q;
+        }
       }
     }
   }
@@ -368,21 +369,29 @@ static int launch_mode(const GemmArgs& a, int amode, int bmode, bool vec, int bl
 }
 
 extern "C" int capmi_gemm_stat_tiles(int M, int tile) {
-  const int BM = tile == CAPMI_TILE_128 ? 128 : 64;
-  return (M + BM - 1) / BM;
+  // statistics rows are always kept per 64-row slice, whatever tile ran (see capmi.h)
+  (void)tile;
+  return (M + 63) / 64;
+}
+
+static long long tiles_of(const capmi_gemm_problem* probs, int nprob, int bm, int bn) {
+  long long t = 0;
+  for (int i = 0; i < nprob; ++i)
+    t += (long long)((probs[i].M + bm - 1) / bm) * ((probs[i].N + bn - 1) / bn) * probs[i].ksplit;
+  return t;
 }
 
 extern "C" int capmi_gemm(const capmi_gemm_problem* probs, int nprob, int amode, int bmode,
                           int tile, void* stream) {
   CAPMI_REQUIRE(nprob >= 1 && nprob <= CAPMI_MAX_GROUP, CAPMI_EINVAL);
   CAPMI_REQUIRE(amode >= 0 && amode <= 3 && bmode >= 0 && bmode <= 1, CAPMI_EINVAL);
-  CAPMI_REQUIRE(tile == CAPMI_TILE_128 || tile == CAPMI_TILE_64, CAPMI_EINVAL);
-  const int BM = tile == CAPMI_TILE_128 ? 128 : 64, BN = BM;
+  CAPMI_REQUIRE(tile >= CAPMI_TILE_128 && tile <= CAPMI_TILE_AUTO, CAPMI_EINVAL);
   GemmArgs a;
   memset(&a, 0, sizeof(a));
   a.nprob = nprob;
   bool vec = true;
-  long long total = 0;
+  bool nt_ok = (amode == 0 || amode == 2) && bmode == 0;  // v2 kernel eligible
+  int maxN = 0;
   for (int i = 0; i < nprob; ++i) {
     const capmi_gemm_problem& p = probs[i];
     CAPMI_REQUIRE(p.M >= 0 && p.N >= 0 && p.K >= 0 && p.ksplit >= 1, CAPMI_EINVAL);
@@ -395,6 +404,8 @@ extern "C" int capmi_gemm(const capmi_gemm_problem* probs, int nprob, int amode,
       CAPMI_REQUIRE(aligned16(p.A), CAPMI_EALIGN);
       CAPMI_REQUIRE(p.in_scale == nullptr || (aligned16(p.in_scale) && aligned16(p.in_shift)),
                     CAPMI_EALIGN);
+      CAPMI_REQUIRE(aligned16(p.B) && p.ldb % 4 == 0, CAPMI_EALIGN);
+      nt_ok = nt_ok && p.cCin % 32 == 0;
     }
     if (amode == 3) {
       CAPMI_REQUIRE(p.K == p.cKH * p.cKW * p.cCin && p.M == p.cN * p.cHo * p.cWo, CAPMI_EINVAL);
@@ -408,13 +419,36 @@ extern "C" int capmi_gemm(const capmi_gemm_problem* probs, int nprob, int amode,
       vec = vec && aligned16(p.B) && p.ldb % 4 == 0 && p.K % 4 == 0;
     else
       vec = vec && aligned16(p.B) && p.ldb % 4 == 0 && p.N % 4 == 0;
-    if (amode == 2) CAPMI_REQUIRE(aligned16(p.B) && p.ldb % 4 == 0, CAPMI_EALIGN);
     a.p[i] = p;
-    a.tiles_m[i] = (p.M + BM - 1) / BM;
-    a.tiles_n[i] = (p.N + BN - 1) / BN;
+    maxN = std::max(maxN, p.N);
+  }
+  nt_ok = nt_ok && (vec || amode == 2);
+  int bm = 128, bn = 128;
+  if (tile == CAPMI_TILE_64) {
+    bm = bn = 64;
+  } else if (tile == CAPMI_TILE_128x64) {
+    bn = 64;
+  } else if (tile == CAPMI_TILE_AUTO) {
+    if (!nt_ok) {
+      bm = bn = (tiles_of(probs, nprob, 128, 128) >= 256 ? 128 : 64);
+    } else if (maxN > 64 && tiles_of(probs, nprob, 128, 128) >= 480) {
+      bm = bn = 128;
+    } else if (tiles_of(probs, nprob, 128, 64) >= 480) {
+      bn = 64;
+    } else {
+      bm = bn = 64;
+    }
+  }
+  if (!nt_ok && bm != bn) bn = bm = 128;
+  const int bk = nt_ok ? 32 : BK;
+  long long total = 0;
+  for (int i = 0; i < nprob; ++i) {
+    const capmi_gemm_problem& p = probs[i];
+    a.tiles_m[i] = (p.M + bm - 1) / bm;
+    a.tiles_n[i] = (p.N + bn - 1) / bn;
     int kc = (p.K + p.ksplit - 1) / p.ksplit;
-    kc = ((kc + BK - 1) / BK) * BK;
-    a.kchunk[i] = kc > 0 ? kc : BK;
+    kc = ((kc + bk - 1) / bk) * bk;
+    a.kchunk[i] = kc > 0 ? kc : bk;
     a.tiles_begin[i] = (int)total;
     total += (long long)a.tiles_m[i] * a.tiles_n[i] * p.ksplit;
   }
@@ -422,7 +456,8 @@ extern "C" int capmi_gemm(const capmi_gemm_problem* probs, int nprob, int amode,
   CAPMI_REQUIRE(total < (1LL << 31), CAPMI_ERANGE);
   if (total == 0) return 0;
   hipStream_t s = as_stream(stream);
-  if (tile == CAPMI_TILE_128) return launch_mode<128, 128, 64, 64>(a, amode, bmode, vec, (int)total, s);
+  if (nt_ok) return gemm_nt_launch(a, amode, bm, bn, (int)total, s);
+  if (bm == 128) return launch_mode<128, 128, 64, 64>(a, amode, bmode, vec, (int)total, s);
   return launch_mode<64, 64, 32, 32>(a, amode, bmode, vec, (int)total, s);
 }
 
@@ -456,16 +491,21 @@ extern "C" int capmi_splitk_reduce(const float* in, int S, long long slab, int r
   return 0;
 }
 
-// stage 1: work[blk_r][c] = sum over rows [blk_r*R, blk_r*R+R) ; stage 2: out[c] = scale*sum work
-__global__ void colsum_stage1(const float* __restrict__ in, int rows, int cols, long long ld,
+// stage 1: work[g][c] = sum of rows [g*R, g*R+R) (64 columns x 4 row-lanes per WG, <= 64 groups);
+// stage 2: out[c] = scale * sum_g work[g][c]
+__global__ void colsum_stage1(const float* __restrict__ in, int rows, int cols, long long ld, int R,
                               float* __restrict__ work) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
-  const int r0 = blockIdx.y * CAPMI_COLSUM_ROWS;
-  const int r1 = min(rows, r0 + CAPMI_COLSUM_ROWS);
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int r0 = blockIdx.y * R, r1 = min(rows, r0 + R);
   float s = 0.f;
-  for (int r = r0; r < r1; ++r) s += in[(long long)r * ld + c];
-  work[(long long)blockIdx.y * cols + c] = s;
+  if (c < cols)
+    for (int r = r0 + rl; r < r1; r += 4) s += in[(long long)r * ld + c];
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && c < cols)
+    work[(long long)blockIdx.y * cols + c] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
 }
 
 __global__ void colsum_stage2(const float* __restrict__ work, int nb, int cols, float scale,
@@ -482,11 +522,13 @@ extern "C" int capmi_colsum(const float* in, int rows, int cols, long long ld, f
                             float* work, float* out, int accumulate, void* stream) {
   CAPMI_REQUIRE(rows >= 0 && cols >= 0, CAPMI_EINVAL);
   if (cols == 0) return 0;
-  const int nb = rows > 0 ? (int)cdiv(rows, CAPMI_COLSUM_ROWS) : 0;
+  int R = std::max(64, (rows + CAPMI_COLSUM_GROUPS - 1) / CAPMI_COLSUM_GROUPS);
+  R = (R + 3) & ~3;
+  const int nb = rows > 0 ? (rows + R - 1) / R : 0;
   hipStream_t s = as_stream(stream);
   if (nb > 0)
-    hipLaunchKernelGGL(colsum_stage1, dim3(cdiv(cols, 256), nb), dim3(256), 0, s, in, rows, cols,
-                       ld, work);
+    hipLaunchKernelGGL(colsum_stage1, dim3(cdiv(cols, 64), nb), dim3(256), 0, s, in, rows, cols, ld, R,
+                       work);
   hipLaunchKernelGGL(colsum_stage2, dim3(cdiv(cols, 256)), dim3(256), 0, s, work, nb, cols, scale,
                      out, accumulate);
   CAPMI_LAUNCH_CHECK();

@@ -1,0 +1,21 @@
+// Launch descriptor shared by the GEMM kernels (gemm.hip, gemm_nt.hip).
+#pragma once
+#include "common.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct GemmArgs {
+  capmi_gemm_problem p[CAPMI_MAX_GROUP];
+  int tiles_begin[CAPMI_MAX_GROUP + 1];
+  int tiles_m[CAPMI_MAX_GROUP];
+  int tiles_n[CAPMI_MAX_GROUP];
+  int kchunk[CAPMI_MAX_GROUP];
+  int nprob;
+};
+
+__device__ __forceinline__ long long remap(long long r, long long r1, long long ld, long long s2) {
+  return r1 > 0 ? (r % r1) * ld + (r / r1) * s2 : r * ld;
+}
+
+// NT kernel (A K-major dense or NHWC conv, B = W[N][K]); BM x BN in {128x128, 128x64, 64x64}
+int gemm_nt_launch(const GemmArgs& a, int amode, int bm, int bn, int blocks, hipStream_t s);

@@ -1,0 +1,309 @@
+// GEMM v2 for the case that dominates the step: A K-major (dense rows, or the implicit
+// im2col of an NHWC activation) x B = W[N][K] (nn.Linear / packed conv weight), fp32 MFMA.
+//
+// vs the generic kernel (gemm.hip):
+//   * BK = 32 and an LDS image in the operands' own [row][k] layout (row stride 36 floats),
+//     so the global->LDS staging is float4 -> ds_write_b128 with no transpose;
+//   * the k order inside each 8-wide k-group is permuted so one ds_read_b128 per lane feeds
+//     four consecutive v_mfma_f32_32x32x2_f32: MFMA s of group g multiplies k = 8g+s (lanes
+//     0-31) and k = 8g+4+s (lanes 32-63), and lane (i, h) reads row i, k 8g+4h..8g+4h+3.
+//     Every k is used exactly once (A and B share the permutation), the 36-float stride
+//     makes the b128 reads conflict-free (36*i mod 64 distinct over each 16-lane group);
+//   * the next k-tile's global loads are only ISSUED at the top of a k-step (masked slots
+//     read a valid dummy address); masking and the fused BN-apply+ReLU prologue are applied
+//     when the registers are written to LDS, after the MFMAs, so load latency overlaps math;
+//   * the conv's (kh, kw, ci) walk is incremental (no integer division in the k loop) and
+//     every problem field is read once into registers before the loop;
+//   * tile shapes 128x128 / 128x64 / 64x64 (4 waves, 2x2) so grids of the small-M layers
+//     (ResNet layer3/layer4, M = 64*196 / 64*49) still fill 256 CUs with >= 2 WGs each;
+//   * XCD-aware block order: consecutive tiles (same A rows) land on one XCD's L2.
+// Numerics: unchanged (exact fp32 fmaf chains, different k order than any CPU library).
+#include "gemm_args.h"
+
+namespace {
+
+constexpr int BK2 = 32;
+constexpr int S2 = BK2 + 4;  // LDS row stride in floats
+
+template <int BM, int BN, int AMODE, bool PRO>
+__global__ void __launch_bounds__(256) gemm_nt_kernel(const GemmArgs args) {
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
+  constexpr int NA = BM * BK2 / 4 / 256, NB = BN * BK2 / 4 / 256;
+  static_assert(NA >= 1 && NB >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) float As[2][BM * S2];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * S2];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  int bid = blockIdx.x;
+  if (args.nprob == 1) {  // XCD-aware remap (bijective for any grid size)
+    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+  }
+  int pi = 0;
+  while (pi + 1 < args.nprob && bid >= args.tiles_begin[pi + 1]) ++pi;
+  const capmi_gemm_problem& P = args.p[pi];
+  const int local = bid - args.tiles_begin[pi];
+  const int tiles_n = args.tiles_n[pi], tiles_m = args.tiles_m[pi];
+  const int tn = local % tiles_n;
+  const int tm = (local / tiles_n) % tiles_m;
+  const int z = local / (tiles_n * tiles_m);
+  const int M = P.M, N = P.N;
+  const int k_begin = z * args.kchunk[pi];
+  const int k_end = min(P.K, k_begin + args.kchunk[pi]);
+  const int nkt = k_end > k_begin ? (k_end - k_begin + BK2 - 1) / BK2 : 0;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const float* __restrict__ Ag = P.A;
+  const float* __restrict__ Bg = P.B;
+  const long long ldb = P.ldb;
+  // conv geometry, read once
+  const int cH = P.cH, cW = P.cW, cCin = P.cCin, cKW = P.cKW;
+  const float* __restrict__ isc = P.in_scale;
+  const float* __restrict__ ish = P.in_shift;
+
+  // ---- staging slots: float4 f -> (row f>>3, k 4*(f&7)) ------------------------------
+  long long a_base[NA];  // dense: row offset; conv: image base offset
+  int a_ih0[NA], a_iw0[NA];
+  bool a_ok[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int row = m0 + ((tid + i * 256) >> 3);
+    a_ok[i] = row < M;
+    if (AMODE == 0) {
+      a_base[i] = a_ok[i] ? remap(row, P.a_r1, P.lda, P.a_s2) : 0;
+      a_ih0[i] = a_iw0[i] = 0;
+    } else {
+      const int hw = P.cHo * P.cWo;
+      const int n = row / hw, rem = row - n * hw;
+      const int oh = rem / P.cWo, ow = rem - oh * P.cWo;
+      a_ih0[i] = oh * P.cStride - P.cPad;
+      a_iw0[i] = ow * P.cStride - P.cPad;
+      a_base[i] = (long long)n * cH * cW * cCin;
+    }
+  }
+  const int kq = (tid & 7) * 4;
+  long long b_base[NB];
+  bool b_ok[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int n = n0 + ((tid + i * 256) >> 3);
+    b_ok[i] = n < N;
+    b_base[i] = b_ok[i] ? (long long)n * ldb : 0;
+  }
+  // conv k walk: k = ((kh * KW) + kw) * Cin + ci, advanced by BK2 per k-tile
+  int c_ci = 0, c_kh = 0, c_kw = 0;
+  if (AMODE == 2) {
+    const int kpos = k_begin / cCin;
+    c_ci = k_begin - kpos * cCin;
+    c_kh = kpos / cKW;
+    c_kw = kpos - c_kh * cKW;
+  }
+
+  float4 ra[NA], rb[NB], rsc = f4(1.f), rsh = f4(0.f);
+  unsigned amask = 0, bmask = 0;
+  auto load_tile = [&](int kt) {
+    const int k = k_begin + kt * BK2 + kq;
+    const bool kok = k < k_end;  // K % 4 == 0: a float4 is all-in or all-out
+    amask = 0;
+    bmask = 0;
+    if (AMODE == 0) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const bool ok = a_ok[i] && kok;
+        ra[i] = *reinterpret_cast<const float4*>(Ag + (ok ? a_base[i] + k : 0));
+        amask |= (unsigned)ok << i;
+      }
+    } else {
+      const int ci = c_ci + kq;
+      if (PRO) {
+        rsc = *reinterpret_cast<const float4*>(isc + ci);
+        rsh = *reinterpret_cast<const float4*>(ish + ci);
+      }
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int ih = a_ih0[i] + c_kh, iw = a_iw0[i] + c_kw;
+        const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
+        const long long off = a_base[i] + ((long long)(ih * cW + iw)) * cCin + ci;
+        ra[i] = *reinterpret_cast<const float4*>(Ag + (ok ? off : 0));
+        amask |= (unsigned)ok << i;
+      }
+      c_ci += BK2;  // advance the (kh, kw, ci) walk to the next k-tile
+      if (c_ci >= cCin) {
+        c_ci = 0;
+        if (++c_kw == cKW) {
+          c_kw = 0;
+          ++c_kh;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const bool ok = b_ok[i] && kok;
+      rb[i] = *reinterpret_cast<const float4*>(Bg + (ok ? b_base[i] + k : 0));
+      bmask |= (unsigned)ok << i;
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      float4 v = ra[i];
+      if (PRO) v = relu4(fma4(v, rsc, rsh));
+      if (!((amask >> i) & 1u)) v = f4(0.f);
+      *reinterpret_cast<float4*>(&As[buf][((tid + i * 256) >> 3) * S2 + kq]) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      float4 v = rb[i];
+      if (!((bmask >> i) & 1u)) v = f4(0.f);
+      *reinterpret_cast<float4*>(&Bs[buf][((tid + i * 256) >> 3) * S2 + kq]) = v;
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (nkt > 0) {
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int buf = kt & 1;
+      const bool more = kt + 1 < nkt;
+      if (more) load_tile(kt + 1);
+      const float* Ab = As[buf] + (wm0 + lr) * S2 + 4 * lh;
+      const float* Bb = Bs[buf] + (wn0 + lr) * S2 + 4 * lh;
+#pragma unroll
+      for (int g = 0; g < BK2 / 8; ++g) {
+        float4 a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const float4*>(Ab + 32 * i * S2 + 8 * g);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const float4*>(Bb + 32 * j * S2 + 8 * g);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              const float av = s == 0 ? a[i].x : s == 1 ? a[i].y : s == 2 ? a[i].z : a[i].w;
+              const float bv = s == 0 ? b[j].x : s == 1 ? b[j].y : s == 2 ? b[j].z : b[j].w;
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
+            }
+      }
+      if (more) store_tile(buf ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue (same contract as gemm.hip) -----------------------------------------
+  const float alpha = P.alpha * (P.alpha_ptr ? *P.alpha_ptr : 1.f);
+  float* Cz = P.C + (long long)z * P.c_split_stride;
+  const float* bias1 = P.bias;
+  const float* bias2 = P.bias2;
+  const float beta = P.beta;
+  const int relu = P.relu;
+  const long long ldc = P.ldc, c_r1 = P.c_r1, c_s2 = P.c_s2;
+  float csum[TN], csq[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    csum[j] = 0.f;
+    csq[j] = 0.f;
+    const int col = n0 + wn0 + 32 * j + lr;
+    const bool cok = col < N;
+    float bias = 0.f;
+    if (z == 0 && cok) {
+      if (bias1) bias += bias1[col];
+      if (bias2) bias += bias2[col];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (cok && row < M) {
+          float* cp = Cz + remap(row, c_r1, ldc, c_s2) + col;
+          float v = fmaf(acc[i][j][r], alpha, bias);
+          if (beta != 0.f) v = fmaf(beta, *cp, v);
+          if (relu) v = fmaxf(v, 0.f);
+          *cp = v;
+          csum[j] += v;
+          csq[j] = fmaf(v, v, csq[j]);
+        }
+      }
+    }
+  }
+  float* __restrict__ stats = P.stats;
+  if (stats != nullptr) {
+    // per-channel (sum, sumsq) of the stored values per 64-row slice: stats[slice][col][2]
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      csum[j] += __shfl_xor(csum[j], 32, 64);
+      csq[j] += __shfl_xor(csq[j], 32, 64);
+    }
+    if (WM == 64) {  // each wave row owns one slice
+      if (lh == 0) {
+        const long long sl = (m0 + wm0) >> 6;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = n0 + wn0 + 32 * j + lr;
+          if (col < N && m0 + wm0 < M) {
+            stats[(sl * N + col) * 2 + 0] = csum[j];
+            stats[(sl * N + col) * 2 + 1] = csq[j];
+          }
+        }
+      }
+    } else {  // BM == 64: both wave rows share slice tm
+      float* red = As[0];  // the K loop ended with a barrier: LDS is free
+      if (lh == 0) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          red[(wid * 2 + 0) * WN + 32 * j + lr] = csum[j];
+          red[(wid * 2 + 1) * WN + 32 * j + lr] = csq[j];
+        }
+      }
+      __syncthreads();
+      for (int c = tid; c < BN; c += 256) {
+        const int wn = c / WN, cc = c % WN;
+        const float s = red[((0 * 2 + wn) * 2 + 0) * WN + cc] + red[((1 * 2 + wn) * 2 + 0) * WN + cc];
+        const float q = red[((0 * 2 + wn) * 2 + 1) * WN + cc] + red[((1 * 2 + wn) * 2 + 1) * WN + cc];
+        const int col = n0 + c;
+        if (col < N) {
+          stats[((long long)tm * N + col) * 2 + 0] = s;
+          stats[((long long)tm * N + col) * 2 + 1] = q;
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN>
+int launch_bmbn(const GemmArgs& a, int amode, bool pro, int blocks, hipStream_t s) {
+  if (amode == 0)
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 0, false>), dim3(blocks), dim3(256), 0, s, a);
+  else if (pro)
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 2, true>), dim3(blocks), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 2, false>), dim3(blocks), dim3(256), 0, s, a);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace
+
+int gemm_nt_launch(const GemmArgs& a, int amode, int bm, int bn, int blocks, hipStream_t s) {
+  bool pro = false;
+  for (int i = 0; i < a.nprob; ++i) pro = pro || a.p[i].in_scale != nullptr;
+  for (int i = 0; i < a.nprob; ++i)
+    if (pro && a.p[i].in_scale == nullptr) return CAPMI_EINVAL;  // grouped: all or none
+  if (bm == 128 && bn == 128) return launch_bmbn<128, 128>(a, amode, pro, blocks, s);
+  if (bm == 128 && bn == 64) return launch_bmbn<128, 64>(a, amode, pro, blocks, s);
+  if (bm == 64 && bn == 64) return launch_bmbn<64, 64>(a, amode, pro, blocks, s);
+  return CAPMI_EINVAL;
+}

@@ -51,7 +51,8 @@ enum capmi_bmode {
   CAPMI_B_NMAJOR_W = 0, /* B[k][n] = W[n][k] (nn.Linear weight / packed conv weight), ldb = row stride of W */
   CAPMI_B_KROWS = 1     /* B[k][n] row-major, ldb = row stride */
 };
-enum capmi_tile { CAPMI_TILE_128 = 0, CAPMI_TILE_64 = 1 };
+/* tile: 128x128, 64x64, 128x64, or AUTO (chosen from the grid size; what the encoder uses) */
+enum capmi_tile { CAPMI_TILE_128 = 0, CAPMI_TILE_64 = 1, CAPMI_TILE_128x64 = 2, CAPMI_TILE_AUTO = 3 };
 
 typedef struct capmi_gemm_problem {
   int M, N, K;
@@ -64,7 +65,7 @@ typedef struct capmi_gemm_problem {
   const float* alpha_ptr;/* device scalar multiplying A*B, or NULL */
   float alpha, beta;     /* host scalars; beta != 0 reads C */
   int relu;
-  float* stats;          /* NULL or [ceil(M/BM)][N][2] per-tile (sum, sumsq) of the stored C (BN-train stats) */
+  float* stats;          /* NULL or [ceil(M/64)][N][2]: per 64-row slice (sum, sumsq) of the stored C (BN-train stats) */
   /* implicit-GEMM conv geometry (A = input activation, modes 2/3) */
   int cN, cH, cW, cCin, cKH, cKW, cStride, cPad, cHo, cWo;
   const float* in_scale; /* NULL or [Cin]: A element := relu(x*in_scale[ci] + in_shift[ci]) in-bounds (BN-apply+ReLU prologue) */
@@ -73,15 +74,15 @@ typedef struct capmi_gemm_problem {
 
 int capmi_gemm(const capmi_gemm_problem* problems, int nprob, int amode, int bmode, int tile,
                void* stream);
-/* rows of the per-tile statistics buffer capmi_gemm writes for a given M and tile */
+/* rows of the statistics buffer capmi_gemm writes for M rows: ceil(M/64) (tile ignored) */
 int capmi_gemm_stat_tiles(int M, int tile);
 
 /* sum of S partial slabs: out[r][c] = sum_s in[s*slab + r*ld_in + c] (+ bias[c]); rows x cols */
 int capmi_splitk_reduce(const float* in, int S, long long slab, int rows, int cols, long long ld_in,
                         const float* bias, float* out, long long ld_out, void* stream);
 /* column sums of a rows x cols row-major matrix (bias gradients): out[c] = scale * sum_r in[r*ld + c].
- * work must hold ceil(rows/CAPMI_COLSUM_ROWS) * cols floats. accumulate != 0 adds into out. */
-#define CAPMI_COLSUM_ROWS 256
+ * work must hold CAPMI_COLSUM_GROUPS * cols floats. accumulate != 0 adds into out. */
+#define CAPMI_COLSUM_GROUPS 64
 int capmi_colsum(const float* in, int rows, int cols, long long ld, float scale, float* work,
                  float* out, int accumulate, void* stream);
 
@@ -93,11 +94,13 @@ int capmi_colsum(const float* in, int rows, int cols, long long ld, float scale,
 int capmi_conv_weight_pack(const float* w, int Cout, int Cin, int KH, int KW, float* out, void* stream);
 /* BatchNorm2d(train) finalize from capmi_gemm stats: mean/var over `count` rows, then
  * scale = gamma*rsqrt(var+eps), shift = beta - mean*scale; running stats updated in place
- * (momentum, unbiased var) when running_mean != NULL. mean/var out (may be NULL). */
+ * (momentum, unbiased var) when running_mean != NULL. mean/var out (may be NULL).
+ * work: CAPMI_BN_WORK_DOUBLES(C) doubles of scratch. */
+#define CAPMI_BN_WORK_DOUBLES(C) (128 * 2 * (long long)(C))
 int capmi_bn_finalize(const float* stats, int tiles, int C, long long count, const float* gamma,
                       const float* beta, float* running_mean, float* running_var, float momentum,
                       float eps, float* scale, float* shift, float* save_mean, float* save_var,
-                      void* stream);
+                      void* work, void* stream);
 /* BatchNorm2d(eval): scale/shift from running statistics */
 int capmi_bn_eval_params(const float* gamma, const float* beta, const float* running_mean,
                          const float* running_var, int C, float eps, float* scale, float* shift,
@@ -155,12 +158,14 @@ int capmi_ce_fwd_bwd(const float* logits, const long long* caps, int B, int T, i
                      const int* bt, int nrows, float* loss_rows, float* lse, float* dlogits,
                      int dl_time_major, const float* gscale, void* stream);
 /* alpha regulariser ((alpha_c - sum_t alpha)^2).mean() over (B,P), alphas (B,T,P):
- * writes reg (1 float) and dreg[b][p] = -2 (alpha_c - sum_t alpha) / (B*P). */
-int capmi_alpha_reg(const float* alphas, int B, int T, int P, float alpha_c, float* reg,
+ * reg_part[g] = sum over workgroup g's (b,p) of (alpha_c - sum_t alpha)^2 / (B*P), g < capmi_alpha_reg_parts(B,P);
+ * dreg[b][p] = -2 (alpha_c - sum_t alpha) / (B*P). */
+int capmi_alpha_reg_parts(int B, int P);
+int capmi_alpha_reg(const float* alphas, int B, int T, int P, float alpha_c, float* reg_part,
                     float* dreg, void* stream);
-/* loss = sum(loss_rows[0:n]) / nrows + (reg ? reg[0] : 0) -> out[0] (single block, deterministic) */
-int capmi_loss_finalize(const float* loss_rows, int n, int nrows, const float* reg, float* out,
-                        void* stream);
+/* loss = sum(loss_rows[0:n]) / nrows + sum(reg_part[0:nreg]) -> out[0] (one workgroup, deterministic) */
+int capmi_loss_finalize(const float* loss_rows, int n, int nrows, const float* reg_part, int nreg,
+                        float* out, void* stream);
 
 /* ---- backward through time ---- */
 /* dh = dhd[b][:] (already dropout-masked, may be NULL) + sum_s dh_part[s][b][:]; dc = dc_in (NULL=0)

@@ -28,8 +28,9 @@ def rnd(*shape, seed=0):
     return torch.rand(*shape, generator=g, dtype=torch.float64) * 2 - 1
 
 
-@pytest.mark.parametrize("tile", [0, 1])
-@pytest.mark.parametrize("M,N,Kd", [(300, 200, 96), (64, 2048, 512), (129, 65, 50), (1, 7, 3)])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("M,N,Kd", [(300, 200, 96), (64, 2048, 512), (129, 65, 52), (129, 65, 50), (1, 7, 3),
+                                    (1000, 64, 300)])
 def test_linear_fwd(tile, M, N, Kd):
     K = _K()
     X, W, b, b2 = rnd(M, Kd, seed=1), rnd(N, Kd, seed=2), rnd(N, seed=3), rnd(N, seed=4)
@@ -89,24 +90,26 @@ def test_colsum():
     check(out, x.sum(0), x.abs().sum(0), "colsum")
 
 
-def test_bn_stats_epilogue():
+@pytest.mark.parametrize("tile", [0, 1, 2])
+def test_bn_stats_epilogue(tile):
     K = _K()
     M, N, Kd = 1000, 96, 64
     X, W = rnd(M, Kd, seed=13), rnd(N, Kd, seed=14)
     C = torch.empty(M, N, device=DEV)
     tiles = K.stat_tiles(M)
     stats = torch.empty(tiles, N, 2, device=DEV)
-    K.gemm(K.problem(M, N, Kd, X.float().to(DEV), Kd, W.float().to(DEV), Kd, C, N, stats=stats), 0, 0, 0)
+    K.gemm(K.problem(M, N, Kd, X.float().to(DEV), Kd, W.float().to(DEV), Kd, C, N, stats=stats), 0, 0, tile)
     Cd = C.double().cpu()
     s = stats.double().cpu().sum(0)
     torch.testing.assert_close(s[:, 0], Cd.sum(0), rtol=1e-5, atol=1e-3)
     torch.testing.assert_close(s[:, 1], (Cd * Cd).sum(0), rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("tile", [0, 3])
 @pytest.mark.parametrize("k,stride,cin,cout,hw,prologue", [
     (3, 1, 64, 64, 14, True), (3, 2, 128, 128, 15, True), (1, 2, 64, 256, 14, False),
-    (1, 1, 64, 256, 9, True)])
-def test_conv_nhwc(k, stride, cin, cout, hw, prologue):
+    (1, 1, 64, 256, 9, True), (3, 1, 48, 80, 7, True)])
+def test_conv_nhwc(k, stride, cin, cout, hw, prologue, tile):
     K = _K()
     N = 3
     x = rnd(N, cin, hw, hw, seed=15)
@@ -124,7 +127,7 @@ def test_conv_nhwc(k, stride, cin, cout, hw, prologue):
     geo = dict(N=N, H=hw, W=hw, Cin=cin, KH=k, KW=k, stride=stride, pad=pad, Ho=Ho, Wo=Ho)
     K.gemm(K.problem(N * Ho * Ho, cout, k * k * cin, x_nhwc, 0, wp, k * k * cin, out, cout, conv=geo,
                      in_scale=sc.float().to(DEV) if prologue else None,
-                     in_shift=sh.float().to(DEV) if prologue else None), 2, 0, 0)
+                     in_shift=sh.float().to(DEV) if prologue else None), 2, 0, tile)
     got = out.view(N, Ho, Ho, cout).permute(0, 3, 1, 2)
     check(got, ref, ref_abs, f"conv{k}x{k}/s{stride}")
 
