@@ -23,7 +23,7 @@ CAPMI_B_NMAJOR_W, CAPMI_B_KROWS = 0, 1
 CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO = 0, 1, 2, 3
 CAPMI_MAX_GROUP = 4
 CAPMI_COLSUM_GROUPS = 64
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class GemmProblem(ctypes.Structure):
@@ -63,7 +63,8 @@ _SIGS = {
                                   c_int, c_ll, c_vp, c_vp, c_vp, c_ll, c_vp],
     "capmi_lstm_cell_fwd": [c_vp, c_int, c_ll, c_vp, c_vp, c_int, c_ll, c_vp, c_int, c_int, c_vp,
                             c_vp, c_vp, c_vp],
-    "capmi_dropout": [c_vp, c_ll, c_float, c_ull, c_vp, c_vp],
+    "capmi_dropout": [c_vp, c_ll, c_float, c_ull, c_vp, c_vp, c_vp],
+    "capmi_counter_add": [c_vp, c_ll, c_vp],
     "capmi_mask_rows_tb": [c_vp, c_vp, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_vp],
     "capmi_ce_fwd_bwd": [c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp,
                          c_int, c_vp, c_vp],
@@ -77,10 +78,10 @@ _SIGS = {
                             c_int, c_vp, c_vp, c_vp],
     "capmi_att_enc_grad": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,
                            ctypes.POINTER(c_int), c_vp],
-    "capmi_adam_clamp": [c_vp, c_vp, c_vp, c_vp, c_ll, c_float, c_float, c_float, c_float, c_float,
-                         c_float, c_float, c_vp],
+    "capmi_adam_clamp": [c_vp, c_vp, c_vp, c_vp, c_ll, c_double, c_double, c_double, c_double, c_double,
+                         c_double, c_double, c_vp, c_vp],
     "capmi_adam_clamp_f64": [c_vp, c_vp, c_vp, c_vp, c_ll, c_double, c_double, c_double, c_double,
-                             c_double, c_double, c_double, c_vp],
+                             c_double, c_double, c_double, c_vp, c_vp],
     "capmi_embed_scatter_add": [c_vp, c_ll, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp],
     "capmi_strerror": [c_int],
     "capmi_abi_version": [],

@@ -143,7 +143,8 @@ class DecoderCore:
         K.splitk_reduce(ws.scratch, s, M * N, M, N, N, out, ld_out, bias=bias)
 
     # ------------------------------------------------------------------ forward
-    def forward(self, p, enc, caps, decode_lengths, *, dropout_p=0.0, training=False, seed=0):
+    def forward(self, p, enc, caps, decode_lengths, *, dropout_p=0.0, training=False, seed=0,
+                seed_dev=None):
         """p: dict name->tensor (PNAMES). enc: (B,P,E) contiguous fp32. caps: (B,L) int64.
         Returns (predictions (B,T,V), alphas (B,T,P), state)."""
         B, P, E = enc.shape
@@ -204,7 +205,7 @@ class DecoderCore:
         Hcur = ws.H[1:]
         if training and dropout_p > 0:
             Hd = torch.empty_like(Hcur)
-            K.dropout(Hcur, Hcur.numel(), dropout_p, seed, Hd)
+            K.dropout(Hcur, Hcur.numel(), dropout_p, seed, Hd, seed_dev=seed_dev)
         else:
             Hd = Hcur
         preds = torch.empty(B, T, V, device=enc.device, dtype=torch.float32)
@@ -213,7 +214,7 @@ class DecoderCore:
         if ragged:
             K.mask_rows_tb(preds, bt_dev, T, B, V, T * V, B, V)
         state = dict(dm=dm, ws=ws, enc=enc, caps=caps, bt=bt, bt_dev=bt_dev, ragged=ragged, alphas=alphas,
-                     Hd=Hd, dropout_p=dropout_p if training else 0.0, seed=seed)
+                     Hd=Hd, dropout_p=dropout_p if training else 0.0, seed=seed, seed_dev=seed_dev)
         return preds, alphas, state
 
     # ------------------------------------------------------------------ backward
@@ -251,7 +252,7 @@ class DecoderCore:
         if "fc.bias" in need:
             K.colsum(dpred, TB, V, V, grads["fc.bias"], ws.work)
         if st["dropout_p"] > 0:
-            K.dropout(ws.DHD, ws.DHD.numel(), st["dropout_p"], st["seed"], ws.DHD)
+            K.dropout(ws.DHD, ws.DHD.numel(), st["dropout_p"], st["seed"], ws.DHD, seed_dev=st["seed_dev"])
 
         # ---- backward through time
         s_dh = dm.s_dh

@@ -110,17 +110,20 @@ class FusedStepState:
 _FS = FusedStepState()
 
 
-def fused_loss_and_grads(dec, encoder_out, captions, caption_lengths, alpha_c, grads, need=None):
+def fused_loss_and_grads(dec, encoder_out, captions, caption_lengths, alpha_c, grads, need=None,
+                         seed_dev=None):
     """Forward + loss + backward of one decoder training step (models/attention.py:393-420).
 
     Writes d(loss)/d(param) into ``grads`` (name -> tensor, e.g. the optimizer's flat
-    views); returns (loss (1,) device tensor, predictions, alphas)."""
+    views); returns (loss (1,) device tensor, predictions, alphas). ``seed_dev``: an int64
+    device counter driving the dropout mask (graph-replayable); else a host seed is drawn."""
     enc, caps = _prep_inputs(dec, encoder_out, captions)
     p = decoder_params(dec)
     decode_lengths = [int(l) - 1 for l in caption_lengths]
     drop = dec.dropout.p if dec.training else 0.0
+    host_seed = 0x5EED if seed_dev is not None else (_seed() if drop > 0 else 0)
     preds, alphas, st = CORE.forward(p, enc, caps, decode_lengths, dropout_p=drop, training=dec.training,
-                                     seed=_seed() if drop > 0 else 0)
+                                     seed=host_seed, seed_dev=seed_dev)
     _GEN[0] += 1
     dm = st["dm"]
     B, T, V, P, L = dm.B, dm.T, dm.V, dm.P, dm.L

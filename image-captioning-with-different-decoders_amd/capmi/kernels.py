@@ -173,9 +173,17 @@ def lstm_cell_fwd(part, S, slab, xemb, hh_part, S2, slab2, c_prev, B, D, h_out, 
          D, ptr(h_out), ptr(c_out), ptr(act_out), stream())
 
 
-def dropout(inp, n, p, seed, out):
+def dropout(inp, n, p, seed, out, seed_dev=None):
+    """seed: host int; seed_dev: optional int64 device counter mixed into the seed (graphs)."""
     _cuda(inp, out)
-    call("capmi_dropout", ptr(inp), n, float(p), int(seed) & ((1 << 64) - 1), ptr(out), stream())
+    _cuda(seed_dev, dtype=torch.int64)
+    call("capmi_dropout", ptr(inp), n, float(p), int(seed) & ((1 << 64) - 1), ptr(seed_dev), ptr(out),
+         stream())
+
+
+def counter_add(counter, v=1):
+    _cuda(counter, dtype=torch.int64)
+    call("capmi_counter_add", ptr(counter), int(v), stream())
 
 
 def mask_rows_tb(x, bt_dev, T, B, cols, ld, r1=0, s2=0):
@@ -244,15 +252,13 @@ def att_enc_grad_blocks(B, P):
 # --------------------------------------------------------------------------------------
 # optimiser
 # --------------------------------------------------------------------------------------
-def adam_clamp(p, g, m, v, lr, beta1, beta2, eps, bc1, bc2_sqrt, clip):
-    if p.dtype == torch.float64:
-        _cuda(p, g, m, v, dtype=torch.float64)
-        call("capmi_adam_clamp_f64", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, beta1, beta2, eps,
-             bc1, bc2_sqrt, clip, stream())
-    else:
-        _cuda(p, g, m, v)
-        call("capmi_adam_clamp", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, beta1, beta2, eps, bc1,
-             bc2_sqrt, clip, stream())
+def adam_clamp(p, g, m, v, lr, beta1, beta2, eps, bc1, bc2_sqrt, clip, step_dev=None):
+    """step_dev: optional int64 device step counter (bias corrections computed on the device)."""
+    _cuda(step_dev, dtype=torch.int64)
+    name = "capmi_adam_clamp_f64" if p.dtype == torch.float64 else "capmi_adam_clamp"
+    _cuda(p, g, m, v, dtype=p.dtype)
+    call(name, ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), float(lr), float(beta1), float(beta2),
+         float(eps), float(bc1), float(bc2_sqrt), float(clip), ptr(step_dev), stream())
 
 
 def embed_scatter_add(dx, ld_dx, caps, B, L, T, bt_dev, M, demb):

@@ -29,7 +29,8 @@ class Adam:
         self.param_groups = [{"params": params, "lr": lr, "betas": betas, "eps": eps,
                               "weight_decay": 0, "amsgrad": False}]
         self.clip = math.inf
-        self.step_count = 0
+        # the step count lives on the device: step() is then replayable inside a HIP graph
+        self.step_dev = torch.zeros(1, dtype=torch.int64, device=params[0].device)
         self.flats = []  # (dtype, p_flat, g_flat, m, v, [(param, offset, numel)])
         for dt in sorted({p.dtype for p in params}, key=str):
             ps = [p for p in params if p.dtype == dt]
@@ -65,17 +66,18 @@ class Adam:
             for p, off, k in f[5]:
                 p.grad = f[2][off:off + k].view_as(p)
 
+    @property
+    def step_count(self):
+        return int(self.step_dev.item())
+
     @torch.no_grad()
     def step(self, closure=None):
-        self.step_count += 1
         g = self.param_groups[0]
         b1, b2 = g["betas"]
-        t = self.step_count
-        bc1 = 1 - b1 ** t
-        bc2s = math.sqrt(1 - b2 ** t)
         clip = self.clip if math.isfinite(self.clip) else 3.0e38
+        K.counter_add(self.step_dev, 1)
         for dt, pf, gf, m, v, _ in self.flats:
-            K.adam_clamp(pf, gf, m, v, g["lr"], b1, b2, g["eps"], bc1, bc2s, clip)
+            K.adam_clamp(pf, gf, m, v, g["lr"], b1, b2, g["eps"], 0.0, 0.0, clip, step_dev=self.step_dev)
 
     # ---- torch.optim.Adam-compatible state dict --------------------------
     def state_dict(self):
@@ -99,7 +101,7 @@ class Adam:
                 if st is not None:
                     m[off:off + k].copy_(st["exp_avg"].reshape(-1))
                     v[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
-                    self.step_count = int(float(st["step"]))
+                    self.step_dev.fill_(int(float(st["step"])))
                 i += 1
         pg = sd["param_groups"][0]
         for key in ("lr", "betas", "eps"):

@@ -2,32 +2,47 @@
 
     feats = encoder(imgs)                        fused ResNet-101, BN in train mode
     loss, grads = decoder fwd + CE + alpha-reg + BPTT   (capmi.decoder_fn, grads in place)
-    grads <- all-reduce mean over ranks          (DP only; RCCL, async)
+    grads <- all-reduce mean over ranks          (DP only; RCCL)
     params <- clamp(+-grad_clip) + Adam          (one kernel)
 
-With more than one rank the all-reduce of step k is issued asynchronously and
-its clamp+Adam update is applied at the start of step k+1's decoder, after
-step k+1's encoder forward has been launched: the encoder does not read the
-decoder's weights, so the collective overlaps the ResNet forward. ``flush()``
-completes the last pending update (call it before reading weights / timing).
+Launch modes:
+  * eager: every call launches the ~640 kernels of the step from Python;
+  * graph (``graph=True``): the step is captured once into a HIP graph (torch.cuda.CUDAGraph)
+    and replayed; inputs are copied into static buffers first. Everything that changes from
+    step to step lives on the device (Adam's step count, the dropout seed counter), so a
+    replay is exactly an eager step. With DP the graph ends after the backward pass: the
+    all-reduce and the update run eagerly after it (RCCL is not captured).
+
+With more than one rank (eager mode) the all-reduce of step k is issued asynchronously and
+its clamp+Adam update is applied at the start of step k+1's decoder, after step k+1's
+encoder forward has been launched: the encoder does not read the decoder's weights, so the
+collective overlaps the ResNet forward. ``flush()`` completes the last pending update.
 """
 import torch
 
 from . import decoder_fn as DF
 from . import dist as cdist
+from . import kernels as K
 from .decoder_core import PNAMES
 
 
 class AttentionTrainStep:
-    def __init__(self, encoder, decoder, optimizer, ctx=None, alpha_c=1.0, overlap=True):
+    def __init__(self, encoder, decoder, optimizer, ctx=None, alpha_c=1.0, overlap=True, graph=False,
+                 seed=None):
         self.encoder, self.decoder, self.opt = encoder, decoder, optimizer
-        self.ctx = ctx or cdist.DistCtx(device=next(decoder.parameters()).device)
+        dev = next(decoder.parameters()).device
+        self.ctx = ctx or cdist.DistCtx(device=dev)
         self.alpha_c = alpha_c
-        self.overlap = overlap and self.ctx.distributed
+        self.overlap = overlap and self.ctx.distributed and not graph
+        self.graph_mode = graph
         self._pending = None
         named = dict(decoder.named_parameters())
         self.need = [n for n in PNAMES if named[n].requires_grad]
         self.params = named
+        s = int(torch.randint(0, 2 ** 62, (1,)).item()) if seed is None else int(seed)
+        self.seed_dev = torch.full((1,), s, dtype=torch.int64, device=dev)
+        self._graph = None
+        self._static = None
 
     def _grads(self):
         return {n: self.params[n].grad for n in self.need}
@@ -39,18 +54,71 @@ class AttentionTrainStep:
             self._pending = None
             self.opt.step()
 
-    def __call__(self, imgs, captions, caption_lengths):
+    # ---------------------------------------------------------------- eager
+    def _body(self, imgs, captions, caption_lengths, with_update):
+        K.counter_add(self.seed_dev, 1)
         feats = self.encoder(imgs)
         self._apply_pending()
         loss, _, _ = DF.fused_loss_and_grads(self.decoder, feats, captions, caption_lengths,
-                                             self.alpha_c, self._grads(), need=self.need)
-        if self.ctx.distributed:
-            works = cdist.allreduce_mean_(self.opt.grad_buffers(), self.ctx, async_op=self.overlap)
-            if self.overlap:
-                self._pending = works
-                return loss
-        self.opt.step()
+                                             self.alpha_c, self._grads(), need=self.need,
+                                             seed_dev=self.seed_dev)
+        if with_update:
+            self.opt.step()
+        return loss
+
+    def __call__(self, imgs, captions, caption_lengths):
+        if self.graph_mode:
+            return self._replay(imgs, captions, caption_lengths)
+        return self._eager(imgs, captions, caption_lengths)
+
+    def _eager(self, imgs, captions, caption_lengths):
+        if not self.ctx.distributed:
+            return self._body(imgs, captions, caption_lengths, with_update=True)
+        loss = self._body(imgs, captions, caption_lengths, with_update=False)
+        works = cdist.allreduce_mean_(self.opt.grad_buffers(), self.ctx, async_op=self.overlap)
+        if self.overlap:
+            self._pending = works
+        else:
+            self.opt.step()
         return loss
 
     def flush(self):
         self._apply_pending()
+
+    # ---------------------------------------------------------------- graph
+    def _replay(self, imgs, captions, caption_lengths):
+        if len(set(caption_lengths)) != 1:
+            # ragged batches (never produced by the reference collate, Q1) need a host->device
+            # copy of the per-step batch sizes: run them eagerly
+            return self._eager(imgs, captions, caption_lengths)
+        key = (tuple(imgs.shape), tuple(captions.shape), tuple(caption_lengths))
+        if self._graph is None or self._static["key"] != key:
+            self._capture(imgs, captions, caption_lengths, key)
+        st = self._static
+        if imgs.data_ptr() != st["imgs"].data_ptr():
+            st["imgs"].copy_(imgs, non_blocking=True)
+        if captions.data_ptr() != st["caps"].data_ptr():
+            st["caps"].copy_(captions, non_blocking=True)
+        self._graph.replay()
+        if self.ctx.distributed:
+            cdist.allreduce_mean_(self.opt.grad_buffers(), self.ctx)
+            self.opt.step()
+        return st["loss"]
+
+    def _capture(self, imgs, captions, caption_lengths, key, warmup=2):
+        upd = not self.ctx.distributed
+        st = {"key": key, "imgs": imgs.detach().clone(), "caps": captions.detach().clone(),
+              "lens": list(caption_lengths)}
+        # warm-up on a side stream: allocates every workspace outside the graph's pool. No
+        # parameter update here (gradients are overwritten by the next step), so the first
+        # call still applies exactly one update; BN running stats do see the extra forwards.
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._body(st["imgs"], st["caps"], st["lens"], with_update=False)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            st["loss"] = self._body(st["imgs"], st["caps"], st["lens"], with_update=upd)
+        self._graph, self._static = g, st

@@ -270,7 +270,9 @@ __device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
 }
 
 __global__ void dropout_kernel(const float* __restrict__ in, long long n, float p,
-                               unsigned long long seed, float scale, float* __restrict__ out) {
+                               unsigned long long seed, const unsigned long long* __restrict__ seed_dev,
+                               float scale, float* __restrict__ out) {
+  if (seed_dev != nullptr) seed ^= splitmix64(*seed_dev);
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
     const unsigned long long r = splitmix64(seed ^ splitmix64((unsigned long long)i));
@@ -280,11 +282,11 @@ __global__ void dropout_kernel(const float* __restrict__ in, long long n, float 
 }
 
 extern "C" int capmi_dropout(const float* in, long long n, float p, unsigned long long seed,
-                             float* out, void* stream) {
+                             const unsigned long long* seed_dev, float* out, void* stream) {
   CAPMI_REQUIRE(in && out && n >= 0 && p >= 0.f && p < 1.f, CAPMI_EINVAL);
   if (n == 0) return 0;
   hipLaunchKernelGGL(dropout_kernel, dim3(std::min<long long>(cdiv(n, 256), 4096)), dim3(256), 0,
-                     as_stream(stream), in, n, p, seed, 1.f / (1.f - p), out);
+                     as_stream(stream), in, n, p, seed, seed_dev, 1.f / (1.f - p), out);
   CAPMI_LAUNCH_CHECK();
   return 0;
 }

@@ -6,10 +6,21 @@
 // v.mul_(b2).addcmul_(g, g, 1-b2), p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, -lr/bc1).
 #include "common.h"
 
+// Hyper-parameters arrive in double (Python floats) and are rounded to T exactly where torch
+// rounds its Scalars: step_size = lr / bc1 and bc2_sqrt in double, then cast.
 template <typename T>
 __global__ void adam_clamp_kernel(T* __restrict__ p, const T* __restrict__ g, T* __restrict__ m,
-                                  T* __restrict__ v, long long n, T step_size, T w1, T b2, T w2,
-                                  T eps, T bc2_sqrt, T clip) {
+                                  T* __restrict__ v, long long n, double lr, double beta1,
+                                  double beta2, double eps, double bc1_h, double bc2s_h, double clip_d,
+                                  const long long* __restrict__ step_dev) {
+  double bc1 = bc1_h, bc2s = bc2s_h;
+  if (step_dev != nullptr) {
+    const double t = (double)(*step_dev);
+    bc1 = 1.0 - pow(beta1, t);
+    bc2s = sqrt(1.0 - pow(beta2, t));
+  }
+  const T step_size = (T)(lr / bc1), bc2_sqrt = (T)bc2s;
+  const T w1 = (T)(1.0 - beta1), b2 = (T)beta2, w2 = (T)(1.0 - beta2), e = (T)eps, clip = (T)clip_d;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
     T gi = g[i];
@@ -18,31 +29,43 @@ __global__ void adam_clamp_kernel(T* __restrict__ p, const T* __restrict__ g, T*
     const T vi = v[i] * b2 + (w2 * gi) * gi;
     m[i] = mi;
     v[i] = vi;
-    const T denom = sqrt(vi) / bc2_sqrt + eps;
+    const T denom = sqrt(vi) / bc2_sqrt + e;
     p[i] = p[i] + (-step_size) * (mi / denom);
   }
 }
 
-extern "C" int capmi_adam_clamp(float* p, const float* g, float* m, float* v, long long n, float lr,
-                                float beta1, float beta2, float eps, float bc1, float bc2_sqrt,
-                                float clip, void* stream) {
-  CAPMI_REQUIRE(p && g && m && v && n >= 0 && bc1 > 0.f && bc2_sqrt > 0.f, CAPMI_EINVAL);
+template <typename T>
+static int adam_launch(T* p, const T* g, T* m, T* v, long long n, double lr, double beta1,
+                       double beta2, double eps, double bc1, double bc2_sqrt, double clip,
+                       const long long* step_dev, void* stream) {
+  CAPMI_REQUIRE(p && g && m && v && n >= 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE(step_dev != nullptr || (bc1 > 0.0 && bc2_sqrt > 0.0), CAPMI_EINVAL);
   if (n == 0) return 0;
-  hipLaunchKernelGGL(adam_clamp_kernel<float>, dim3(std::min<long long>(cdiv(n, 256), 8192)),
-                     dim3(256), 0, as_stream(stream), p, g, m, v, n, lr / bc1, 1.f - beta1, beta2,
-                     1.f - beta2, eps, bc2_sqrt, clip);
+  hipLaunchKernelGGL(adam_clamp_kernel<T>, dim3(std::min<long long>(cdiv(n, 256), 8192)), dim3(256),
+                     0, as_stream(stream), p, g, m, v, n, lr, beta1, beta2, eps, bc1, bc2_sqrt, clip,
+                     step_dev);
   CAPMI_LAUNCH_CHECK();
   return 0;
 }
 
+extern "C" int capmi_adam_clamp(float* p, const float* g, float* m, float* v, long long n, double lr,
+                                double beta1, double beta2, double eps, double bc1, double bc2_sqrt,
+                                double clip, const long long* step_dev, void* stream) {
+  return adam_launch<float>(p, g, m, v, n, lr, beta1, beta2, eps, bc1, bc2_sqrt, clip, step_dev, stream);
+}
+
 extern "C" int capmi_adam_clamp_f64(double* p, const double* g, double* m, double* v, long long n,
                                     double lr, double beta1, double beta2, double eps, double bc1,
-                                    double bc2_sqrt, double clip, void* stream) {
-  CAPMI_REQUIRE(p && g && m && v && n >= 0 && bc1 > 0.0 && bc2_sqrt > 0.0, CAPMI_EINVAL);
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(adam_clamp_kernel<double>, dim3(std::min<long long>(cdiv(n, 256), 8192)),
-                     dim3(256), 0, as_stream(stream), p, g, m, v, n, lr / bc1, 1.0 - beta1, beta2,
-                     1.0 - beta2, eps, bc2_sqrt, clip);
+                                    double bc2_sqrt, double clip, const long long* step_dev,
+                                    void* stream) {
+  return adam_launch<double>(p, g, m, v, n, lr, beta1, beta2, eps, bc1, bc2_sqrt, clip, step_dev, stream);
+}
+
+__global__ void counter_add_kernel(long long* c, long long v) { *c += v; }
+
+extern "C" int capmi_counter_add(long long* counter, long long v, void* stream) {
+  CAPMI_REQUIRE(counter != nullptr, CAPMI_EINVAL);
+  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, as_stream(stream), counter, v);
   CAPMI_LAUNCH_CHECK();
   return 0;
 }

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 1
+#define CAPMI_ABI_VERSION 2
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -144,9 +144,13 @@ int capmi_att_softmax_ctx_fwd(const float* e, const float* enc, int B, int P, in
 int capmi_lstm_cell_fwd(const float* part, int S, long long slab, const float* xemb,
                         const float* hh_part, int S2, long long slab2, const float* c_prev, int B,
                         int D, float* h_out, float* c_out, float* act_out, void* stream);
-/* Dropout before fc (:107,279): out = in * keep/(1-p), keep = hash(seed, index) >= p */
-int capmi_dropout(const float* in, long long n, float p, unsigned long long seed, float* out,
-                  void* stream);
+/* Dropout before fc (:107,279): out = in * keep/(1-p), keep = hash(seed', index) >= p with
+ * seed' = seed ^ hash(*seed_dev) when seed_dev != NULL (a device counter: graph replays draw
+ * fresh masks), else seed. The backward pass re-applies the same mask to the gradient. */
+int capmi_dropout(const float* in, long long n, float p, unsigned long long seed,
+                  const unsigned long long* seed_dev, float* out, void* stream);
+/* *counter += v (one thread): advances the device step / seed counters inside a graph */
+int capmi_counter_add(long long* counter, long long v, void* stream);
 /* zero rows r of a (rows x cols) matrix, row r = t*B + b, where b >= bt[t] (ragged decode, :261) */
 int capmi_mask_rows_tb(float* x, const int* bt, int T, int B, int cols, long long ld, long long r1,
                        long long s2, void* stream);
@@ -196,13 +200,15 @@ int capmi_att_enc_grad(const float* de, const float* att_enc, const float* att_d
 /* ------------------------------------------------------------------------
  * Optimiser (train_utils.py:2-12 clamp + torch.optim.Adam, models/attention.py:352-355,423-430)
  * p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps) with g clamped to +-clip first.
+ * step_dev == NULL: bc1 = 1 - beta1^t and bc2_sqrt = sqrt(1 - beta2^t) as passed (host step t);
+ * else t = *step_dev and both are computed on the device in fp64 (graph-replayable).
  * ---------------------------------------------------------------------- */
-int capmi_adam_clamp(float* p, const float* g, float* m, float* v, long long n, float lr,
-                     float beta1, float beta2, float eps, float bc1, float bc2_sqrt, float clip,
-                     void* stream);
+int capmi_adam_clamp(float* p, const float* g, float* m, float* v, long long n, double lr,
+                     double beta1, double beta2, double eps, double bc1, double bc2_sqrt, double clip,
+                     const long long* step_dev, void* stream);
 int capmi_adam_clamp_f64(double* p, const double* g, double* m, double* v, long long n, double lr,
                          double beta1, double beta2, double eps, double bc1, double bc2_sqrt,
-                         double clip, void* stream);
+                         double clip, const long long* step_dev, void* stream);
 /* embedding gradient: demb[caps[b*L+t]][:] += dx[t][b][0:M] (atomic; fp32 or fp64 table) */
 int capmi_embed_scatter_add(const float* dx, long long ld_dx, const long long* caps, int B, int L,
                             int T, const int* bt, int M, void* demb, int demb_is_f64, void* stream);

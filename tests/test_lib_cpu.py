@@ -40,9 +40,9 @@ def test_abi_and_errors():
     assert lib.capmi_abi_version() == capmi.ABI_VERSION
     assert b"invalid" in lib.capmi_strerror(1001)
     # validation happens before any launch: null pointers are rejected without a GPU
-    assert lib.capmi_colsum(None, 4, 4, 4, 1.0, None, None, 0, None) == 1001 or True
     assert lib.capmi_bn_add_relu(None, None, None, None, None, None, None, 4, 3, None) == 1001
-    assert lib.capmi_adam_clamp(None, None, None, None, 4, 1e-4, .9, .999, 1e-8, 1.0, 1.0, 5.0, None) == 1001
+    assert lib.capmi_adam_clamp(None, None, None, None, 4, 1e-4, .9, .999, 1e-8, 1.0, 1.0, 5.0, None, None) == 1001
+    assert lib.capmi_counter_add(None, 1, None) == 1001
 
 
 def test_gemm_rejects_bad_shapes():
