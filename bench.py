@@ -171,7 +171,7 @@ def main():
         per_img = conv_flops_per_image(_view(encoder))
         roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
                 "frac": round(ach / FP32_MFMA_PEAK_TF, 4), "traffic": None,
-                "kernel": "gemm_kernel<128,128,...> (ResNet-101 implicit-GEMM convs)",
+                "kernel": "gemm_nt_kernel (ResNet-101 implicit-GEMM convs, stream-K) + conv1 gemm_kernel",
                 "flops_per_launch": round(flops / launches), "avg_launch_us": round(ms * 1e3 / launches, 2),
                 "conv_gflop_per_image": round(per_img / 1e9, 3),
                 "conv_ms_per_step": round(ms / args.steps, 3),

@@ -23,7 +23,7 @@ CAPMI_B_NMAJOR_W, CAPMI_B_KROWS = 0, 1
 CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO = 0, 1, 2, 3
 CAPMI_MAX_GROUP = 4
 CAPMI_COLSUM_GROUPS = 64
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class GemmProblem(ctypes.Structure):
@@ -46,6 +46,8 @@ class GemmProblem(ctypes.Structure):
 _SIGS = {
     "capmi_gemm": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_int, c_vp],
     "capmi_gemm_stat_tiles": [c_int, c_int],
+    "capmi_gemm_workspace_bytes": [],
+    "capmi_gemm_sk": [ctypes.POINTER(GemmProblem), c_int, c_int, c_vp, c_ll, c_vp],
     "capmi_splitk_reduce": [c_vp, c_int, c_ll, c_int, c_int, c_ll, c_vp, c_vp, c_ll, c_vp],
     "capmi_colsum": [c_vp, c_int, c_int, c_ll, c_float, c_vp, c_vp, c_int, c_vp],
     "capmi_conv_weight_pack": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
@@ -86,7 +88,7 @@ _SIGS = {
     "capmi_strerror": [c_int],
     "capmi_abi_version": [],
 }
-_RESTYPES = {"capmi_strerror": ctypes.c_char_p}
+_RESTYPES = {"capmi_strerror": ctypes.c_char_p, "capmi_gemm_workspace_bytes": c_ll}
 EXPORTS = tuple(_SIGS)
 
 

@@ -64,6 +64,21 @@ def gemm(problems, amode=CAPMI_A_KMAJOR, bmode=CAPMI_B_NMAJOR_W, tile=CAPMI_TILE
     call("capmi_gemm", arr, len(problems), amode, bmode, tile, stream())
 
 
+def gemm_workspace_bytes():
+    return int(lib.capmi_gemm_workspace_bytes())
+
+
+def gemm_workspace(device):
+    """Zeroed stream-K workspace for capmi_gemm_sk (one per stream that runs it)."""
+    n = (gemm_workspace_bytes() + 3) // 4
+    return torch.zeros(n, device=device, dtype=torch.int32)
+
+
+def gemm_sk(prob, amode, workspace, tile=CAPMI_TILE_AUTO):
+    _cuda(workspace, dtype=torch.int32)
+    call("capmi_gemm_sk", ctypes.byref(prob), amode, tile, ptr(workspace), workspace.numel() * 4, stream())
+
+
 def stat_tiles(M, tile=CAPMI_TILE_128):
     return lib.capmi_gemm_stat_tiles(int(M), int(tile))
 

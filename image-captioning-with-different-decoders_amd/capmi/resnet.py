@@ -134,6 +134,7 @@ class EncoderRunner:
             ws["stats"] = torch.empty(2 * ((N * H1 * W1 + 63) // 64) * 256, **f)
             ws["bnwork"] = torch.empty(K.bn_work_doubles(2048), device=device, dtype=torch.float64)
             ws["ss"] = {}
+            ws["sk"] = K.gemm_workspace(device)  # stream-K partials + flags (zeroed once)
             self._ws, self._ws_key = ws, key
         return self._ws
 
@@ -180,7 +181,10 @@ class EncoderRunner:
             sc, sh = in_ss if in_ss is not None else (None, None)
             prob = K.problem(rows, co, Kd, x, 0, w, Kd, out, co, conv=geo, in_scale=sc, in_shift=sh, **kw_)
             mode = CAPMI_A_CONV_NHWC
-        launch = lambda: K.gemm(prob, mode, CAPMI_B_NMAJOR_W, K.TILE_AUTO)  # noqa: E731
+        if nchw:
+            launch = lambda: K.gemm(prob, mode, CAPMI_B_NMAJOR_W, K.TILE_AUTO)  # noqa: E731
+        else:
+            launch = lambda: K.gemm_sk(prob, mode, self._ws["sk"], K.TILE_AUTO)  # noqa: E731
         if self.conv_hook is not None:
             self.conv_hook(tag, 2.0 * rows * co * Kd, launch)
         else:

@@ -381,12 +381,19 @@ static long long tiles_of(const capmi_gemm_problem* probs, int nprob, int bm, in
   return t;
 }
 
-extern "C" int capmi_gemm(const capmi_gemm_problem* probs, int nprob, int amode, int bmode,
-                          int tile, void* stream) {
-  CAPMI_REQUIRE(nprob >= 1 && nprob <= CAPMI_MAX_GROUP, CAPMI_EINVAL);
+namespace {
+struct GemmPlan {
+  GemmArgs a;
+  int bm, bn;
+  bool nt_ok, vec;
+  long long total;  // workgroups of the data-parallel launch
+};
+
+int gemm_plan(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, int tile, GemmPlan& g) {
+  CAPMI_REQUIRE(probs != nullptr && nprob >= 1 && nprob <= CAPMI_MAX_GROUP, CAPMI_EINVAL);
   CAPMI_REQUIRE(amode >= 0 && amode <= 3 && bmode >= 0 && bmode <= 1, CAPMI_EINVAL);
   CAPMI_REQUIRE(tile >= CAPMI_TILE_128 && tile <= CAPMI_TILE_AUTO, CAPMI_EINVAL);
-  GemmArgs a;
+  GemmArgs& a = g.a;
   memset(&a, 0, sizeof(a));
   a.nprob = nprob;
   bool vec = true;
@@ -431,11 +438,9 @@ extern "C" int capmi_gemm(const capmi_gemm_problem* probs, int nprob, int amode,
   } else if (tile == CAPMI_TILE_AUTO) {
     if (!nt_ok) {
       bm = bn = (tiles_of(probs, nprob, 128, 128) >= 256 ? 128 : 64);
-    } else if (maxN > 64 && tiles_of(probs, nprob, 128, 128) >= 480) {
-      bm = bn = 128;
-    } else if (tiles_of(probs, nprob, 128, 64) >= 480) {
-      bn = 64;
     } else {
+      // measured on the ResNet-101 / decoder shapes (tools/gemm_sweep.py): the 64x64 tile
+      // (4 WGs per CU) is the fastest or within noise of it on every one of them
       bm = bn = 64;
     }
   }
@@ -454,11 +459,85 @@ extern "C" int capmi_gemm(const capmi_gemm_problem* probs, int nprob, int amode,
   }
   a.tiles_begin[nprob] = (int)total;
   CAPMI_REQUIRE(total < (1LL << 31), CAPMI_ERANGE);
-  if (total == 0) return 0;
+  g.bm = bm;
+  g.bn = bn;
+  g.nt_ok = nt_ok;
+  g.vec = vec;
+  g.total = total;
+  return 0;
+}
+
+int gemm_launch_dp(const GemmPlan& g, int amode, int bmode, hipStream_t s) {
+  if (g.total == 0) return 0;
+  if (g.nt_ok) return gemm_nt_launch(g.a, amode, g.bm, g.bn, (int)g.total, s);
+  if (g.bm == 128) return launch_mode<128, 128, 64, 64>(g.a, amode, bmode, g.vec, (int)g.total, s);
+  return launch_mode<64, 64, 32, 32>(g.a, amode, bmode, g.vec, (int)g.total, s);
+}
+
+int cu_count() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cache[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
+constexpr int kSkMaxWgPerCu = 4;
+long long sk_flag_bytes(int cus) { return ((long long)(cus * kSkMaxWgPerCu + 1) * 4 + 255) / 256 * 256; }
+}  // namespace
+
+extern "C" int capmi_gemm(const capmi_gemm_problem* probs, int nprob, int amode, int bmode,
+                          int tile, void* stream) {
+  GemmPlan g;
+  const int rc = gemm_plan(probs, nprob, amode, bmode, tile, g);
+  if (rc) return rc;
+  return gemm_launch_dp(g, amode, bmode, as_stream(stream));
+}
+
+extern "C" long long capmi_gemm_workspace_bytes(void) {
+  const int cus = cu_count();
+  // parked partials: (WGs per CU) * BM * BN floats per CU is 64 KB for 4 x 64x64 and for
+  // 2 x 128x64, 128 KB for 2 x 128x128
+  return sk_flag_bytes(cus) + (long long)cus * 128 * 1024;
+}
+
+extern "C" int capmi_gemm_sk(const capmi_gemm_problem* prob, int amode, int tile, void* workspace,
+                             long long ws_bytes, void* stream) {
+  CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
+  const int nkt = (prob->K + 31) / 32;
+  const bool automatic = tile == CAPMI_TILE_AUTO;
+  // measured (tools/gemm_sweep.py, ResNet-101 shapes at batch 64): with >= 16 k-tiles per
+  // output tile, stream-K over 128x64 tiles is the fastest form; below that the per-segment
+  // pipeline fill outweighs the balance gain and 64x64 data-parallel wins
+  if (automatic) tile = nkt >= 16 ? CAPMI_TILE_128x64 : CAPMI_TILE_64;
+  GemmPlan g;
+  const int rc = gemm_plan(prob, 1, amode, CAPMI_B_NMAJOR_W, tile, g);
+  if (rc) return rc;
   hipStream_t s = as_stream(stream);
-  if (nt_ok) return gemm_nt_launch(a, amode, bm, bn, (int)total, s);
-  if (bm == 128) return launch_mode<128, 128, 64, 64>(a, amode, bmode, vec, (int)total, s);
-  return launch_mode<64, 64, 32, 32>(a, amode, bmode, vec, (int)total, s);
+  const int cus = cu_count();
+  const long long slots = (long long)cus * gemm_nt_wg_per_cu(g.bm, g.bn);
+  const long long tiles = g.total;
+  bool sk = g.nt_ok && prob->ksplit == 1 && tiles > 0 && (!automatic || nkt >= 16);
+  if (sk) {
+    CAPMI_REQUIRE(workspace != nullptr && aligned16(workspace), CAPMI_EINVAL);
+    CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
+    // stream-K only when the data-parallel grid would leave a costly partial last round
+    const long long rounds = (tiles + slots - 1) / slots;
+    sk = (double)tiles / (double)(rounds * slots) < 0.9;
+  }
+  if (!sk) return gemm_launch_dp(g, amode, CAPMI_B_NMAJOR_W, s);
+  GemmArgs& a = g.a;
+  a.sk_nkt = (prob->K + 31) / 32;
+  a.sk_units = tiles * a.sk_nkt;
+  a.sk_workers = (int)std::min<long long>(slots, a.sk_units);
+  a.sk_flags = static_cast<int*>(workspace);
+  a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
+  return gemm_nt_launch(a, amode, g.bm, g.bn, a.sk_workers, s);
 }
 
 // ------------------------------------------------------------------------------------

@@ -11,6 +11,12 @@ struct GemmArgs {
   int tiles_n[CAPMI_MAX_GROUP];
   int kchunk[CAPMI_MAX_GROUP];
   int nprob;
+  // stream-K (gemm_nt only, one problem, no k-split): 0 workers = data-parallel launch
+  int sk_workers;
+  int sk_nkt;            // k-tiles per output tile
+  long long sk_units;    // tiles * sk_nkt
+  float* sk_part;        // [workers][BM*BN] parked k-prefix partials
+  int* sk_flags;         // [workers + 1], zero between launches; [workers] = spin-timeout flag
 };
 
 __device__ __forceinline__ long long remap(long long r, long long r1, long long ld, long long s2) {
@@ -19,3 +25,5 @@ __device__ __forceinline__ long long remap(long long r, long long r1, long long 
 
 // NT kernel (A K-major dense or NHWC conv, B = W[N][K]); BM x BN in {128x128, 128x64, 64x64}
 int gemm_nt_launch(const GemmArgs& a, int amode, int bm, int bn, int blocks, hipStream_t s);
+// resident workgroups per CU of the NT kernel for a tile shape (LDS / register bound)
+inline int gemm_nt_wg_per_cu(int bm, int bn) { return bm == 64 && bn == 64 ? 4 : 2; }

@@ -25,8 +25,22 @@ namespace {
 constexpr int BK2 = 32;
 constexpr int S2 = BK2 + 4;  // LDS row stride in floats
 
-template <int BM, int BN, int AMODE, bool PRO>
-__global__ void __launch_bounds__(256) gemm_nt_kernel(const GemmArgs args) {
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kSc1 = 16;  // buffer-op aux bit: sc1 (write-through store / L1-bypassing load)
+
+// buffer descriptor of one parked-partial slot (wave-uniform inputs only)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slot_rsrc(float* base, long long off_floats) {
+  float* p = base + off_floats;
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, 256 * 1024, 0x00020000);
+}
+
+// resident workgroups per SIMD the register budget is sized for (== gemm_nt_wg_per_cu)
+template <int BM, int BN>
+constexpr int kWavesPerEu = (BM == 64 && BN == 64) ? 4 : 2;
+
+template <int BM, int BN, int AMODE, bool PRO, bool SK>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWavesPerEu<BM, BN>)))
+gemm_nt_kernel(const GemmArgs args) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
   constexpr int NA = BM * BK2 / 4 / 256, NB = BN * BK2 / 4 / 256;
   static_assert(NA >= 1 && NB >= 1, "tile");
@@ -36,147 +50,131 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(const GemmArgs args) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
   const int lr = lane & 31, lh = lane >> 5;
-
-  int bid = blockIdx.x;
-  if (args.nprob == 1) {  // XCD-aware remap (bijective for any grid size)
-    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = bid & 7;
-    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
-  }
-  int pi = 0;
-  while (pi + 1 < args.nprob && bid >= args.tiles_begin[pi + 1]) ++pi;
-  const capmi_gemm_problem& P = args.p[pi];
-  const int local = bid - args.tiles_begin[pi];
-  const int tiles_n = args.tiles_n[pi], tiles_m = args.tiles_m[pi];
-  const int tn = local % tiles_n;
-  const int tm = (local / tiles_n) % tiles_m;
-  const int z = local / (tiles_n * tiles_m);
-  const int M = P.M, N = P.N;
-  const int k_begin = z * args.kchunk[pi];
-  const int k_end = min(P.K, k_begin + args.kchunk[pi]);
-  const int nkt = k_end > k_begin ? (k_end - k_begin + BK2 - 1) / BK2 : 0;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const float* __restrict__ Ag = P.A;
-  const float* __restrict__ Bg = P.B;
-  const long long ldb = P.ldb;
-  // conv geometry, read once
-  const int cH = P.cH, cW = P.cW, cCin = P.cCin, cKW = P.cKW;
-  const float* __restrict__ isc = P.in_scale;
-  const float* __restrict__ ish = P.in_shift;
-
-  // ---- staging slots: float4 f -> (row f>>3, k 4*(f&7)) ------------------------------
-  long long a_base[NA];  // dense: row offset; conv: image base offset
-  int a_ih0[NA], a_iw0[NA];
-  bool a_ok[NA];
-#pragma unroll
-  for (int i = 0; i < NA; ++i) {
-    const int row = m0 + ((tid + i * 256) >> 3);
-    a_ok[i] = row < M;
-    if (AMODE == 0) {
-      a_base[i] = a_ok[i] ? remap(row, P.a_r1, P.lda, P.a_s2) : 0;
-      a_ih0[i] = a_iw0[i] = 0;
-    } else {
-      const int hw = P.cHo * P.cWo;
-      const int n = row / hw, rem = row - n * hw;
-      const int oh = rem / P.cWo, ow = rem - oh * P.cWo;
-      a_ih0[i] = oh * P.cStride - P.cPad;
-      a_iw0[i] = ow * P.cStride - P.cPad;
-      a_base[i] = (long long)n * cH * cW * cCin;
-    }
-  }
   const int kq = (tid & 7) * 4;
-  long long b_base[NB];
-  bool b_ok[NB];
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    const int n = n0 + ((tid + i * 256) >> 3);
-    b_ok[i] = n < N;
-    b_base[i] = b_ok[i] ? (long long)n * ldb : 0;
-  }
-  // conv k walk: k = ((kh * KW) + kw) * Cin + ci, advanced by BK2 per k-tile
-  int c_ci = 0, c_kh = 0, c_kw = 0;
-  if (AMODE == 2) {
-    const int kpos = k_begin / cCin;
-    c_ci = k_begin - kpos * cCin;
-    c_kh = kpos / cKW;
-    c_kw = kpos - c_kh * cKW;
-  }
-
-  float4 ra[NA], rb[NB], rsc = f4(1.f), rsh = f4(0.f);
-  unsigned amask = 0, bmask = 0;
-  auto load_tile = [&](int kt) {
-    const int k = k_begin + kt * BK2 + kq;
-    const bool kok = k < k_end;  // K % 4 == 0: a float4 is all-in or all-out
-    amask = 0;
-    bmask = 0;
-    if (AMODE == 0) {
-#pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        const bool ok = a_ok[i] && kok;
-        ra[i] = *reinterpret_cast<const float4*>(Ag + (ok ? a_base[i] + k : 0));
-        amask |= (unsigned)ok << i;
-      }
-    } else {
-      const int ci = c_ci + kq;
-      if (PRO) {
-        rsc = *reinterpret_cast<const float4*>(isc + ci);
-        rsh = *reinterpret_cast<const float4*>(ish + ci);
-      }
-#pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        const int ih = a_ih0[i] + c_kh, iw = a_iw0[i] + c_kw;
-        const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
-        const long long off = a_base[i] + ((long long)(ih * cW + iw)) * cCin + ci;
-        ra[i] = *reinterpret_cast<const float4*>(Ag + (ok ? off : 0));
-        amask |= (unsigned)ok << i;
-      }
-      c_ci += BK2;  // advance the (kh, kw, ci) walk to the next k-tile
-      if (c_ci >= cCin) {
-        c_ci = 0;
-        if (++c_kw == cKW) {
-          c_kw = 0;
-          ++c_kh;
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const bool ok = b_ok[i] && kok;
-      rb[i] = *reinterpret_cast<const float4*>(Bg + (ok ? b_base[i] + k : 0));
-      bmask |= (unsigned)ok << i;
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      float4 v = ra[i];
-      if (PRO) v = relu4(fma4(v, rsc, rsh));
-      if (!((amask >> i) & 1u)) v = f4(0.f);
-      *reinterpret_cast<float4*>(&As[buf][((tid + i * 256) >> 3) * S2 + kq]) = v;
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      float4 v = rb[i];
-      if (!((bmask >> i) & 1u)) v = f4(0.f);
-      *reinterpret_cast<float4*>(&Bs[buf][((tid + i * 256) >> 3) * S2 + kq]) = v;
-    }
-  };
 
   f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  if (nkt > 0) {
-    load_tile(0);
-    store_tile(0);
-    __syncthreads();
-    for (int kt = 0; kt < nkt; ++kt) {
-      const int buf = kt & 1;
-      const bool more = kt + 1 < nkt;
-      if (more) load_tile(kt + 1);
+  // ---- main loop: acc = A[m0:m0+BM, k_lo:k_hi) * B[n0:n0+BN, k_lo:k_hi)^T ------------------
+  auto mainloop = [&](const capmi_gemm_problem& P, int m0, int n0, int k_lo, int k_hi) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int nkt = k_hi > k_lo ? (k_hi - k_lo + BK2 - 1) / BK2 : 0;
+    if (nkt == 0) return;
+    const int M = P.M, N = P.N;
+    const float* __restrict__ Ag = P.A;
+    const float* __restrict__ Bg = P.B;
+    const long long ldb = P.ldb;
+    // conv geometry, read once
+    const int cH = P.cH, cW = P.cW, cCin = P.cCin, cKW = P.cKW;
+    const float* __restrict__ isc = P.in_scale;
+    const float* __restrict__ ish = P.in_shift;
+
+    // staging slots: float4 f -> (row f>>3, k 4*(f&7))
+    long long a_base[NA];  // dense: row offset; conv: image base offset
+    int a_ih0[NA], a_iw0[NA];
+    bool a_ok[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int row = m0 + ((tid + i * 256) >> 3);
+      a_ok[i] = row < M;
+      if (AMODE == 0) {
+        a_base[i] = a_ok[i] ? remap(row, P.a_r1, P.lda, P.a_s2) : 0;
+        a_ih0[i] = a_iw0[i] = 0;
+      } else {
+        const int hw = P.cHo * P.cWo;
+        const int n = row / hw, rem = row - n * hw;
+        const int oh = rem / P.cWo, ow = rem - oh * P.cWo;
+        a_ih0[i] = oh * P.cStride - P.cPad;
+        a_iw0[i] = ow * P.cStride - P.cPad;
+        a_base[i] = (long long)n * cH * cW * cCin;
+      }
+    }
+    long long b_base[NB];
+    bool b_ok[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int n = n0 + ((tid + i * 256) >> 3);
+      b_ok[i] = n < N;
+      b_base[i] = b_ok[i] ? (long long)n * ldb : 0;
+    }
+    // conv k walk: k = ((kh * KW) + kw) * Cin + ci, advanced by BK2 per k-tile
+    int c_ci = 0, c_kh = 0, c_kw = 0;
+    if (AMODE == 2) {
+      const int kpos = k_lo / cCin;
+      c_ci = k_lo - kpos * cCin;
+      c_kh = kpos / cKW;
+      c_kw = kpos - c_kh * cKW;
+    }
+
+    // Two register stages: the loads of k-tile t+2 are issued while tile t is multiplied out
+    // of LDS and tile t+1 (loaded one k-step earlier) is written to the other LDS buffer, so
+    // every global load has two k-steps of MFMA work to land.
+    struct Stage {
+      float4 ra[NA], rb[NB], sc, sh;
+      unsigned am, bm;
+    };
+    auto load_tile = [&](Stage& st, int kt) {
+      const int k = k_lo + kt * BK2 + kq;
+      const bool kok = k < k_hi;  // K % 4 == 0: a float4 is all-in or all-out
+      st.am = 0;
+      st.bm = 0;
+      if (AMODE == 0) {
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+          const bool ok = a_ok[i] && kok;
+          st.ra[i] = *reinterpret_cast<const float4*>(Ag + (ok ? a_base[i] + k : 0));
+          st.am |= (unsigned)ok << i;
+        }
+      } else {
+        const int ci = c_ci + kq;
+        if (PRO) {
+          st.sc = *reinterpret_cast<const float4*>(isc + ci);
+          st.sh = *reinterpret_cast<const float4*>(ish + ci);
+        }
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+          const int ih = a_ih0[i] + c_kh, iw = a_iw0[i] + c_kw;
+          const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
+          const long long off = a_base[i] + ((long long)(ih * cW + iw)) * cCin + ci;
+          st.ra[i] = *reinterpret_cast<const float4*>(Ag + (ok ? off : 0));
+          st.am |= (unsigned)ok << i;
+        }
+        c_ci += BK2;  // advance the (kh, kw, ci) walk to the next k-tile
+        if (c_ci >= cCin) {
+          c_ci = 0;
+          if (++c_kw == cKW) {
+            c_kw = 0;
+            ++c_kh;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const bool ok = b_ok[i] && kok;
+        st.rb[i] = *reinterpret_cast<const float4*>(Bg + (ok ? b_base[i] + k : 0));
+        st.bm |= (unsigned)ok << i;
+      }
+    };
+    auto store_tile = [&](const Stage& st, int buf) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        float4 v = st.ra[i];
+        if (PRO) v = relu4(fma4(v, st.sc, st.sh));
+        if (!((st.am >> i) & 1u)) v = f4(0.f);
+        *reinterpret_cast<float4*>(&As[buf][((tid + i * 256) >> 3) * S2 + kq]) = v;
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        float4 v = st.rb[i];
+        if (!((st.bm >> i) & 1u)) v = f4(0.f);
+        *reinterpret_cast<float4*>(&Bs[buf][((tid + i * 256) >> 3) * S2 + kq]) = v;
+      }
+    };
+    auto compute = [&](int buf) {
       const float* Ab = As[buf] + (wm0 + lr) * S2 + 4 * lh;
       const float* Bb = Bs[buf] + (wn0 + lr) * S2 + 4 * lh;
 #pragma unroll
@@ -197,100 +195,238 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(const GemmArgs args) {
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
             }
       }
-      if (more) store_tile(buf ^ 1);
+    };
+    // one k-step: issue loads of tile kt+2 into `ld`, multiply tile kt, park tile kt+1 (`sv`)
+    auto kstep = [&](Stage& ld, const Stage& sv, int kt) {
+      if (kt + 2 < nkt) load_tile(ld, kt + 2);
+      compute(kt & 1);
+      if (kt + 1 < nkt) store_tile(sv, (kt + 1) & 1);
       __syncthreads();
-    }
-  }
+    };
 
-  // ---- epilogue (same contract as gemm.hip) -----------------------------------------
-  const float alpha = P.alpha * (P.alpha_ptr ? *P.alpha_ptr : 1.f);
-  float* Cz = P.C + (long long)z * P.c_split_stride;
-  const float* bias1 = P.bias;
-  const float* bias2 = P.bias2;
-  const float beta = P.beta;
-  const int relu = P.relu;
-  const long long ldc = P.ldc, c_r1 = P.c_r1, c_s2 = P.c_s2;
-  float csum[TN], csq[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    csum[j] = 0.f;
-    csq[j] = 0.f;
-    const int col = n0 + wn0 + 32 * j + lr;
-    const bool cok = col < N;
-    float bias = 0.f;
-    if (z == 0 && cok) {
-      if (bias1) bias += bias1[col];
-      if (bias2) bias += bias2[col];
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (cok && row < M) {
-          float* cp = Cz + remap(row, c_r1, ldc, c_s2) + col;
-          float v = fmaf(acc[i][j][r], alpha, bias);
-          if (beta != 0.f) v = fmaf(beta, *cp, v);
-          if (relu) v = fmaxf(v, 0.f);
-          *cp = v;
-          csum[j] += v;
-          csq[j] = fmaf(v, v, csq[j]);
-        }
+    // 128x128 with the BN prologue cannot afford the second register stage (it would drop to
+    // one wave per SIMD): it prefetches one tile ahead.
+    constexpr bool DEEP = !(BM == 128 && BN == 128 && PRO);
+    Stage s0, s1;
+    s0.sc = s1.sc = f4(1.f);
+    s0.sh = s1.sh = f4(0.f);
+    load_tile(s0, 0);
+    store_tile(s0, 0);
+    if (DEEP) {
+      if (nkt > 1) load_tile(s1, 1);
+      __syncthreads();
+      for (int kt = 0; kt < nkt; kt += 2) {
+        kstep(s0, s1, kt);
+        if (kt + 1 < nkt) kstep(s1, s0, kt + 1);
+      }
+    } else {
+      __syncthreads();
+      for (int kt = 0; kt < nkt; ++kt) {
+        if (kt + 1 < nkt) load_tile(s0, kt + 1);
+        compute(kt & 1);
+        if (kt + 1 < nkt) store_tile(s0, (kt + 1) & 1);
+        __syncthreads();
       }
     }
-  }
-  float* __restrict__ stats = P.stats;
-  if (stats != nullptr) {
-    // per-channel (sum, sumsq) of the stored values per 64-row slice: stats[slice][col][2]
+  };
+
+  // ---- epilogue: alpha, bias (split 0 only), beta*C, relu, store, BN statistics -------------
+  auto epilogue = [&](const capmi_gemm_problem& P, int tm, int tn, int z) {
+    const int M = P.M, N = P.N;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const float alpha = P.alpha * (P.alpha_ptr ? *P.alpha_ptr : 1.f);
+    float* Cz = P.C + (long long)z * P.c_split_stride;
+    const float* bias1 = P.bias;
+    const float* bias2 = P.bias2;
+    const float beta = P.beta;
+    const int relu = P.relu;
+    const long long ldc = P.ldc, c_r1 = P.c_r1, c_s2 = P.c_s2;
+    float csum[TN], csq[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      csum[j] += __shfl_xor(csum[j], 32, 64);
-      csq[j] += __shfl_xor(csq[j], 32, 64);
-    }
-    if (WM == 64) {  // each wave row owns one slice
-      if (lh == 0) {
-        const long long sl = (m0 + wm0) >> 6;
+      csum[j] = 0.f;
+      csq[j] = 0.f;
+      const int col = n0 + wn0 + 32 * j + lr;
+      const bool cok = col < N;
+      float bias = 0.f;
+      if (z == 0 && cok) {
+        if (bias1) bias += bias1[col];
+        if (bias2) bias += bias2[col];
+      }
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = n0 + wn0 + 32 * j + lr;
-          if (col < N && m0 + wm0 < M) {
-            stats[(sl * N + col) * 2 + 0] = csum[j];
-            stats[(sl * N + col) * 2 + 1] = csq[j];
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (cok && row < M) {
+            float* cp = Cz + remap(row, c_r1, ldc, c_s2) + col;
+            float v = fmaf(acc[i][j][r], alpha, bias);
+            if (beta != 0.f) v = fmaf(beta, *cp, v);
+            if (relu) v = fmaxf(v, 0.f);
+            *cp = v;
+            csum[j] += v;
+            csq[j] = fmaf(v, v, csq[j]);
           }
         }
       }
-    } else {  // BM == 64: both wave rows share slice tm
-      float* red = As[0];  // the K loop ended with a barrier: LDS is free
-      if (lh == 0) {
+    }
+    float* __restrict__ stats = P.stats;
+    if (stats != nullptr) {
+      // per-channel (sum, sumsq) of the stored values per 64-row slice: stats[slice][col][2]
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          red[(wid * 2 + 0) * WN + 32 * j + lr] = csum[j];
-          red[(wid * 2 + 1) * WN + 32 * j + lr] = csq[j];
-        }
+      for (int j = 0; j < TN; ++j) {
+        csum[j] += __shfl_xor(csum[j], 32, 64);
+        csq[j] += __shfl_xor(csq[j], 32, 64);
       }
-      __syncthreads();
-      for (int c = tid; c < BN; c += 256) {
-        const int wn = c / WN, cc = c % WN;
-        const float s = red[((0 * 2 + wn) * 2 + 0) * WN + cc] + red[((1 * 2 + wn) * 2 + 0) * WN + cc];
-        const float q = red[((0 * 2 + wn) * 2 + 1) * WN + cc] + red[((1 * 2 + wn) * 2 + 1) * WN + cc];
-        const int col = n0 + c;
-        if (col < N) {
-          stats[((long long)tm * N + col) * 2 + 0] = s;
-          stats[((long long)tm * N + col) * 2 + 1] = q;
+      if (WM == 64) {  // each wave row owns one slice
+        if (lh == 0) {
+          const long long sl = (m0 + wm0) >> 6;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int col = n0 + wn0 + 32 * j + lr;
+            if (col < N && m0 + wm0 < M) {
+              stats[(sl * N + col) * 2 + 0] = csum[j];
+              stats[(sl * N + col) * 2 + 1] = csq[j];
+            }
+          }
         }
+      } else {  // BM == 64: both wave rows share slice tm
+        float* red = As[0];  // the K loop ended with a barrier: LDS is free
+        if (lh == 0) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            red[(wid * 2 + 0) * WN + 32 * j + lr] = csum[j];
+            red[(wid * 2 + 1) * WN + 32 * j + lr] = csq[j];
+          }
+        }
+        __syncthreads();
+        for (int c = tid; c < BN; c += 256) {
+          const int wn = c / WN, cc = c % WN;
+          const float s = red[((0 * 2 + wn) * 2 + 0) * WN + cc] + red[((1 * 2 + wn) * 2 + 0) * WN + cc];
+          const float q = red[((0 * 2 + wn) * 2 + 1) * WN + cc] + red[((1 * 2 + wn) * 2 + 1) * WN + cc];
+          const int col = n0 + c;
+          if (col < N) {
+            stats[((long long)tm * N + col) * 2 + 0] = s;
+            stats[((long long)tm * N + col) * 2 + 1] = q;
+          }
+        }
+        __syncthreads();  // LDS reused by the next tile (stream-K)
       }
     }
+  };
+
+  if (!SK) {
+    // ---- data-parallel: one tile (of one problem / k-split) per workgroup --------------------
+    int bid = blockIdx.x;
+    if (args.nprob == 1) {  // XCD-aware remap (bijective for any grid size)
+      const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = bid & 7;
+      bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+    }
+    int pi = 0;
+    while (pi + 1 < args.nprob && bid >= args.tiles_begin[pi + 1]) ++pi;
+    const capmi_gemm_problem& P = args.p[pi];
+    const int local = bid - args.tiles_begin[pi];
+    const int tiles_n = args.tiles_n[pi], tiles_m = args.tiles_m[pi];
+    const int tn = local % tiles_n;
+    const int tm = (local / tiles_n) % tiles_m;
+    const int z = local / (tiles_n * tiles_m);
+    const int k_begin = z * args.kchunk[pi];
+    mainloop(P, tm * BM, tn * BN, k_begin, min(P.K, k_begin + args.kchunk[pi]));
+    epilogue(P, tm, tn, z);
+    return;
   }
+
+  // ---- stream-K: worker w owns units [w*U/G, (w+1)*U/G) of the (tile, k-tile) space ------------
+  // Tiles are visited from the last to the first: the first segment of a tile's range (its
+  // k-prefix, owned by the lower-numbered neighbour) is computed at the START of that
+  // worker's schedule and parked in its workspace slot; the worker owning the tile's k-end
+  // visits it LAST, adds the parked partials of the lower-numbered contributors in a fixed
+  // order (deterministic) and runs the epilogue. A worker only ever waits on lower-numbered
+  // workgroups, which are dispatched before it.
+  const capmi_gemm_problem& P = args.p[0];
+  const long long U = args.sk_units, G = gridDim.x, w = blockIdx.x;
+  const int nkt = args.sk_nkt, tiles_n = args.tiles_n[0];
+  const long long u0 = w * U / G, u1 = (w + 1) * U / G;
+  if (u0 >= u1) return;
+  constexpr int PART = BM * BN;
+  int* flags = args.sk_flags;
+  for (long long t = (u1 - 1) / nkt; t >= u0 / nkt; --t) {
+    const long long tb = t * nkt;
+    const int ks = (int)(max(u0, tb) - tb), ke = (int)(min(u1, tb + nkt) - tb);
+    const int tm = (int)(t / tiles_n), tn = (int)(t % tiles_n);
+    mainloop(P, tm * BM, tn * BN, ks * BK2, min(P.K, ke * BK2));
+    if (ke < nkt) {  // k-prefix of a tile finished by a higher-numbered worker: park it
+      // write-through (sc1) 16-B stores, every wave drains them, one lane raises the flag
+      // with an agent-scope store: the hand-off needs no L2 write-back fence
+      const auto rs = slot_rsrc(args.sk_part, w * PART);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            u32x4 v;
+            v.x = __float_as_uint(acc[i][j][4 * q + 0]);
+            v.y = __float_as_uint(acc[i][j][4 * q + 1]);
+            v.z = __float_as_uint(acc[i][j][4 * q + 2]);
+            v.w = __float_as_uint(acc[i][j][4 * q + 3]);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (((i * TN + j) * 4 + q) * 256 + tid) * 16, 0, kSc1);
+          }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(flags + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      continue;
+    }
+    if (ks > 0) {  // add the parked k-prefixes, nearest contributor first
+      for (long long w2 = w - 1;; --w2) {
+        if (tid == 0) {
+          int spins = 0;
+          while (__hip_atomic_load(flags + w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+                 ++spins < (1 << 22))
+            __builtin_amdgcn_s_sleep(2);
+          if (spins >= (1 << 22)) flags[G] = 1;  // never expected: report instead of hanging
+          __hip_atomic_store(flags + w2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the poll
+        // every load of the parked bytes is an sc1 (L1-bypassing) load: no agent acquire needed
+        const auto rs = slot_rsrc(args.sk_part, w2 * PART);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+                  rs, (((i * TN + j) * 4 + q) * 256 + tid) * 16, 0, kSc1);
+              acc[i][j][4 * q + 0] += __uint_as_float(v.x);
+              acc[i][j][4 * q + 1] += __uint_as_float(v.y);
+              acc[i][j][4 * q + 2] += __uint_as_float(v.z);
+              acc[i][j][4 * q + 3] += __uint_as_float(v.w);
+            }
+        if (w2 * U / G <= tb) break;  // w2's range starts inside (or at) this tile
+      }
+    }
+    epilogue(P, tm, tn, 0);
+  }
+}
+
+template <int BM, int BN, bool SK>
+void launch_sk(const GemmArgs& a, int amode, bool pro, int blocks, hipStream_t s) {
+  if (amode == 0)
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 0, false, SK>), dim3(blocks), dim3(256), 0, s, a);
+  else if (pro)
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 2, true, SK>), dim3(blocks), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 2, false, SK>), dim3(blocks), dim3(256), 0, s, a);
 }
 
 template <int BM, int BN>
 int launch_bmbn(const GemmArgs& a, int amode, bool pro, int blocks, hipStream_t s) {
-  if (amode == 0)
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 0, false>), dim3(blocks), dim3(256), 0, s, a);
-  else if (pro)
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 2, true>), dim3(blocks), dim3(256), 0, s, a);
+  if (a.sk_workers > 0)
+    launch_sk<BM, BN, true>(a, amode, pro, blocks, s);
   else
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 2, false>), dim3(blocks), dim3(256), 0, s, a);
+    launch_sk<BM, BN, false>(a, amode, pro, blocks, s);
   CAPMI_LAUNCH_CHECK();
   return 0;
 }

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 2
+#define CAPMI_ABI_VERSION 3
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -76,6 +76,19 @@ int capmi_gemm(const capmi_gemm_problem* problems, int nprob, int amode, int bmo
                void* stream);
 /* rows of the statistics buffer capmi_gemm writes for M rows: ceil(M/64) (tile ignored) */
 int capmi_gemm_stat_tiles(int M, int tile);
+/* Stream-K form of capmi_gemm for ONE problem with bmode CAPMI_B_NMAJOR_W (what every conv
+ * of the encoder is): when the data-parallel grid would end in a partial round of
+ * workgroups (e.g. 784 64x64 tiles on 1024 resident slots), the (tile, k-tile) iteration
+ * space is instead split evenly over one persistent workgroup per resident slot; the k-prefix
+ * of a tile shared by two workgroups is parked in `workspace` and added, in a fixed order, by
+ * the workgroup that owns the tile's k-end (deterministic result). Same output contract
+ * (alpha/bias/beta/relu/stats/prologue) as capmi_gemm; other cases launch capmi_gemm.
+ * workspace: capmi_gemm_workspace_bytes() bytes, 16-B aligned, ZEROED by the caller once
+ * before first use (the kernel leaves it reusable); one workspace per concurrently running
+ * stream. */
+long long capmi_gemm_workspace_bytes(void);
+int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int tile, void* workspace,
+                  long long ws_bytes, void* stream);
 
 /* sum of S partial slabs: out[r][c] = sum_s in[s*slab + r*ld_in + c] (+ bias[c]); rows x cols */
 int capmi_splitk_reduce(const float* in, int S, long long slab, int rows, int cols, long long ld_in,

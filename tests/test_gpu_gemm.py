@@ -145,3 +145,61 @@ def test_conv1_nchw_gather():
     K.gemm(K.problem(N * Ho * Ho, 64, 147, x.float().to(DEV).contiguous(), 0, w.float().to(DEV).contiguous(),
                      147, out, 64, conv=geo), 3, 0, 0)
     check(out.view(N, Ho, Ho, 64).permute(0, 3, 1, 2), ref, ref_abs, "conv1 NCHW gather")
+
+
+# ---------------------------------------------------------------------------------------
+# stream-K (capmi_gemm_sk): persistent workgroups, k-prefixes parked in the workspace
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("tile", [1, 2, 3])
+@pytest.mark.parametrize("M,N,Kd", [(64, 64, 4608), (1000, 96, 64), (3136, 256, 2304), (200, 130, 300),
+                                    (12544, 64, 128)])
+def test_gemm_sk_linear(tile, M, N, Kd):
+    K = _K()
+    X, W, b = rnd(M, Kd, seed=31), rnd(N, Kd, seed=32), rnd(N, seed=33)
+    ws = K.gemm_workspace(DEV)
+    C = torch.empty(M, N, device=DEV)
+    stats = torch.empty(K.stat_tiles(M), N, 2, device=DEV)
+    # the problem struct holds raw pointers: keep the device operands alive across both launches
+    Xd, Wd, bd = X.float().to(DEV), W.float().to(DEV), b.float().to(DEV)
+    prob = K.problem(M, N, Kd, Xd, Kd, Wd, Kd, C, N, bias=bd, stats=stats)
+    K.gemm_sk(prob, 0, ws, tile)
+    first = C.clone()
+    K.gemm_sk(prob, 0, ws, tile)  # the workspace is reusable and the result deterministic
+    torch.cuda.synchronize()
+    assert torch.equal(first, C)
+    nflags = torch.cuda.get_device_properties(0).multi_processor_count * 4 + 1
+    assert int(ws[:nflags].abs().sum()) == 0, "stream-K flags not left zero (or spin timeout hit)"
+    check(C, X @ W.T + b, X.abs() @ W.abs().T + b.abs(), "stream-K linear")
+    Cd = C.double().cpu()
+    s = stats.double().cpu().sum(0)
+    torch.testing.assert_close(s[:, 0], Cd.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(s[:, 1], (Cd * Cd).sum(0), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("k,stride,cin,cout,hw", [(3, 1, 64, 128, 14), (3, 2, 128, 64, 15), (1, 1, 256, 64, 7)])
+def test_conv_sk_prologue(k, stride, cin, cout, hw):
+    K = _K()
+    N = 4
+    x = rnd(N, cin, hw, hw, seed=34)
+    w = rnd(cout, cin, k, k, seed=35) * 0.1
+    sc, sh = rnd(cin, seed=36), rnd(cin, seed=37)
+    pad = k // 2
+    xin = torch.relu(x * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1))
+    ref = F.conv2d(xin, w, stride=stride, padding=pad)
+    ref_abs = F.conv2d(xin.abs(), w.abs(), stride=stride, padding=pad)
+    Ho = ref.shape[2]
+    x_nhwc = x.permute(0, 2, 3, 1).contiguous().float().to(DEV)
+    wp = torch.empty(cout, k, k, cin, device=DEV)
+    K.conv_weight_pack(w.float().to(DEV).contiguous(), wp)
+    M = N * Ho * Ho
+    out = torch.empty(M, cout, device=DEV)
+    stats = torch.empty(K.stat_tiles(M), cout, 2, device=DEV)
+    geo = dict(N=N, H=hw, W=hw, Cin=cin, KH=k, KW=k, stride=stride, pad=pad, Ho=Ho, Wo=Ho)
+    ws = K.gemm_workspace(DEV)
+    K.gemm_sk(K.problem(M, cout, k * k * cin, x_nhwc, 0, wp, k * k * cin, out, cout, conv=geo, stats=stats,
+                        in_scale=sc.float().to(DEV), in_shift=sh.float().to(DEV)), 2, ws)
+    got = out.view(N, Ho, Ho, cout).permute(0, 3, 1, 2)
+    check(got, ref, ref_abs, f"stream-K conv{k}x{k}/s{stride}")
+    s = stats.double().cpu().sum(0)
+    Cd = out.double().cpu()
+    torch.testing.assert_close(s[:, 0], Cd.sum(0), rtol=1e-5, atol=1e-3)

@@ -14,7 +14,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def header_functions():
     src = open(os.path.join(REPO, "include", "capmi.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(capmi_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?(?:\w+\s+)*\w+\*?\s+\*?(capmi_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_exports_match_header():

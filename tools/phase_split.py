@@ -15,9 +15,10 @@ def short(n):
 def main():
     c = sqlite3.connect(sys.argv[1])
     rows = list(c.execute("select name, duration, start, end from kernels order by start"))
-    starts = [i for i, r in enumerate(rows) if "gemm_kernel<128, 128, 64, 64, 3" in r[0]]
-    i0 = starts[-2]  # a complete step (the last one may be followed by teardown)
-    i1 = starts[-1]
+    starts = [i for i, r in enumerate(rows) if "gemm_kernel<128, 128, 64, 64, 3" in r[0]] + [len(rows)]
+    # the last complete training step: a segment between two conv1 launches that contains Adam
+    segs = [(a, b) for a, b in zip(starts, starts[1:]) if any("adam_clamp" in r[0] for r in rows[a:b])]
+    i0, i1 = segs[-1]
     step = rows[i0:i1]
     wall = step[-1][3] - step[0][2]
     phase = "encoder"
