@@ -18,12 +18,12 @@ LIB_PATH = os.path.join(_HERE, "libcapmi.so")
 c_int, c_ll, c_float, c_double, c_vp = ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
 c_ull = ctypes.c_ulonglong
 
-CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_A_CONV_NHWC, CAPMI_A_CONV_NCHW = 0, 1, 2, 3
+CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_A_CONV_NHWC, CAPMI_A_CONV_NCHW, CAPMI_A_CONV_NHWC4 = 0, 1, 2, 3, 4
 CAPMI_B_NMAJOR_W, CAPMI_B_KROWS = 0, 1
 CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO = 0, 1, 2, 3
 CAPMI_MAX_GROUP = 4
 CAPMI_COLSUM_GROUPS = 64
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class GemmProblem(ctypes.Structure):
@@ -47,10 +47,12 @@ _SIGS = {
     "capmi_gemm": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_int, c_vp],
     "capmi_gemm_stat_tiles": [c_int, c_int],
     "capmi_gemm_workspace_bytes": [],
-    "capmi_gemm_sk": [ctypes.POINTER(GemmProblem), c_int, c_int, c_vp, c_ll, c_vp],
+    "capmi_gemm_sk": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_vp, c_ll, c_vp],
     "capmi_splitk_reduce": [c_vp, c_int, c_ll, c_int, c_int, c_ll, c_vp, c_vp, c_ll, c_vp],
     "capmi_colsum": [c_vp, c_int, c_int, c_ll, c_float, c_vp, c_vp, c_int, c_vp],
     "capmi_conv_weight_pack": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
+    "capmi_conv_weight_pack_pad": [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp],
+    "capmi_image_nhwc4": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_bn_finalize": [c_vp, c_int, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_float, c_float,
                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "capmi_bn_eval_params": [c_vp, c_vp, c_vp, c_vp, c_int, c_float, c_vp, c_vp, c_vp],

@@ -105,6 +105,7 @@ class Workspace:
         self.BF_PART = e(nblk, 1, **f)
         # generic scratch: split-K slabs of the hoisted GEMMs and colsum work
         self.scratch = e(max(8 * T * B * D, 32 * B * D, T * B * M, 256 * 128 * 128), **f)
+        self.sk = K.gemm_workspace(device)  # stream-K workspace of the hoisted GEMMs
         self.work = e(max(K.colsum_work_size(T * B, V), K.colsum_work_size(B * P, A),
                           K.colsum_work_size(T * B, 4 * D), K.colsum_work_size(T * B, E), 64), **f)
 
@@ -126,21 +127,11 @@ class DecoderCore:
 
     # ------------------------------------------------------------------ helpers
     @staticmethod
-    def _gemm_into(ws, out, ld_out, M, N, Kd, A, lda, B, ldb, amode, bmode, bias=None, bias2=None,
-                   tile=K.TILE_128, target=256, **kw):
-        """C = op(A) op(B) (+bias); split-K through ws.scratch + reduce when the tile grid is small."""
-        s = _split(M, N, Kd, tile, target, min_k=256)
-        if s > 1 and s * M * N > ws.scratch.numel():
-            s = max(1, ws.scratch.numel() // (M * N))
-        if s == 1:
-            K.gemm(K.problem(M, N, Kd, A, lda, B, ldb, out, ld_out, bias=bias, bias2=bias2, **kw),
-                   amode, bmode, tile)
-            return
-        K.gemm(K.problem(M, N, Kd, A, lda, B, ldb, ws.scratch, N, ksplit=s, c_split_stride=M * N, **kw),
-               amode, bmode, tile)
-        if bias2 is not None:
-            raise NotImplementedError
-        K.splitk_reduce(ws.scratch, s, M * N, M, N, N, out, ld_out, bias=bias)
+    def _gemm_into(ws, out, ld_out, M, N, Kd, A, lda, B, ldb, amode, bmode, bias=None, **kw):
+        """C = op(A) op(B) (+bias) for the hoisted (all-timestep) GEMMs: stream-K, so a grid of
+        few output tiles (dW_enc_att: 128 tiles of 128x64 over K = B*P) still fills the chip."""
+        K.gemm_sk(K.problem(M, N, Kd, A, lda, B, ldb, out, ld_out, bias=bias, **kw), amode, ws.sk,
+                  K.TILE_AUTO, bmode)
 
     # ------------------------------------------------------------------ forward
     def forward(self, p, enc, caps, decode_lengths, *, dropout_p=0.0, training=False, seed=0,
@@ -174,10 +165,10 @@ class DecoderCore:
         K.splitk_reduce(slab, sh, B * D, B, D, D, ws.H[0], D, bias=p["h_lin.bias"])
         K.splitk_reduce(slab[sh * B * D:], sh, B * D, B, D, D, ws.C[0], D, bias=p["c_lin.bias"])
         # hoisted enc_att (:54) and the embedding half of the LSTM input GEMM
-        K.gemm(K.problem(B * P, A, E, enc, E, p["attention.enc_att.weight"], E, ws.ATT_ENC, A,
-                         bias=p["attention.enc_att.bias"]), AK, BW, K.TILE_AUTO)
-        K.gemm(K.problem(T * B, 4 * D, M, ws.X, X, W_ih, X, ws.XEMB, 4 * D, bias=p["decode_step.bias_ih"],
-                         bias2=p["decode_step.bias_hh"]), AK, BW, K.TILE_AUTO)
+        self._gemm_into(ws, ws.ATT_ENC, A, B * P, A, E, enc, E, p["attention.enc_att.weight"], E, AK, BW,
+                        bias=p["attention.enc_att.bias"])
+        self._gemm_into(ws, ws.XEMB, 4 * D, T * B, 4 * D, M, ws.X, X, W_ih, X, AK, BW,
+                        bias=p["decode_step.bias_ih"], bias2=p["decode_step.bias_hh"])
 
         alphas = torch.empty(B, T, P, device=enc.device, dtype=torch.float32)
         s_a, s_g, s_hh = dm.s_h
@@ -209,8 +200,8 @@ class DecoderCore:
         else:
             Hd = Hcur
         preds = torch.empty(B, T, V, device=enc.device, dtype=torch.float32)
-        K.gemm(K.problem(T * B, V, D, Hd, D, p["fc.weight"], D, preds, T * V, c_r1=B, c_s2=V,
-                         bias=p["fc.bias"]), AK, BW, K.TILE_AUTO)
+        self._gemm_into(ws, preds, T * V, T * B, V, D, Hd, D, p["fc.weight"], D, AK, BW, bias=p["fc.bias"],
+                        c_r1=B, c_s2=V)
         if ragged:
             K.mask_rows_tb(preds, bt_dev, T, B, V, T * V, B, V)
         state = dict(dm=dm, ws=ws, enc=enc, caps=caps, bt=bt, bt_dev=bt_dev, ragged=ragged, alphas=alphas,
@@ -247,8 +238,7 @@ class DecoderCore:
         # ---- fc (:279): dHd = dpred W_fc ; dW_fc = dpred^T Hd ; db_fc = colsum(dpred)
         self._gemm_into(ws, ws.DHD, D, TB, D, V, dpred, lda_p, p["fc.weight"], D, AK, BKR, **ar)
         if "fc.weight" in need:
-            K.gemm(K.problem(V, D, TB, dpred, lda_p, st["Hd"], D, grads["fc.weight"], D, **ar), AMM, BKR,
-                   K.TILE_128)
+            self._gemm_into(ws, grads["fc.weight"], D, V, D, TB, dpred, lda_p, st["Hd"], D, AMM, BKR, **ar)
         if "fc.bias" in need:
             K.colsum(dpred, TB, V, V, grads["fc.bias"], ws.work)
         if st["dropout_p"] > 0:

@@ -74,9 +74,10 @@ def gemm_workspace(device):
     return torch.zeros(n, device=device, dtype=torch.int32)
 
 
-def gemm_sk(prob, amode, workspace, tile=CAPMI_TILE_AUTO):
+def gemm_sk(prob, amode, workspace, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W):
     _cuda(workspace, dtype=torch.int32)
-    call("capmi_gemm_sk", ctypes.byref(prob), amode, tile, ptr(workspace), workspace.numel() * 4, stream())
+    call("capmi_gemm_sk", ctypes.byref(prob), amode, bmode, tile, ptr(workspace), workspace.numel() * 4,
+         stream())
 
 
 def stat_tiles(M, tile=CAPMI_TILE_128):
@@ -115,8 +116,23 @@ def conv_weight_pack(w, out):
     call("capmi_conv_weight_pack", ptr(w), co, ci, kh, kw, ptr(out), stream())
 
 
+def conv_weight_pack_pad(w, cin_pad, out):
+    _cuda(w, out)
+    co, ci, kh, kw = w.shape
+    assert w.is_contiguous() and out.numel() == co * kh * kw * cin_pad
+    call("capmi_conv_weight_pack_pad", ptr(w), co, ci, kh, kw, cin_pad, ptr(out), stream())
+
+
+def image_nhwc4(imgs, out):
+    _cuda(imgs, out)
+    N, C, H, W = imgs.shape
+    assert imgs.is_contiguous() and out.numel() >= N * H * W * 4
+    call("capmi_image_nhwc4", ptr(imgs), N, C, H, W, ptr(out), stream())
+
+
 def bn_work_doubles(C):
-    return 128 * 2 * C
+    """CAPMI_BN_WORK_DOUBLES: 64 counter doubles + fp64 partials (allocate zeroed)."""
+    return 64 + 64 * C
 
 
 def bn_finalize(stats, tiles, C, count, gamma, beta, running_mean, running_var, momentum, eps,

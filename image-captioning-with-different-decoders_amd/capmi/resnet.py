@@ -17,7 +17,7 @@ import torch
 import torch.nn as nn
 
 from . import kernels as K
-from ._lib import CAPMI_A_CONV_NCHW, CAPMI_A_CONV_NHWC, CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W
+from ._lib import CAPMI_A_CONV_NHWC, CAPMI_A_CONV_NHWC4, CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W
 
 
 class Bottleneck(nn.Module):
@@ -91,7 +91,8 @@ def resnet101(weights_path=None):
 # fused forward
 # ======================================================================================
 class _Packed:
-    """Conv weights in the GEMM's B layout: [Cout][KH][KW][Cin] (K-contiguous)."""
+    """Conv weights in the GEMM's B layout: [Cout][KH][KW][Cin] (K-contiguous; Cin padded to 4
+    for conv1)."""
 
     def __init__(self):
         self.cache = {}
@@ -101,13 +102,12 @@ class _Packed:
         co, ci, kh, kw = w.shape
         if kh == 1 and kw == 1:
             return w  # [Cout][Cin] already
-        if ci % 16:  # conv1 (Cin = 3): consumed in its native [Cout][Cin][KH][KW] order
-            return w
+        cp = 4 if ci <= 4 else ci  # conv1 (Cin = 3): channels zero-padded to 4 (NHWC4 input)
         key = id(conv)
         ent = self.cache.get(key)
         if ent is None or ent[0] != w._version or ent[1] != w.data_ptr():
-            packed = torch.empty(co, kh, kw, ci, device=w.device, dtype=w.dtype)
-            K.conv_weight_pack(w.detach().contiguous(), packed)
+            packed = torch.empty(co, kh, kw, cp, device=w.device, dtype=w.dtype)
+            K.conv_weight_pack_pad(w.detach().contiguous(), cp, packed)
             ent = (w._version, w.data_ptr(), packed)
             self.cache[key] = ent
         return ent[2]
@@ -132,9 +132,11 @@ class EncoderRunner:
             f = dict(device=device, dtype=torch.float32)
             ws = {n: torch.empty(big, **f) for n in ("x", "y1", "y2", "y3", "yd", "out")}
             ws["stats"] = torch.empty(2 * ((N * H1 * W1 + 63) // 64) * 256, **f)
-            ws["bnwork"] = torch.empty(K.bn_work_doubles(2048), device=device, dtype=torch.float64)
+            # zeroed once: holds the BN finalize arrival counters, re-armed by the kernel
+            ws["bnwork"] = torch.zeros(K.bn_work_doubles(2048), device=device, dtype=torch.float64)
             ws["ss"] = {}
             ws["sk"] = K.gemm_workspace(device)  # stream-K partials + flags (zeroed once)
+            ws["img4"] = torch.empty(N * H * W * 4, **f)  # conv1 input, NHWC padded to 4 channels
             self._ws, self._ws_key = ws, key
         return self._ws
 
@@ -172,8 +174,14 @@ class EncoderRunner:
         stats = ws_stats = self._ws["stats"] if train else None
         kw_ = dict(stats=ws_stats)
         if nchw:
-            prob = K.problem(rows, co, Kd, x, 0, w, Kd, out, co, conv=geo, **kw_)
-            mode = CAPMI_A_CONV_NCHW
+            # conv1: the NCHW images are re-laid out once as NHWC with 4 channels (one float4 per
+            # pixel); the implicit GEMM then runs over k = (kh, kw, c4), the 4th channel zero
+            img4 = self._ws["img4"]
+            K.image_nhwc4(x, img4)
+            K4 = kh * kw * 4
+            geo["Cin"] = 4
+            prob = K.problem(rows, co, K4, img4, 0, w, K4, out, co, conv=geo, **kw_)
+            mode = CAPMI_A_CONV_NHWC4
         elif kh == 1 and st == 1 and in_ss is None:
             prob = K.problem(rows, co, Kd, x, ci, w, Kd, out, co, **kw_)
             mode = CAPMI_A_KMAJOR
@@ -181,10 +189,7 @@ class EncoderRunner:
             sc, sh = in_ss if in_ss is not None else (None, None)
             prob = K.problem(rows, co, Kd, x, 0, w, Kd, out, co, conv=geo, in_scale=sc, in_shift=sh, **kw_)
             mode = CAPMI_A_CONV_NHWC
-        if nchw:
-            launch = lambda: K.gemm(prob, mode, CAPMI_B_NMAJOR_W, K.TILE_AUTO)  # noqa: E731
-        else:
-            launch = lambda: K.gemm_sk(prob, mode, self._ws["sk"], K.TILE_AUTO)  # noqa: E731
+        launch = lambda: K.gemm_sk(prob, mode, self._ws["sk"], K.TILE_AUTO)  # noqa: E731
         if self.conv_hook is not None:
             self.conv_hook(tag, 2.0 * rows * co * Kd, launch)
         else:

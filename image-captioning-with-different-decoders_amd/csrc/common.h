@@ -75,6 +75,30 @@ __device__ __forceinline__ float4 fma4(float4 a, float4 b, float4 c) {
 __device__ __forceinline__ float4 relu4(float4 a) {
   return make_float4(fmaxf(a.x, 0.f), fmaxf(a.y, 0.f), fmaxf(a.z, 0.f), fmaxf(a.w, 0.f));
 }
+// init + sum of the S split-K partial slabs p[s * slab], s = 0..S-1, added in slab order (the
+// same rounding as a plain loop) but with up to 8 loads in flight instead of one
+template <typename T>
+__device__ __forceinline__ T slab_sum(const T* __restrict__ p, int S, long long slab, T acc) {
+  int s = 0;
+  for (; s + 8 <= S; s += 8) {
+    T v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(s + u) * slab];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = acc + v[u];
+  }
+  if (s + 4 <= S) {
+    T v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = p[(s + u) * slab];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = acc + v[u];
+    s += 4;
+  }
+  for (; s < S; ++s) acc = acc + p[s * slab];
+  return acc;
+}
+
 __device__ __forceinline__ float dot4(float4 a, float4 b) {
   return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
 }

@@ -84,8 +84,7 @@ __global__ void __launch_bounds__(256) att_score_fwd_kernel(
   float* ad = smem;  // [A]
   const int b = blockIdx.y, p0 = blockIdx.x * PCH;
   for (int a = threadIdx.x; a < A; a += blockDim.x) {
-    float v = bias_da ? bias_da[a] : 0.f;
-    for (int s = 0; s < S; ++s) v += dec_part[s * dec_slab + (long long)b * A + a];
+    const float v = slab_sum(dec_part + (long long)b * A + a, S, dec_slab, bias_da ? bias_da[a] : 0.f);
     ad[a] = v;
     if (att_dec_out && blockIdx.x == 0) att_dec_out[(long long)b * A + a] = v;
   }
@@ -178,8 +177,8 @@ __global__ void __launch_bounds__(256) att_softmax_ctx_fwd_kernel(
     if (awe_out) *reinterpret_cast<float4*>(awe_out + o) = awe;
     float4 xg = awe;
     if (gate_part) {
-      float4 g = *reinterpret_cast<const float4*>(bias_fb + c);
-      for (int z = 0; z < S; ++z) g = g + *reinterpret_cast<const float4*>(gate_part + z * gate_slab + o);
+      float4 g = slab_sum(reinterpret_cast<const float4*>(gate_part + o), S, gate_slab / 4,
+                          *reinterpret_cast<const float4*>(bias_fb + c));
       g = make_float4(sigmoidf_(g.x), sigmoidf_(g.y), sigmoidf_(g.z), sigmoidf_(g.w));
       if (gate_out) *reinterpret_cast<float4*>(gate_out + o) = g;
       xg = g * awe;
@@ -228,10 +227,8 @@ __global__ void lstm_cell_fwd_kernel(const float* __restrict__ part, int S, long
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const long long o = (long long)b * 4 * D + q * D + j;
-      float v = xemb ? xemb[o] : 0.f;
-      for (int s = 0; s < S; ++s) v += part[s * slab + o];
-      for (int s = 0; s < S2; ++s) v += hh_part[s * slab2 + o];
-      g[q] = v;
+      float v = slab_sum(part + o, S, slab, xemb ? xemb[o] : 0.f);
+      g[q] = slab_sum(hh_part + o, S2, slab2, v);
     }
     const float ig = sig_(g[0]), fg = sig_(g[1]), cg = tanhf(g[2]), og = sig_(g[3]);
     const float c = fg * c_prev[i] + ig * cg;
@@ -253,7 +250,8 @@ extern "C" int capmi_lstm_cell_fwd(const float* part, int S, long long slab, con
   CAPMI_REQUIRE(c_prev && h_out && c_out && act_out && B > 0 && D > 0, CAPMI_EINVAL);
   CAPMI_REQUIRE((S == 0 || part) && (S2 == 0 || hh_part), CAPMI_EINVAL);
   const long long n = (long long)B * D;
-  hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, as_stream(stream),
+  // one lane per (b, j), 64-lane workgroups: B*D = 32768 -> 512 WGs (all CUs busy)
+  hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3(cdiv(n, 64)), dim3(64), 0, as_stream(stream),
                      part, S, slab, xemb, hh_part, S2, slab2, c_prev, B, D, h_out, c_out, act_out);
   CAPMI_LAUNCH_CHECK();
   return 0;
@@ -457,8 +455,7 @@ __global__ void lstm_cell_bwd_kernel(const float* __restrict__ dhd, const float*
       dc_out[i] = 0.f;
       continue;
     }
-    float dh = dhd ? dhd[i] : 0.f;
-    for (int s = 0; s < S; ++s) dh += dh_part[s * slab + i];
+    const float dh = slab_sum(dh_part + i, S, slab, dhd ? dhd[i] : 0.f);
     float dc = dc_in ? dc_in[i] : 0.f;
     const float ig = act[o], fg = act[o + D], cg = act[o + 2 * D], og = act[o + 3 * D];
     const float tc = tanhf(c_cur[i]);
@@ -482,7 +479,7 @@ extern "C" int capmi_lstm_cell_bwd(const float* dhd, const float* dh_part, int S
   CAPMI_REQUIRE(act && c_prev && c_cur && dgates && dc_out && B > 0 && D > 0, CAPMI_EINVAL);
   CAPMI_REQUIRE(S == 0 || dh_part, CAPMI_EINVAL);
   const long long n = (long long)B * D;
-  hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3(cdiv(n, 256)), dim3(256), 0, as_stream(stream), dhd,
+  hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3(cdiv(n, 64)), dim3(64), 0, as_stream(stream), dhd,
                      dh_part, S, slab, dc_in, act, c_prev, c_cur, B, D, bt, dgates, dc_out);
   CAPMI_LAUNCH_CHECK();
   return 0;
@@ -498,8 +495,8 @@ __global__ void __launch_bounds__(256) att_ctx_bwd_kernel(
   const int b = blockIdx.y, p0 = blockIdx.x * PCH;
   for (int c = threadIdx.x * 4; c < E; c += 1024) {
     const long long o = (long long)b * E + c;
-    float4 d = *reinterpret_cast<const float4*>(part + o);
-    for (int s = 1; s < S; ++s) d = d + *reinterpret_cast<const float4*>(part + s * slab + o);
+    const float4 d = slab_sum(reinterpret_cast<const float4*>(part + slab + o), S - 1, slab / 4,
+                              *reinterpret_cast<const float4*>(part + o));
     float4 dw = d;
     if (gate) {
       const float4 g = *reinterpret_cast<const float4*>(gate + o);

@@ -9,89 +9,151 @@
 #include "common.h"
 
 __global__ void conv_weight_pack_kernel(const float* __restrict__ w, int Cout, int Cin, int KH,
-                                        int KW, float* __restrict__ out) {
-  const long long n = (long long)Cout * Cin * KH * KW;
+                                        int KW, int Cp, float* __restrict__ out) {
+  const long long n = (long long)Cout * Cp * KH * KW;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
-    // i indexes the OUTPUT [co][kh][kw][ci]
-    const int ci = (int)(i % Cin);
-    long long r = i / Cin;
+    // i indexes the OUTPUT [co][kh][kw][cp]; channels ci >= Cin are zero padding
+    const int ci = (int)(i % Cp);
+    long long r = i / Cp;
     const int kw = (int)(r % KW);
     r /= KW;
     const int kh = (int)(r % KH);
     const int co = (int)(r / KH);
-    out[i] = w[(((long long)co * Cin + ci) * KH + kh) * KW + kw];
+    out[i] = ci < Cin ? w[(((long long)co * Cin + ci) * KH + kh) * KW + kw] : 0.f;
   }
+}
+
+extern "C" int capmi_conv_weight_pack_pad(const float* w, int Cout, int Cin, int KH, int KW, int Cin_pad,
+                                          float* out, void* stream) {
+  CAPMI_REQUIRE(w && out && Cout > 0 && Cin > 0 && KH > 0 && KW > 0 && Cin_pad >= Cin, CAPMI_EINVAL);
+  const long long n = (long long)Cout * Cin_pad * KH * KW;
+  hipLaunchKernelGGL(conv_weight_pack_kernel, dim3(std::min<long long>(cdiv(n, 256), 8192)),
+                     dim3(256), 0, as_stream(stream), w, Cout, Cin, KH, KW, Cin_pad, out);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
 }
 
 extern "C" int capmi_conv_weight_pack(const float* w, int Cout, int Cin, int KH, int KW, float* out,
                                       void* stream) {
-  CAPMI_REQUIRE(w && out && Cout > 0 && Cin > 0 && KH > 0 && KW > 0, CAPMI_EINVAL);
-  const long long n = (long long)Cout * Cin * KH * KW;
-  hipLaunchKernelGGL(conv_weight_pack_kernel, dim3(std::min<long long>(cdiv(n, 256), 8192)),
-                     dim3(256), 0, as_stream(stream), w, Cout, Cin, KH, KW, out);
+  return capmi_conv_weight_pack_pad(w, Cout, Cin, KH, KW, Cin, out, stream);
+}
+
+// NCHW (C <= 4) -> NHWC with 4 channels (zero padded): one float4 per pixel
+__global__ void image_nhwc4_kernel(const float* __restrict__ in, int N, int C, long long HW,
+                                   float4* __restrict__ out) {
+  const long long n = N * HW;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long b = i / HW, px = i - b * HW;
+    const float* src = in + b * C * HW + px;
+    float4 v = f4(0.f);
+    if (C > 0) v.x = src[0];
+    if (C > 1) v.y = src[HW];
+    if (C > 2) v.z = src[2 * HW];
+    if (C > 3) v.w = src[3 * HW];
+    out[i] = v;
+  }
+}
+
+extern "C" int capmi_image_nhwc4(const float* in, int N, int C, int H, int W, float* out, void* stream) {
+  CAPMI_REQUIRE(in && out && N >= 0 && C >= 1 && C <= 4 && H > 0 && W > 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE(aligned16(out), CAPMI_EALIGN);
+  const long long n = (long long)N * H * W;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(image_nhwc4_kernel, dim3(std::min<long long>(cdiv(n, 256), 16384)), dim3(256), 0,
+                     as_stream(stream), in, N, C, (long long)H * W, reinterpret_cast<float4*>(out));
   CAPMI_LAUNCH_CHECK();
   return 0;
 }
 
 // ---------------------------------------------------------------------------------
-// BN finalize, two stages: (1) G slice-groups x 64 channels, fp64 partial sums per group;
-// (2) per channel: combine the G partials, mean/var -> scale/shift, running stats.
+// BN finalize: G slice-groups x 64 channels reduce the GEMM's per-slice (Σ, Σx²) in fp64,
+// the last group of each channel block turns them into scale/shift and running stats.
 // ---------------------------------------------------------------------------------
 constexpr int BNF_MAXG = 32;
 
-__global__ void bn_stats_stage1(const float* __restrict__ stats, int tiles, int C, int per_g,
-                                double* __restrict__ part) {
+// One launch: block (cb, g) reduces slice group g of channels [64cb, 64cb+64) to fp64 (Σ, Σx²),
+// publishes it with write-through (sc1) 8-B stores and bumps the channel block's arrival
+// counter; the block whose add returns G-1 is the last one and finalizes those 64 channels,
+// summing the G partials in group order (deterministic) behind one agent-scope acquire, then
+// re-arms the counter to 0. The counters live in the caller's work buffer, zeroed once.
+__global__ void bn_finalize_kernel(const float* __restrict__ stats, int tiles, int C, int per_g,
+                                   unsigned long long* part, int* counters, long long count,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* running_mean, float* running_var, float momentum, float eps,
+                                   float* __restrict__ scale, float* __restrict__ shift, float* save_mean,
+                                   float* save_var) {
   __shared__ double rs[4][64], rq[4][64];
   const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
+  const int G = gridDim.y;
   const int t0 = blockIdx.y * per_g, t1 = min(tiles, t0 + per_g);
   double s = 0.0, q = 0.0;
   if (c < C) {
-    for (int t = t0 + tl; t < t1; t += 4) {
-      const float2 v = *reinterpret_cast<const float2*>(stats + ((long long)t * C + c) * 2);
-      s += v.x;
-      q += v.y;
+    // 8 slice loads in flight per lane (a latency-bound loop otherwise), summed in slice order
+    for (int t = t0 + tl; t < t1; t += 32) {
+      float2 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int tt = t + 4 * u;
+        v[u] = tt < t1 ? *reinterpret_cast<const float2*>(stats + ((long long)tt * C + c) * 2)
+                       : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s += v[u].x;
+        q += v[u].y;
+      }
     }
   }
   rs[tl][cl] = s;
   rq[tl][cl] = q;
   __syncthreads();
-  if (tl == 0 && c < C) {
+  if (tl != 0) return;  // wave 0 publishes, and finalizes if it arrives last
+  if (c < C) {
     s = rs[0][cl] + rs[1][cl] + rs[2][cl] + rs[3][cl];
     q = rq[0][cl] + rq[1][cl] + rq[2][cl] + rq[3][cl];
-    part[((long long)blockIdx.y * C + c) * 2 + 0] = s;
-    part[((long long)blockIdx.y * C + c) * 2 + 1] = q;
+    unsigned long long* p = part + ((long long)blockIdx.y * C + c) * 2;
+    __hip_atomic_store(p, (unsigned long long)__double_as_longlong(s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 1, (unsigned long long)__double_as_longlong(q), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
-}
-
-__global__ void bn_stats_stage2(const double* __restrict__ part, int G, int C, long long count,
-                                const float* __restrict__ gamma, const float* __restrict__ beta,
-                                float* running_mean, float* running_var, float momentum, float eps,
-                                float* __restrict__ scale, float* __restrict__ shift,
-                                float* save_mean, float* save_var) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int g = 0; g < G; ++g) {
-    s += part[((long long)g * C + c) * 2 + 0];
-    q += part[((long long)g * C + c) * 2 + 1];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int prev = 0;
+  if (cl == 0) prev = __hip_atomic_fetch_add(counters + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  prev = __shfl(prev, 0, 64);
+  if (prev != G - 1) return;
+  // one agent-scope acquire (drops this CU's L1), then plain loads that can all be in flight
+  // at once (sc1 atomic loads of the G partials would be issued one after the other)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (c < C) {
+    const double2* pd = reinterpret_cast<const double2*>(part);
+    s = 0.0;
+    q = 0.0;
+    for (int g = 0; g < G; ++g) {
+      const double2 v = pd[(long long)g * C + c];
+      s += v.x;
+      q += v.y;
+    }
+    const double n = (double)count;
+    const double mean = s / n;
+    double var = q / n - mean * mean;
+    if (var < 0) var = 0;
+    const double inv = 1.0 / sqrt(var + (double)eps);
+    const float sc = (float)((double)gamma[c] * inv);
+    scale[c] = sc;
+    shift[c] = (float)((double)beta[c] - mean * (double)sc);
+    if (save_mean) save_mean[c] = (float)mean;
+    if (save_var) save_var[c] = (float)var;
+    if (running_mean) {
+      const double unb = count > 1 ? var * n / (n - 1.0) : var;
+      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+      running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+    }
   }
-  const double n = (double)count;
-  const double mean = s / n;
-  double var = q / n - mean * mean;
-  if (var < 0) var = 0;
-  const double inv = 1.0 / sqrt(var + (double)eps);
-  const float sc = (float)((double)gamma[c] * inv);
-  scale[c] = sc;
-  shift[c] = (float)((double)beta[c] - mean * (double)sc);
-  if (save_mean) save_mean[c] = (float)mean;
-  if (save_var) save_var[c] = (float)var;
-  if (running_mean) {
-    const double unb = count > 1 ? var * n / (n - 1.0) : var;
-    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
-  }
+  if (cl == 0) __hip_atomic_store(counters + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 extern "C" int capmi_bn_finalize(const float* stats, int tiles, int C, long long count,
@@ -102,15 +164,17 @@ extern "C" int capmi_bn_finalize(const float* stats, int tiles, int C, long long
   CAPMI_REQUIRE(stats && gamma && beta && scale && shift && work && tiles > 0 && C > 0 && count > 0,
                 CAPMI_EINVAL);
   CAPMI_REQUIRE((running_mean == nullptr) == (running_var == nullptr), CAPMI_EINVAL);
-  CAPMI_REQUIRE(((uintptr_t)stats & 7) == 0 && ((uintptr_t)work & 7) == 0, CAPMI_EALIGN);
+  CAPMI_REQUIRE(((uintptr_t)stats & 7) == 0 && ((uintptr_t)work & 15) == 0, CAPMI_EALIGN);
   const int G = std::min(BNF_MAXG, std::max(1, (tiles + 31) / 32));
   const int per_g = (tiles + G - 1) / G;
-  hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(bn_stats_stage1, dim3(cdiv(C, 64), G), dim3(256), 0, s, stats, tiles, C, per_g,
-                     (double*)work);
-  hipLaunchKernelGGL(bn_stats_stage2, dim3(cdiv(C, 256)), dim3(256), 0, s, (const double*)work, G, C,
-                     count, gamma, beta, running_mean, running_var, momentum, eps, scale, shift,
-                     save_mean, save_var);
+  CAPMI_REQUIRE(C <= 8192, CAPMI_ERANGE);
+  // [0, 64 doubles): the arrival counters (one int per 64-channel block, fixed place whatever
+  // C is, so BN layers of different widths can share one zeroed work buffer); then partials
+  int* counters = static_cast<int*>(work);
+  unsigned long long* part = static_cast<unsigned long long*>(work) + 64;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64), G), dim3(256), 0, as_stream(stream), stats,
+                     tiles, C, per_g, part, counters, count, gamma, beta, running_mean, running_var,
+                     momentum, eps, scale, shift, save_mean, save_var);
   CAPMI_LAUNCH_CHECK();
   return 0;
 }

@@ -391,13 +391,16 @@ struct GemmPlan {
 
 int gemm_plan(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, int tile, GemmPlan& g) {
   CAPMI_REQUIRE(probs != nullptr && nprob >= 1 && nprob <= CAPMI_MAX_GROUP, CAPMI_EINVAL);
-  CAPMI_REQUIRE(amode >= 0 && amode <= 3 && bmode >= 0 && bmode <= 1, CAPMI_EINVAL);
+  CAPMI_REQUIRE(amode >= 0 && amode <= 4 && bmode >= 0 && bmode <= 1, CAPMI_EINVAL);
   CAPMI_REQUIRE(tile >= CAPMI_TILE_128 && tile <= CAPMI_TILE_AUTO, CAPMI_EINVAL);
+  CAPMI_REQUIRE(amode != 4 || bmode == 0, CAPMI_EINVAL);
   GemmArgs& a = g.a;
   memset(&a, 0, sizeof(a));
   a.nprob = nprob;
   bool vec = true;
-  bool nt_ok = (amode == 0 || amode == 2) && bmode == 0;  // v2 kernel eligible
+  // v2 kernel eligible: row-major A (dense / conv) with B = W[N][K], or the transposed-staging
+  // forms (A stored as k rows and/or B stored as k rows) of the backward GEMMs
+  bool nt_ok = ((amode == 0 || amode == 2 || amode == 4) && bmode == 0) || ((amode == 0 || amode == 1) && bmode == 1);
   int maxN = 0;
   for (int i = 0; i < nprob; ++i) {
     const capmi_gemm_problem& p = probs[i];
@@ -414,6 +417,11 @@ int gemm_plan(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, 
       CAPMI_REQUIRE(aligned16(p.B) && p.ldb % 4 == 0, CAPMI_EALIGN);
       nt_ok = nt_ok && p.cCin % 32 == 0;
     }
+    if (amode == 4) {
+      CAPMI_REQUIRE(p.cCin == 4 && p.K == p.cKH * p.cKW * 4 && p.M == p.cN * p.cHo * p.cWo, CAPMI_EINVAL);
+      CAPMI_REQUIRE(aligned16(p.A) && aligned16(p.B) && p.ldb % 4 == 0 && p.in_scale == nullptr,
+                    CAPMI_EALIGN);
+    }
     if (amode == 3) {
       CAPMI_REQUIRE(p.K == p.cKH * p.cKW * p.cCin && p.M == p.cN * p.cHo * p.cWo, CAPMI_EINVAL);
     }
@@ -429,7 +437,7 @@ int gemm_plan(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, 
     a.p[i] = p;
     maxN = std::max(maxN, p.N);
   }
-  nt_ok = nt_ok && (vec || amode == 2);
+  nt_ok = nt_ok && (vec || ((amode == 2 || amode == 4) && bmode == 0));
   int bm = 128, bn = 128;
   if (tile == CAPMI_TILE_64) {
     bm = bn = 64;
@@ -469,7 +477,7 @@ int gemm_plan(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, 
 
 int gemm_launch_dp(const GemmPlan& g, int amode, int bmode, hipStream_t s) {
   if (g.total == 0) return 0;
-  if (g.nt_ok) return gemm_nt_launch(g.a, amode, g.bm, g.bn, (int)g.total, s);
+  if (g.nt_ok) return gemm_nt_launch(g.a, amode, bmode, g.bm, g.bn, (int)g.total, s);
   if (g.bm == 128) return launch_mode<128, 128, 64, 64>(g.a, amode, bmode, g.vec, (int)g.total, s);
   return launch_mode<64, 64, 32, 32>(g.a, amode, bmode, g.vec, (int)g.total, s);
 }
@@ -506,8 +514,8 @@ extern "C" long long capmi_gemm_workspace_bytes(void) {
   return sk_flag_bytes(cus) + (long long)cus * 128 * 1024;
 }
 
-extern "C" int capmi_gemm_sk(const capmi_gemm_problem* prob, int amode, int tile, void* workspace,
-                             long long ws_bytes, void* stream) {
+extern "C" int capmi_gemm_sk(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
+                             void* workspace, long long ws_bytes, void* stream) {
   CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
   const int nkt = (prob->K + 31) / 32;
   const bool automatic = tile == CAPMI_TILE_AUTO;
@@ -516,7 +524,7 @@ extern "C" int capmi_gemm_sk(const capmi_gemm_problem* prob, int amode, int tile
   // pipeline fill outweighs the balance gain and 64x64 data-parallel wins
   if (automatic) tile = nkt >= 16 ? CAPMI_TILE_128x64 : CAPMI_TILE_64;
   GemmPlan g;
-  const int rc = gemm_plan(prob, 1, amode, CAPMI_B_NMAJOR_W, tile, g);
+  const int rc = gemm_plan(prob, 1, amode, bmode, tile, g);
   if (rc) return rc;
   hipStream_t s = as_stream(stream);
   const int cus = cu_count();
@@ -530,14 +538,14 @@ extern "C" int capmi_gemm_sk(const capmi_gemm_problem* prob, int amode, int tile
     const long long rounds = (tiles + slots - 1) / slots;
     sk = (double)tiles / (double)(rounds * slots) < 0.9;
   }
-  if (!sk) return gemm_launch_dp(g, amode, CAPMI_B_NMAJOR_W, s);
+  if (!sk) return gemm_launch_dp(g, amode, bmode, s);
   GemmArgs& a = g.a;
   a.sk_nkt = (prob->K + 31) / 32;
   a.sk_units = tiles * a.sk_nkt;
   a.sk_workers = (int)std::min<long long>(slots, a.sk_units);
   a.sk_flags = static_cast<int*>(workspace);
   a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
-  return gemm_nt_launch(a, amode, g.bm, g.bn, a.sk_workers, s);
+  return gemm_nt_launch(a, amode, bmode, g.bm, g.bn, a.sk_workers, s);
 }
 
 // ------------------------------------------------------------------------------------
@@ -551,9 +559,7 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ in, int S, long l
        i += (long long)gridDim.x * blockDim.x) {
     const int r = (int)(i / cols), c = (int)(i - (long long)r * cols);
     const float* p = in + r * ld_in + c;
-    float s = bias ? bias[c] : 0.f;
-    for (int z = 0; z < S; ++z) s += p[z * slab];
-    out[r * ld_out + c] = s;
+    out[r * ld_out + c] = slab_sum(p, S, slab, bias ? bias[c] : 0.f);
   }
 }
 

@@ -12,6 +12,8 @@
 //   * the next k-tile's global loads are only ISSUED at the top of a k-step (masked slots
 //     read a valid dummy address); masking and the fused BN-apply+ReLU prologue are applied
 //     when the registers are written to LDS, after the MFMAs, so load latency overlaps math;
+//   * conv1 (Cin = 3) runs on an NHWC copy of the images padded to 4 channels (AMODE 4): a
+//     float4 is one pixel, k = (kh, kw, c4);
 //   * the conv's (kh, kw, ci) walk is incremental (no integer division in the k loop) and
 //     every problem field is read once into registers before the loop;
 //   * tile shapes 128x128 / 128x64 / 64x64 (4 waves, 2x2) so grids of the small-M layers
@@ -34,11 +36,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t slot_rsrc(float* base, long lo
   return __builtin_amdgcn_make_buffer_rsrc(p, 0, 256 * 1024, 0x00020000);
 }
 
+// transposed staging: v = 4 consecutive m (or n) at one k -> rows d, d+S2, d+2S2, d+3S2 of
+// the [m][k] LDS image; store j writes component (j + r) & 3, r = (tid & 15) >> 2
+__device__ __forceinline__ void store_t4(float* d, const float4 v, int tid) {
+  const int r = (tid & 15) >> 2;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = (j + r) & 3;
+    const float x = c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
+    d[c * S2] = x;
+  }
+}
+
 // resident workgroups per SIMD the register budget is sized for (== gemm_nt_wg_per_cu)
 template <int BM, int BN>
 constexpr int kWavesPerEu = (BM == 64 && BN == 64) ? 4 : 2;
 
-template <int BM, int BN, int AMODE, bool PRO, bool SK>
+template <int BM, int BN, int AMODE, int BMODE, bool PRO, bool SK>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWavesPerEu<BM, BN>)))
 gemm_nt_kernel(const GemmArgs args) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
@@ -73,13 +87,30 @@ gemm_nt_kernel(const GemmArgs args) {
     const float* __restrict__ isc = P.in_scale;
     const float* __restrict__ ish = P.in_shift;
 
-    // staging slots: float4 f -> (row f>>3, k 4*(f&7))
-    long long a_base[NA];  // dense: row offset; conv: image base offset
+    // staging slots. Row-major operands (k contiguous): float4 f -> (row f>>3, k 4*(f&7)).
+    // Transposed operands (AMODE 1 / BMODE 1: stored as k rows, m/n contiguous): slot i of
+    // thread tid holds the float4 at column group jq = tid%16 + 16*(i % (Q/16)) of k-row
+    // tid/16 + 16*(i / (Q/16)) (16 lanes read 256 contiguous bytes of a k-row), and writes it
+    // to the same [m][k] LDS image by four scalar stores whose order is rotated by
+    // (tid%16)>>2, which makes every one of them bank-conflict-free (64 distinct banks).
+    constexpr int AQ = BM / 4, BQ = BN / 4;  // float4s per k-row of a transposed tile
+    constexpr int AQ16 = AQ / 16, BQ16 = BQ / 16;
+    long long a_base[NA];  // dense: row offset; conv: image base offset; transposed: column
     int a_ih0[NA], a_iw0[NA];
     bool a_ok[NA];
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int row = m0 + ((tid + i * 256) >> 3);
+      const int f = tid + i * 256;
+      if (AMODE == 1) {
+        const int jq = (tid & 15) + 16 * (i % AQ16);
+        const int m = m0 + jq * 4;
+        a_ok[i] = m < M;  // M % 4 == 0
+        a_base[i] = m;
+        a_ih0[i] = (tid >> 4) + 16 * (i / AQ16);  // k within the tile
+        a_iw0[i] = jq;
+        continue;
+      }
+      const int row = m0 + (f >> 3);
       a_ok[i] = row < M;
       if (AMODE == 0) {
         a_base[i] = a_ok[i] ? remap(row, P.a_r1, P.lda, P.a_s2) : 0;
@@ -94,12 +125,23 @@ gemm_nt_kernel(const GemmArgs args) {
       }
     }
     long long b_base[NB];
+    int b_k[NB];
     bool b_ok[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int n = n0 + ((tid + i * 256) >> 3);
-      b_ok[i] = n < N;
-      b_base[i] = b_ok[i] ? (long long)n * ldb : 0;
+      const int f = tid + i * 256;
+      if (BMODE == 1) {
+        const int jq = (tid & 15) + 16 * (i % BQ16);
+        const int n = n0 + jq * 4;
+        b_ok[i] = n < N;  // N % 4 == 0
+        b_base[i] = n;
+        b_k[i] = (tid >> 4) + 16 * (i / BQ16);
+      } else {
+        const int n = n0 + (f >> 3);
+        b_ok[i] = n < N;
+        b_base[i] = b_ok[i] ? (long long)n * ldb : 0;
+        b_k[i] = 0;
+      }
     }
     // conv k walk: k = ((kh * KW) + kw) * Cin + ci, advanced by BK2 per k-tile
     int c_ci = 0, c_kh = 0, c_kw = 0;
@@ -129,6 +171,26 @@ gemm_nt_kernel(const GemmArgs args) {
           st.ra[i] = *reinterpret_cast<const float4*>(Ag + (ok ? a_base[i] + k : 0));
           st.am |= (unsigned)ok << i;
         }
+      } else if (AMODE == 1) {
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+          const int kr = k_lo + kt * BK2 + a_ih0[i];
+          const bool ok = a_ok[i] && kr < k_hi;
+          const long long off = remap(kr, P.a_r1, P.lda, P.a_s2) + a_base[i];
+          st.ra[i] = *reinterpret_cast<const float4*>(Ag + (ok ? off : 0));
+          st.am |= (unsigned)ok << i;
+        }
+      } else if (AMODE == 4) {
+        // NHWC4 (conv1): one float4 = the 4 (zero-padded) channels of one input pixel
+        const int pos = k >> 2, kh = pos / cKW, kw = pos - kh * cKW;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+          const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
+          const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
+          const long long off = a_base[i] + ((long long)(ih * cW + iw)) * 4;
+          st.ra[i] = *reinterpret_cast<const float4*>(Ag + (ok ? off : 0));
+          st.am |= (unsigned)ok << i;
+        }
       } else {
         const int ci = c_ci + kq;
         if (PRO) {
@@ -154,9 +216,16 @@ gemm_nt_kernel(const GemmArgs args) {
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const bool ok = b_ok[i] && kok;
-        st.rb[i] = *reinterpret_cast<const float4*>(Bg + (ok ? b_base[i] + k : 0));
-        st.bm |= (unsigned)ok << i;
+        if (BMODE == 1) {
+          const int kr = k_lo + kt * BK2 + b_k[i];
+          const bool ok = b_ok[i] && kr < k_hi;
+          st.rb[i] = *reinterpret_cast<const float4*>(Bg + (ok ? (long long)kr * ldb + b_base[i] : 0));
+          st.bm |= (unsigned)ok << i;
+        } else {
+          const bool ok = b_ok[i] && kok;
+          st.rb[i] = *reinterpret_cast<const float4*>(Bg + (ok ? b_base[i] + k : 0));
+          st.bm |= (unsigned)ok << i;
+        }
       }
     };
     auto store_tile = [&](const Stage& st, int buf) {
@@ -165,13 +234,23 @@ gemm_nt_kernel(const GemmArgs args) {
         float4 v = st.ra[i];
         if (PRO) v = relu4(fma4(v, st.sc, st.sh));
         if (!((st.am >> i) & 1u)) v = f4(0.f);
-        *reinterpret_cast<float4*>(&As[buf][((tid + i * 256) >> 3) * S2 + kq]) = v;
+        const int f = tid + i * 256;
+        if (AMODE == 1) {
+          store_t4(&As[buf][(i % AQ16 * 16 + (tid & 15)) * 4 * S2 + (tid >> 4) + 16 * (i / AQ16)], v, tid);
+        } else {
+          *reinterpret_cast<float4*>(&As[buf][(f >> 3) * S2 + kq]) = v;
+        }
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
         float4 v = st.rb[i];
         if (!((st.bm >> i) & 1u)) v = f4(0.f);
-        *reinterpret_cast<float4*>(&Bs[buf][((tid + i * 256) >> 3) * S2 + kq]) = v;
+        const int f = tid + i * 256;
+        if (BMODE == 1) {
+          store_t4(&Bs[buf][(i % BQ16 * 16 + (tid & 15)) * 4 * S2 + (tid >> 4) + 16 * (i / BQ16)], v, tid);
+        } else {
+          *reinterpret_cast<float4*>(&Bs[buf][(f >> 3) * S2 + kq]) = v;
+        }
       }
     };
     auto compute = [&](int buf) {
@@ -196,11 +275,14 @@ gemm_nt_kernel(const GemmArgs args) {
             }
       }
     };
-    // one k-step: issue loads of tile kt+2 into `ld`, multiply tile kt, park tile kt+1 (`sv`)
+    // one k-step: issue loads of tile kt+2 into `ld`, multiply tile kt, park tile kt+1 (`sv`).
+    // The loads and stores are unconditional (tiles past the end load masked dummies and park
+    // zeros in the unused buffer): a branch around them makes the compiler's vmcnt merge at the
+    // join wait for the loads just issued, i.e. it silently drops the second prefetch stage.
     auto kstep = [&](Stage& ld, const Stage& sv, int kt) {
-      if (kt + 2 < nkt) load_tile(ld, kt + 2);
+      load_tile(ld, kt + 2);
       compute(kt & 1);
-      if (kt + 1 < nkt) store_tile(sv, (kt + 1) & 1);
+      store_tile(sv, (kt + 1) & 1);
       __syncthreads();
     };
 
@@ -213,7 +295,7 @@ gemm_nt_kernel(const GemmArgs args) {
     load_tile(s0, 0);
     store_tile(s0, 0);
     if (DEEP) {
-      if (nkt > 1) load_tile(s1, 1);
+      load_tile(s1, 1);
       __syncthreads();
       for (int kt = 0; kt < nkt; kt += 2) {
         kstep(s0, s1, kt);
@@ -222,9 +304,9 @@ gemm_nt_kernel(const GemmArgs args) {
     } else {
       __syncthreads();
       for (int kt = 0; kt < nkt; ++kt) {
-        if (kt + 1 < nkt) load_tile(s0, kt + 1);
+        load_tile(s0, kt + 1);
         compute(kt & 1);
-        if (kt + 1 < nkt) store_tile(s0, (kt + 1) & 1);
+        store_tile(s0, (kt + 1) & 1);
         __syncthreads();
       }
     }
@@ -412,34 +494,46 @@ gemm_nt_kernel(const GemmArgs args) {
 }
 
 template <int BM, int BN, bool SK>
-void launch_sk(const GemmArgs& a, int amode, bool pro, int blocks, hipStream_t s) {
-  if (amode == 0)
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 0, false, SK>), dim3(blocks), dim3(256), 0, s, a);
-  else if (pro)
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 2, true, SK>), dim3(blocks), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 2, false, SK>), dim3(blocks), dim3(256), 0, s, a);
+void launch_sk(const GemmArgs& a, int amode, int bmode, bool pro, int blocks, hipStream_t s) {
+  const dim3 g(blocks), b(256);
+  if (bmode == 1) {
+    if (amode == 1)
+      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 1, 1, false, SK>), g, b, 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 0, 1, false, SK>), g, b, 0, s, a);
+  } else if (amode == 1) {
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 1, 0, false, SK>), g, b, 0, s, a);
+  } else if (amode == 4) {
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 4, 0, false, SK>), g, b, 0, s, a);
+  } else if (amode == 0) {
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 0, 0, false, SK>), g, b, 0, s, a);
+  } else if (pro) {
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 2, 0, true, SK>), g, b, 0, s, a);
+  } else {
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 2, 0, false, SK>), g, b, 0, s, a);
+  }
 }
 
 template <int BM, int BN>
-int launch_bmbn(const GemmArgs& a, int amode, bool pro, int blocks, hipStream_t s) {
+int launch_bmbn(const GemmArgs& a, int amode, int bmode, bool pro, int blocks, hipStream_t s) {
   if (a.sk_workers > 0)
-    launch_sk<BM, BN, true>(a, amode, pro, blocks, s);
+    launch_sk<BM, BN, true>(a, amode, bmode, pro, blocks, s);
   else
-    launch_sk<BM, BN, false>(a, amode, pro, blocks, s);
+    launch_sk<BM, BN, false>(a, amode, bmode, pro, blocks, s);
   CAPMI_LAUNCH_CHECK();
   return 0;
 }
 
 }  // namespace
 
-int gemm_nt_launch(const GemmArgs& a, int amode, int bm, int bn, int blocks, hipStream_t s) {
+int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int blocks, hipStream_t s) {
   bool pro = false;
   for (int i = 0; i < a.nprob; ++i) pro = pro || a.p[i].in_scale != nullptr;
   for (int i = 0; i < a.nprob; ++i)
     if (pro && a.p[i].in_scale == nullptr) return CAPMI_EINVAL;  // grouped: all or none
-  if (bm == 128 && bn == 128) return launch_bmbn<128, 128>(a, amode, pro, blocks, s);
-  if (bm == 128 && bn == 64) return launch_bmbn<128, 64>(a, amode, pro, blocks, s);
-  if (bm == 64 && bn == 64) return launch_bmbn<64, 64>(a, amode, pro, blocks, s);
+  if (pro && amode != 2) return CAPMI_EINVAL;
+  if (bm == 128 && bn == 128) return launch_bmbn<128, 128>(a, amode, bmode, pro, blocks, s);
+  if (bm == 128 && bn == 64) return launch_bmbn<128, 64>(a, amode, bmode, pro, blocks, s);
+  if (bm == 64 && bn == 64) return launch_bmbn<64, 64>(a, amode, bmode, pro, blocks, s);
   return CAPMI_EINVAL;
 }

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 3
+#define CAPMI_ABI_VERSION 4
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -45,7 +45,8 @@ enum capmi_amode {
   CAPMI_A_KMAJOR = 0,   /* A[m][k]: off(m) + k, off(r) = (r % a_r1)*lda + (r / a_r1)*a_s2 */
   CAPMI_A_MMAJOR = 1,   /* A[k][m]: off(k) + m  (i.e. A^T of a row-major matrix)          */
   CAPMI_A_CONV_NHWC = 2,/* implicit im2col of an NHWC input, k = (kh, kw, ci), Cin % 16 == 0 */
-  CAPMI_A_CONV_NCHW = 3 /* implicit im2col of an NCHW input, k = (ci, kh, kw) (conv1)    */
+  CAPMI_A_CONV_NCHW = 3,/* implicit im2col of an NCHW input, k = (ci, kh, kw) (generic kernel) */
+  CAPMI_A_CONV_NHWC4 = 4/* implicit im2col of an NHWC input padded to Cin = 4 (conv1 on capmi_image_nhwc4 output), k = (kh, kw, c4) */
 };
 enum capmi_bmode {
   CAPMI_B_NMAJOR_W = 0, /* B[k][n] = W[n][k] (nn.Linear weight / packed conv weight), ldb = row stride of W */
@@ -76,8 +77,8 @@ int capmi_gemm(const capmi_gemm_problem* problems, int nprob, int amode, int bmo
                void* stream);
 /* rows of the statistics buffer capmi_gemm writes for M rows: ceil(M/64) (tile ignored) */
 int capmi_gemm_stat_tiles(int M, int tile);
-/* Stream-K form of capmi_gemm for ONE problem with bmode CAPMI_B_NMAJOR_W (what every conv
- * of the encoder is): when the data-parallel grid would end in a partial round of
+/* Stream-K form of capmi_gemm for ONE problem (every conv of the encoder, the decoder's hoisted
+ * GEMMs and weight gradients): when the data-parallel grid would end in a partial round of
  * workgroups (e.g. 784 64x64 tiles on 1024 resident slots), the (tile, k-tile) iteration
  * space is instead split evenly over one persistent workgroup per resident slot; the k-prefix
  * of a tile shared by two workgroups is parked in `workspace` and added, in a fixed order, by
@@ -87,7 +88,7 @@ int capmi_gemm_stat_tiles(int M, int tile);
  * before first use (the kernel leaves it reusable); one workspace per concurrently running
  * stream. */
 long long capmi_gemm_workspace_bytes(void);
-int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int tile, void* workspace,
+int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int tile, void* workspace,
                   long long ws_bytes, void* stream);
 
 /* sum of S partial slabs: out[r][c] = sum_s in[s*slab + r*ld_in + c] (+ bias[c]); rows x cols */
@@ -105,11 +106,19 @@ int capmi_colsum(const float* in, int rows, int cols, long long ld, float scale,
  * ---------------------------------------------------------------------- */
 /* [Cout][Cin][KH][KW] -> [Cout][KH][KW][Cin] */
 int capmi_conv_weight_pack(const float* w, int Cout, int Cin, int KH, int KW, float* out, void* stream);
+/* same, channels zero-padded to Cin_pad >= Cin: [Cout][KH][KW][Cin_pad] (conv1: Cin_pad = 4) */
+int capmi_conv_weight_pack_pad(const float* w, int Cout, int Cin, int KH, int KW, int Cin_pad, float* out,
+                               void* stream);
+/* images NCHW (C <= 4) -> NHWC with 4 channels, zero padded (input of the CAPMI_A_CONV_NHWC4 conv1;
+ * the reference's imgs tensor, models/attention.py:389 -> encoder(imgs)) */
+int capmi_image_nhwc4(const float* in, int N, int C, int H, int W, float* out, void* stream);
 /* BatchNorm2d(train) finalize from capmi_gemm stats: mean/var over `count` rows, then
  * scale = gamma*rsqrt(var+eps), shift = beta - mean*scale; running stats updated in place
  * (momentum, unbiased var) when running_mean != NULL. mean/var out (may be NULL).
- * work: CAPMI_BN_WORK_DOUBLES(C) doubles of scratch. */
-#define CAPMI_BN_WORK_DOUBLES(C) (128 * 2 * (long long)(C))
+ * work: CAPMI_BN_WORK_DOUBLES(C) doubles of scratch, ZEROED by the caller before first use (it
+ * holds per-channel-block arrival counters the kernel re-arms to zero; one work buffer per
+ * concurrently running stream). */
+#define CAPMI_BN_WORK_DOUBLES(C) (64 + 64 * (long long)(C)) /* C <= 8192 */
 int capmi_bn_finalize(const float* stats, int tiles, int C, long long count, const float* gamma,
                       const float* beta, float* running_mean, float* running_var, float momentum,
                       float eps, float* scale, float* shift, float* save_mean, float* save_var,

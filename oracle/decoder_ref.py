@@ -60,15 +60,16 @@ def decoder_forward(p, encoder_out, encoded_captions, caption_lengths, dropout_p
     embeddings = F.embedding(encoded_captions, emb_w)                      # :247
     h, c = init_hidden_state(p, enc)                                       # :250
     V = p["fc.weight"].shape[0]
-    predictions = torch.zeros(B, T, V, dtype=torch.float32)                # :253-254
-    alphas = torch.zeros(B, T, P, dtype=torch.float32)                     # :257-258
+    wdt = p["decode_step.weight_ih"].dtype  # fp32 as in the reference; fp64 only for diagnostics
+    predictions = torch.zeros(B, T, V, dtype=wdt)                          # :253-254
+    alphas = torch.zeros(B, T, P, dtype=wdt)                               # :257-258
     for t in range(T):                                                     # :260
         bt = sum(l > t for l in decode_lengths)                            # :261
         awe, alpha = soft_attention(p, enc[:bt], h[:bt])                   # :267-268
         gate = torch.sigmoid(_lin(h[:bt], p, "f_beta"))                    # :270
         awe = gate * awe                                                   # :271
         x = torch.cat([embeddings[:bt, t, :].double(), awe.double()], 1)   # :274-275
-        h, c = lstm_cell(x.float(), h[:bt].float(), c[:bt].float(), p)     # :277-278
+        h, c = lstm_cell(x.to(wdt), h[:bt].to(wdt), c[:bt].to(wdt), p)     # :277-278 (.float())
         hd = h
         if dropout_masks is not None:
             hd = h * dropout_masks[t, :bt]

@@ -63,14 +63,34 @@ def test_soft_attention_matches_golden(golden, tag):
     assert_close(awe, t(fx["awe"]), 1e-4, 1e-5, "awe")
 
 
+KINK_ROWS = ("attention.enc_att.weight", "attention.enc_att.bias", "attention.dec_att.weight",
+             "attention.dec_att.bias")
+
+
 def _grad_check(got, want, name):
+    """Returns the set of rows excused by the ReLU-kink rule (empty for other parameters)."""
     if name.endswith("attention.full_att.bias"):
         # d loss / d b_full = sum_p dalpha-softmax-backward = 0 exactly (softmax is shift
         # invariant); the reference and capmi both return fp32 rounding noise here.
         assert float(got.abs().max()) < 1e-6 and float(want.abs().max()) < 1e-6, name
-        return
+        return set()
     scale = float(want.abs().max()) if want.numel() else 1.0
+    if name.split(" ")[-1] in KINK_ROWS:
+        # The attention uses ReLU (models/attention.py:56). Where a pre-activation
+        # att_enc + att_dec lands within fp32 rounding of 0, the GPU and the CPU reference can
+        # take opposite sides of the kink: one such (b, p, a, t) changes d(att_enc)[b, p, a] and
+        # d(att_dec)_t[b, a] by a full term, i.e. row a of dW_enc_att and of dW_dec_att. At most
+        # 2 such rows are excused (a few flips are expected among B*P*A*T ~ 1e7
+        # pre-activations), every other row must match, and the caller checks that the excused
+        # rows of the two weights coincide (same a: the kink, not a kernel error).
+        g2, w2 = got.reshape(got.shape[0], -1).double().cpu(), want.reshape(want.shape[0], -1).double()
+        bad_rows = ((g2 - w2).abs() > 1e-3 * scale + 2e-3 * w2.abs() + 1e-9).any(1)
+        assert int(bad_rows.sum()) <= 2, f"{name}: {int(bad_rows.sum())} rows out of tolerance"
+        keep = ~bad_rows
+        assert_close(g2[keep], w2[keep], 2e-3, 1e-3 * scale + 1e-9, name)
+        return set(bad_rows.nonzero().view(-1).tolist())
     assert_close(got, want, 2e-3, 1e-3 * scale + 1e-9, name)
+    return set()
 
 
 @pytest.mark.parametrize("cfg", [
@@ -100,8 +120,10 @@ def test_fused_train_step_matches_oracle(cfg):
     assert_close(loss.view(()), rloss, 1e-5, 1e-6, "loss")
     assert_close(preds, rpreds, LOGIT_RTOL, LOGIT_ATOL, "predictions")
     assert_close(alphas, ralphas, 0.0, ALPHA_ATOL, "alphas")
-    for n in trainable:
-        _grad_check(grads[n].view_as(rraw[n]), rraw[n], "grad " + n)
+    excused = {n: _grad_check(grads[n].view_as(rraw[n]), rraw[n], "grad " + n) for n in trainable}
+    kinks = set().union(*(excused.get(n, set()) for n in KINK_ROWS))
+    assert len(kinks) <= 2 and excused.get("attention.dec_att.weight", set()) <= \
+        excused.get("attention.enc_att.weight", set()) | excused.get("attention.enc_att.bias", set()), excused
     # clamp + Adam: the fused kernel vs the oracle's torch-Adam restatement fed the SAME
     # gradients (Adam's first step is ~lr*sign(g), so it is only well-conditioned this way)
     ours = {n: grads[n].detach().cpu().clone().view_as(rraw[n]) for n in trainable}

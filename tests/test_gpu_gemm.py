@@ -41,11 +41,13 @@ def test_linear_fwd(tile, M, N, Kd):
     check(C, ref, X.abs() @ W.abs().T + b.abs() + b2.abs(), "linear")
 
 
-@pytest.mark.parametrize("tile", [0, 1])
-def test_transposed_modes_and_remap(tile):
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("N,Kx", [(36, 44), (37, 45), (520, 260)])
+def test_transposed_modes_and_remap(tile, N, Kx):
+    """k-row operands (transposed staging in the v2 kernel; N % 4 != 0 takes the generic kernel)."""
     K = _K()
     # dW = dY^T X with dY stored batch-major (B,T,N) and read time-major through the 2-level remap
-    B, T, N, Kx = 5, 7, 36, 44
+    B, T = 5, 7
     dY = rnd(B, T, N, seed=5)
     Xt = rnd(T * B, Kx, seed=6)  # time-major rows r = t*B + b
     C = torch.empty(N, Kx, device=DEV)
@@ -147,6 +149,34 @@ def test_conv1_nchw_gather():
     check(out.view(N, Ho, Ho, 64).permute(0, 3, 1, 2), ref, ref_abs, "conv1 NCHW gather")
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3])
+def test_conv1_nhwc4(tile):
+    """conv1 as the encoder runs it: images -> NHWC4, weights packed with Cin padded to 4."""
+    K = _K()
+    N, H = 3, 46
+    x = rnd(N, 3, H, H, seed=21)
+    w = rnd(64, 3, 7, 7, seed=22) * 0.1
+    ref = F.conv2d(x, w, stride=2, padding=3)
+    ref_abs = F.conv2d(x.abs(), w.abs(), stride=2, padding=3)
+    Ho = ref.shape[2]
+    xd = x.float().to(DEV).contiguous()
+    img4 = torch.full((N * H * H * 4,), float("nan"), device=DEV)
+    K.image_nhwc4(xd, img4)
+    assert torch.equal(img4.view(N, H, H, 4)[..., :3].cpu(), xd.permute(0, 2, 3, 1).cpu())
+    assert float(img4.view(N, H, H, 4)[..., 3].abs().sum()) == 0.0
+    wp = torch.full((64 * 49 * 4,), float("nan"), device=DEV)
+    K.conv_weight_pack_pad(w.float().to(DEV).contiguous(), 4, wp)
+    M = N * Ho * Ho
+    out = torch.empty(M, 64, device=DEV)
+    stats = torch.empty(K.stat_tiles(M), 64, 2, device=DEV)
+    geo = dict(N=N, H=H, W=H, Cin=4, KH=7, KW=7, stride=2, pad=3, Ho=Ho, Wo=Ho)
+    ws = K.gemm_workspace(DEV)
+    K.gemm_sk(K.problem(M, 64, 196, img4, 0, wp, 196, out, 64, conv=geo, stats=stats), 4, ws, tile)
+    check(out.view(N, Ho, Ho, 64).permute(0, 3, 1, 2), ref, ref_abs, "conv1 NHWC4")
+    s = stats.double().cpu().sum(0)
+    torch.testing.assert_close(s[:, 0], out.double().cpu().sum(0), rtol=1e-5, atol=1e-3)
+
+
 # ---------------------------------------------------------------------------------------
 # stream-K (capmi_gemm_sk): persistent workgroups, k-prefixes parked in the workspace
 # ---------------------------------------------------------------------------------------
@@ -203,3 +233,49 @@ def test_conv_sk_prologue(k, stride, cin, cout, hw):
     s = stats.double().cpu().sum(0)
     Cd = out.double().cpu()
     torch.testing.assert_close(s[:, 0], Cd.sum(0), rtol=1e-5, atol=1e-3)
+
+
+def test_bn_finalize_shared_work():
+    """BN finalize (one launch, last-arriving group finalizes) vs fp64, several widths sharing one
+    zeroed work buffer, counters re-armed to zero after every call."""
+    K = _K()
+    work = torch.zeros(K.bn_work_doubles(2048), device=DEV, dtype=torch.float64)
+    for it, (C, tiles) in enumerate([(64, 3136), (2048, 49), (256, 196), (64, 3136), (1024, 7)]):
+        g = torch.Generator().manual_seed(40 + it)
+        x = torch.randn(tiles * 64, C, generator=g, dtype=torch.float64) * 3 + 1
+        rows = x.shape[0]
+        stats = torch.stack([x.view(tiles, 64, C).sum(1), (x * x).view(tiles, 64, C).sum(1)], -1)
+        gamma, beta = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g)
+        rm, rv = torch.randn(C, generator=g), torch.rand(C, generator=g) + 0.5
+        sd = [t.float().to(DEV) for t in (stats, gamma, beta, rm, rv)]
+        scale, shift = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        K.bn_finalize(sd[0], tiles, C, rows, sd[1], sd[2], sd[3], sd[4], 0.1, 1e-5, scale, shift, work)
+        torch.cuda.synchronize()
+        mean, var = x.mean(0), x.var(0, unbiased=False)
+        sc = gamma.double() / torch.sqrt(var + 1e-5)
+        torch.testing.assert_close(scale.double().cpu(), sc, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(shift.double().cpu(), beta.double() - mean * sc, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(sd[3].double().cpu(), 0.9 * rm.double() + 0.1 * mean, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(sd[4].double().cpu(), 0.9 * rv.double() + 0.1 * x.var(0), rtol=1e-5, atol=1e-5)
+        assert int(work[:64].view(torch.int32).abs().sum()) == 0, "arrival counters not re-armed"
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3])
+@pytest.mark.parametrize("M,N,Kd", [(512, 2048, 784), (32, 2048, 588), (2048, 2560, 1536), (512, 64, 12544)])
+def test_gemm_sk_transposed(tile, M, N, Kd):
+    """dW = dY^T X (both operands stored as k rows) through stream-K: the decoder's weight grads."""
+    K = _K()
+    dY, X = rnd(Kd, M, seed=51), rnd(Kd, N, seed=52)
+    dYd, Xd = dY.float().to(DEV), X.float().to(DEV)
+    C = torch.empty(M, N, device=DEV)
+    ws = K.gemm_workspace(DEV)
+    K.gemm_sk(K.problem(M, N, Kd, dYd, M, Xd, N, C, N), 1, ws, tile, bmode=1)
+    torch.cuda.synchronize()
+    check(C, dY.T @ X, dY.abs().T @ X.abs(), "stream-K MMAJOR x KROWS")
+    # and dX = dY W with W stored [k][n] (KMAJOR x KROWS)
+    out = torch.empty(Kd, N, device=DEV)
+    W = rnd(M, N, seed=53)
+    Wd = W.float().to(DEV)
+    K.gemm_sk(K.problem(Kd, N, M, dYd, M, Wd, N, out, N), 0, ws, tile, bmode=1)
+    torch.cuda.synchronize()
+    check(out, dY @ W, dY.abs() @ W.abs(), "stream-K KMAJOR x KROWS")

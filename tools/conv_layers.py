@@ -34,10 +34,16 @@ def main():
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = list(c.execute("select name, duration from kernels order by start"))
-    gem = [r for r in rows if "gemm" in r[0]]
     sh = shapes(a.batch)
-    first = [i for i, r in enumerate(gem) if "3, 0" in r[0] and "gemm_kernel<" in r[0]]
-    convs = gem[first[-1]:first[-1] + len(sh)]
+    # conv1 follows the image re-layout kernel (or is the older NCHW-gather generic kernel)
+    starts = [i for i, r in enumerate(rows) if "image_nhwc4" in r[0]]
+    if starts:
+        gem = [r for r in rows[starts[-1]:] if "gemm" in r[0]]
+        convs = gem[:len(sh)]
+    else:
+        gem = [r for r in rows if "gemm" in r[0]]
+        first = [i for i, r in enumerate(gem) if "3, 0" in r[0] and "gemm_kernel<" in r[0]]
+        convs = gem[first[-1]:first[-1] + len(sh)]
     agg, tf, tt = {}, 0, 0
     for (tag, M, N, K), (name, d) in zip(sh, convs):
         f = 2 * M * N * K
@@ -45,7 +51,7 @@ def main():
         e[0] += f
         e[1] += d
         e[2] += 1
-        e[6].add(name.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", ""))
+        e[6].add(name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0])
         tf += f
         tt += d
     print(f"| layer / conv | n | M | N | K | ms | TFLOP/s | kernel |\n|---|---:|---:|---:|---:|---:|---:|---|")

@@ -15,7 +15,9 @@ def short(n):
 def main():
     c = sqlite3.connect(sys.argv[1])
     rows = list(c.execute("select name, duration, start, end from kernels order by start"))
-    starts = [i for i, r in enumerate(rows) if "gemm_kernel<128, 128, 64, 64, 3" in r[0]] + [len(rows)]
+    # a step starts at conv1 (the image re-layout kernel that feeds it, or the older NCHW gather)
+    starts = [i for i, r in enumerate(rows)
+              if "image_nhwc4" in r[0] or "gemm_kernel<128, 128, 64, 64, 3" in r[0]] + [len(rows)]
     # the last complete training step: a segment between two conv1 launches that contains Adam
     segs = [(a, b) for a, b in zip(starts, starts[1:]) if any("adam_clamp" in r[0] for r in rows[a:b])]
     i0, i1 = segs[-1]
