@@ -9,9 +9,10 @@ forward + backward, CE + doubly-stochastic loss, (DP: gradient all-reduce over R
 clamp + Adam. fp32 throughout (the reference's precision). Weights: torch.manual_seed(0)
 random init of the reference architecture (no checkpoints offline).
 
-Rank 0 prints ONE JSON line. ``roofline`` is for the dominant kernel (the conv implicit-
-GEMM family, 86% of the step's FLOPs): achieved = conv FLOPs / summed conv kernel time,
-timed with HIP events on the launch stream around every conv launch of the timed steps.
+Rank 0 prints ONE JSON line. ``roofline`` is for the dominant kernel: the conv implicit-GEMM
+instantiation with the most time per step (the conv family is 86% of the step's FLOPs; the
+family aggregate is reported beside it). achieved = that kernel's algorithmic conv FLOPs /
+its summed launch time, HIP events on the launch stream around every conv launch.
 ``cpu_baseline`` times the CPU oracle (op-for-op restatement of the reference step) on
 the host cores, rank 0 at N = 1 only, on a small bounded sample.
 """
@@ -49,14 +50,13 @@ def parse():
 
 
 class ConvTimer:
-    """HIP-event bracket around every conv GEMM launch (on the launch stream)."""
+    """HIP-event bracket around every conv GEMM launch (on the launch stream), per kernel."""
 
     def __init__(self):
-        self.events = []
-        self.flops = 0.0
+        self.events = []  # (kernel key, flops, start event, end event)
         self.enabled = False
 
-    def __call__(self, tag, flops, launch):
+    def __call__(self, tag, flops, launch, key):
         if not self.enabled:
             launch()
             return
@@ -65,12 +65,30 @@ class ConvTimer:
         s.record()
         launch()
         e.record()
-        self.events.append((s, e))
-        self.flops += flops
+        self.events.append((key, flops, s, e))
 
     def result(self):
-        ms = sum(s.elapsed_time(e) for s, e in self.events)
-        return ms, self.flops, len(self.events)
+        """{kernel key: [launches, flops, ms]} and the family total."""
+        per = {}
+        for key, f, s, e in self.events:
+            ent = per.setdefault(key, [0, 0.0, 0.0])
+            ent[0] += 1
+            ent[1] += f
+            ent[2] += s.elapsed_time(e)
+        return per
+
+
+def _traffic(kernel):
+    """HBM bytes per launch of ``kernel`` from the committed PMC summary (2*FETCH_SIZE +
+    WRITE_SIZE, gfx950 correction; tools/pmc_traffic.py), or None."""
+    path = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+    try:
+        with open(path) as f:
+            tab = json.load(f)
+    except (OSError, ValueError):
+        return None
+    ent = tab.get("kernels", {}).get(kernel)
+    return None if ent is None else ent.get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(args, seconds):
@@ -166,15 +184,24 @@ def main():
     value = N * B * args.steps / dt
     roof = None
     if not args.no_roofline and timer.events:
-        ms, flops, launches = timer.result()
+        per = timer.result()
+        # the dominant kernel: the conv GEMM instantiation with the most time
+        key = max(per, key=lambda k: per[k][2])
+        n, flops, ms = per[key]
         ach = flops / (ms * 1e-3) / 1e12
+        fam_flops = sum(v[1] for v in per.values())
+        fam_ms = sum(v[2] for v in per.values())
         per_img = conv_flops_per_image(_view(encoder))
         roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                "frac": round(ach / FP32_MFMA_PEAK_TF, 4), "traffic": None,
-                "kernel": "gemm_nt_kernel (ResNet-101 implicit-GEMM convs, stream-K) + conv1 gemm_kernel",
-                "flops_per_launch": round(flops / launches), "avg_launch_us": round(ms * 1e3 / launches, 2),
-                "conv_gflop_per_image": round(per_img / 1e9, 3),
-                "conv_ms_per_step": round(ms / args.steps, 3),
+                "frac": round(ach / FP32_MFMA_PEAK_TF, 4), "traffic": _traffic(key),
+                "kernel": key,
+                "launches_per_step": n // args.steps,
+                "flops_per_launch": round(flops / n), "avg_launch_us": round(ms * 1e3 / n, 2),
+                "traffic_unit": "HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, profiles/r01_pmc_traffic.json)",
+                "conv_family": {"achieved_tflops": round(fam_flops / (fam_ms * 1e-3) / 1e12, 3),
+                                "frac": round(fam_flops / (fam_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF, 4),
+                                "conv_ms_per_step": round(fam_ms / args.steps, 3),
+                                "conv_gflop_per_image": round(per_img / 1e9, 3)},
                 "timing": "HIP events around each conv launch, " + (
                     "inside the timed steps" if args.eager else
                     f"{args.steps} eager encoder forwards after the timed graph replays")}

@@ -23,7 +23,7 @@ CAPMI_B_NMAJOR_W, CAPMI_B_KROWS = 0, 1
 CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO = 0, 1, 2, 3
 CAPMI_MAX_GROUP = 4
 CAPMI_COLSUM_GROUPS = 64
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class GemmProblem(ctypes.Structure):
@@ -48,6 +48,7 @@ _SIGS = {
     "capmi_gemm_stat_tiles": [c_int, c_int],
     "capmi_gemm_workspace_bytes": [],
     "capmi_gemm_sk": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_vp, c_ll, c_vp],
+    "capmi_gemm_sk_plan": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp],
     "capmi_splitk_reduce": [c_vp, c_int, c_ll, c_int, c_int, c_ll, c_vp, c_vp, c_ll, c_vp],
     "capmi_colsum": [c_vp, c_int, c_int, c_ll, c_float, c_vp, c_vp, c_int, c_vp],
     "capmi_conv_weight_pack": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],

@@ -80,6 +80,13 @@ def gemm_sk(prob, amode, workspace, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W
          stream())
 
 
+def gemm_sk_plan(prob, amode, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W):
+    """(bm, bn, stream_k, generic) of the launch gemm_sk would make for ``prob``."""
+    v = [ctypes.c_int(0) for _ in range(4)]
+    call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, bmode, tile, *[ctypes.byref(x) for x in v])
+    return tuple(x.value for x in v)
+
+
 def stat_tiles(M, tile=CAPMI_TILE_128):
     return lib.capmi_gemm_stat_tiles(int(M), int(tile))
 

@@ -121,7 +121,7 @@ class EncoderRunner:
         self.packed = _Packed()
         self._ws = None
         self._ws_key = None
-        self.conv_hook = None  # optional callable(tag, fn) wrapping each conv launch (bench timing)
+        self.conv_hook = None  # optional callable(tag, flops, launch_fn, kernel_key) (bench timing)
 
     def _workspace(self, N, H, W, device):
         key = (N, H, W, str(device))
@@ -191,7 +191,11 @@ class EncoderRunner:
             mode = CAPMI_A_CONV_NHWC
         launch = lambda: K.gemm_sk(prob, mode, self._ws["sk"], K.TILE_AUTO)  # noqa: E731
         if self.conv_hook is not None:
-            self.conv_hook(tag, 2.0 * rows * co * Kd, launch)
+            bm, bn, sk, generic = K.gemm_sk_plan(prob, mode, K.TILE_AUTO)
+            b = lambda v: "true" if v else "false"  # noqa: E731
+            key = "gemm_kernel (generic)" if generic else \
+                f"gemm_nt_kernel<{bm}, {bn}, {mode}, 0, {b(in_ss is not None and not nchw)}, {b(sk)}>"
+            self.conv_hook(tag, 2.0 * rows * co * Kd, launch, key)
         else:
             launch()
         del stats

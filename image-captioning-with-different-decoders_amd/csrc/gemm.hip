@@ -514,8 +514,9 @@ extern "C" long long capmi_gemm_workspace_bytes(void) {
   return sk_flag_bytes(cus) + (long long)cus * 128 * 1024;
 }
 
-extern "C" int capmi_gemm_sk(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
-                             void* workspace, long long ws_bytes, void* stream) {
+namespace {
+// the launch capmi_gemm_sk makes for a problem (shared by the launcher and the plan query)
+int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, GemmPlan& g, bool& sk) {
   CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
   const int nkt = (prob->K + 31) / 32;
   const bool automatic = tile == CAPMI_TILE_AUTO;
@@ -523,25 +524,48 @@ extern "C" int capmi_gemm_sk(const capmi_gemm_problem* prob, int amode, int bmod
   // output tile, stream-K over 128x64 tiles is the fastest form; below that the per-segment
   // pipeline fill outweighs the balance gain and 64x64 data-parallel wins
   if (automatic) tile = nkt >= 16 ? CAPMI_TILE_128x64 : CAPMI_TILE_64;
-  GemmPlan g;
   const int rc = gemm_plan(prob, 1, amode, bmode, tile, g);
   if (rc) return rc;
-  hipStream_t s = as_stream(stream);
-  const int cus = cu_count();
-  const long long slots = (long long)cus * gemm_nt_wg_per_cu(g.bm, g.bn);
+  const long long slots = (long long)cu_count() * gemm_nt_wg_per_cu(g.bm, g.bn);
   const long long tiles = g.total;
-  bool sk = g.nt_ok && prob->ksplit == 1 && tiles > 0 && (!automatic || nkt >= 16);
+  sk = g.nt_ok && prob->ksplit == 1 && tiles > 0 && (!automatic || nkt >= 16);
   if (sk) {
-    CAPMI_REQUIRE(workspace != nullptr && aligned16(workspace), CAPMI_EINVAL);
-    CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
     // stream-K only when the data-parallel grid would leave a costly partial last round
     const long long rounds = (tiles + slots - 1) / slots;
     sk = (double)tiles / (double)(rounds * slots) < 0.9;
   }
+  return 0;
+}
+}  // namespace
+
+extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, int* bm,
+                                  int* bn, int* stream_k, int* generic) {
+  GemmPlan g;
+  bool sk = false;
+  const int rc = sk_decide(prob, amode, bmode, tile, g, sk);
+  if (rc) return rc;
+  if (bm) *bm = g.bm;
+  if (bn) *bn = g.bn;
+  if (stream_k) *stream_k = sk ? 1 : 0;
+  if (generic) *generic = g.nt_ok ? 0 : 1;
+  return 0;
+}
+
+extern "C" int capmi_gemm_sk(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
+                             void* workspace, long long ws_bytes, void* stream) {
+  GemmPlan g;
+  bool sk = false;
+  const int rc = sk_decide(prob, amode, bmode, tile, g, sk);
+  if (rc) return rc;
+  hipStream_t s = as_stream(stream);
   if (!sk) return gemm_launch_dp(g, amode, bmode, s);
+  CAPMI_REQUIRE(workspace != nullptr && aligned16(workspace), CAPMI_EINVAL);
+  CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
+  const int cus = cu_count();
+  const long long slots = (long long)cus * gemm_nt_wg_per_cu(g.bm, g.bn);
   GemmArgs& a = g.a;
   a.sk_nkt = (prob->K + 31) / 32;
-  a.sk_units = tiles * a.sk_nkt;
+  a.sk_units = g.total * a.sk_nkt;
   a.sk_workers = (int)std::min<long long>(slots, a.sk_units);
   a.sk_flags = static_cast<int*>(workspace);
   a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));

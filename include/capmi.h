@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 4
+#define CAPMI_ABI_VERSION 5
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -90,6 +90,10 @@ int capmi_gemm_stat_tiles(int M, int tile);
 long long capmi_gemm_workspace_bytes(void);
 int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int tile, void* workspace,
                   long long ws_bytes, void* stream);
+/* the launch capmi_gemm_sk would make (no GPU work): tile bm x bn, stream_k 0/1, generic = 1
+ * when the problem falls back to the generic kernel. Used by the benchmark to attribute time. */
+int capmi_gemm_sk_plan(const capmi_gemm_problem* problem, int amode, int bmode, int tile, int* bm, int* bn,
+                       int* stream_k, int* generic);
 
 /* sum of S partial slabs: out[r][c] = sum_s in[s*slab + r*ld_in + c] (+ bias[c]); rows x cols */
 int capmi_splitk_reduce(const float* in, int S, long long slab, int rows, int cols, long long ld_in,
