@@ -163,6 +163,7 @@ __global__ void __launch_bounds__(256) att_softmax_ctx_fwd_kernel(
   float4 acc = f4(0.f);
   if (c < E) {
     const float* base = enc + (long long)b * P * E + c;
+#pragma unroll 8
     for (int p = pg; p < P; p += 4)
       acc = fma4(f4(alpha[p]), *reinterpret_cast<const float4*>(base + (long long)p * E), acc);
   }
@@ -518,6 +519,7 @@ __global__ void __launch_bounds__(256) att_ctx_bwd_kernel(
   for (int p = p0 + wid; p < min(P, p0 + PCH); p += 4) {
     const float* row = enc + ((long long)b * P + p) * E;
     float acc = 0.f;
+#pragma unroll 8
     for (int c = lane * 4; c < E; c += 256)
       acc += dot4(*reinterpret_cast<const float4*>(row + c), *reinterpret_cast<const float4*>(dawe + c));
     acc = wave_sum(acc);
@@ -549,7 +551,7 @@ __global__ void __launch_bounds__(256) att_score_bwd_kernel(
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* des = smem;  // [P]
   __shared__ float red[16];
-  __shared__ float part[4][64];
+  __shared__ float4 part4[256];
   const int b = blockIdx.y, tid = threadIdx.x;
   const bool active = b < bt;
   float s = 0.f;
@@ -568,22 +570,32 @@ __global__ void __launch_bounds__(256) att_score_bwd_kernel(
     if (blockIdx.x == 0) de[(long long)b * P + p] = v;
   }
   __syncthreads();
-  const int cl = tid & 63, pg = tid >> 6;
-  const int a = blockIdx.x * 64 + cl;
-  float acc = 0.f;
+  // d(att_dec)[b][a] = wf[a] * sum_p des[p] * [att_enc[b][p][a] + att_dec[b][a] > 0]:
+  // 16 lanes x float4 cover the block's 64 columns, 16 p-groups stride over P
+  const int c4 = tid & 15, pg = tid >> 4;
+  const int a = blockIdx.x * 64 + c4 * 4;
+  float4 acc = f4(0.f);
   if (a < A) {
-    const float ad = att_dec[(long long)b * A + a];
+    const float4 ad = *reinterpret_cast<const float4*>(att_dec + (long long)b * A + a);
     const float* base = att_enc + (long long)b * P * A + a;
-    for (int p = pg; p < P; p += 4) {
-      const float x = base[(long long)p * A] + ad;
-      acc += x > 0.f ? des[p] : 0.f;
+#pragma unroll 4
+    for (int p = pg; p < P; p += 16) {
+      const float4 x = *reinterpret_cast<const float4*>(base + (long long)p * A) + ad;
+      const float d = des[p];
+      acc.x += x.x > 0.f ? d : 0.f;
+      acc.y += x.y > 0.f ? d : 0.f;
+      acc.z += x.z > 0.f ? d : 0.f;
+      acc.w += x.w > 0.f ? d : 0.f;
     }
   }
-  part[pg][cl] = acc;
+  part4[pg * 16 + c4] = acc;
   __syncthreads();
-  if (pg == 0 && a < A) {
-    const float tot = part[0][cl] + part[1][cl] + part[2][cl] + part[3][cl];
-    dad[(long long)b * A + a] = wf[a] * tot;
+  if (tid < 16 && blockIdx.x * 64 + tid * 4 < A) {
+    float4 tot = part4[tid];
+    for (int g = 1; g < 16; ++g) tot = tot + part4[g * 16 + tid];
+    const int a0 = blockIdx.x * 64 + tid * 4;
+    const float4 w = *reinterpret_cast<const float4*>(wf + a0);
+    *reinterpret_cast<float4*>(dad + (long long)b * A + a0) = w * tot;
   }
 }
 
@@ -593,7 +605,8 @@ extern "C" int capmi_att_score_bwd(const float* dalpha, const float* dreg, long 
                                    int bt, float* de, float* dad, void* stream) {
   CAPMI_REQUIRE(dalpha && alpha && att_enc && att_dec && wf && de && dad && B > 0 && P > 0 && A > 0,
                 CAPMI_EINVAL);
-  CAPMI_REQUIRE(P <= 16384, CAPMI_ERANGE);
+  CAPMI_REQUIRE(P <= 16384 && A % 4 == 0, CAPMI_ERANGE);
+  CAPMI_REQUIRE(aligned16(att_enc) && aligned16(att_dec) && aligned16(wf) && aligned16(dad), CAPMI_EALIGN);
   hipLaunchKernelGGL(att_score_bwd_kernel, dim3(cdiv(A, 64), B), dim3(256), P * sizeof(float),
                      as_stream(stream), dalpha, dreg, dreg_ld_b, alpha, alpha_ld_b, att_enc, att_dec,
                      wf, B, P, A, bt, de, dad);

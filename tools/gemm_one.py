@@ -1,0 +1,61 @@
+"""Repeat one conv GEMM launch (for PMC / clock measurements of a single kernel).
+
+python tools/gemm_one.py --shape l3c2 --reps 50 [--tile 3]"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "image-captioning-with-different-decoders_amd"))
+import torch  # noqa: E402
+
+from capmi import kernels as K  # noqa: E402
+from capmi._lib import CAPMI_A_CONV_NHWC, CAPMI_A_KMAJOR  # noqa: E402
+
+SHAPES = {  # name: (Cin, H, W, Cout, k, prologue)
+    "l3c2": (256, 14, 14, 256, 3, True), "l3c3": (256, 14, 14, 1024, 1, True),
+    "l3c1": (1024, 14, 14, 256, 1, False), "l1c2": (64, 56, 56, 64, 3, True),
+    "l1c3": (64, 56, 56, 256, 1, True)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="l3c2")
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--tile", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64)
+    a = ap.parse_args()
+    dev = "cuda"
+    ci, H, W, co, k, pro = SHAPES[a.shape]
+    N = a.batch
+    M, Kd = N * H * W, ci * k * k
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.rand(N, H, W, ci, device=dev, generator=g) - 0.5
+    w = torch.rand(co, Kd, device=dev, generator=g) - 0.5
+    y = torch.empty(M, co, device=dev)
+    stats = torch.empty(K.stat_tiles(M, 1) * co * 2 + 64, device=dev)
+    sc = torch.rand(ci, device=dev, generator=g) + 0.5
+    sh = torch.rand(ci, device=dev, generator=g) - 0.5
+    geo = dict(N=N, H=H, W=W, Cin=ci, KH=k, KW=k, stride=1, pad=k // 2, Ho=H, Wo=W)
+    if k == 1 and not pro:
+        prob, mode = K.problem(M, co, Kd, x, ci, w, Kd, y, co, stats=stats), CAPMI_A_KMAJOR
+    else:
+        prob = K.problem(M, co, Kd, x, 0, w, Kd, y, co, conv=geo, stats=stats,
+                         in_scale=sc if pro else None, in_shift=sh if pro else None)
+        mode = CAPMI_A_CONV_NHWC
+    ws = K.gemm_workspace(dev)
+    print("plan (bm, bn, stream_k, generic):", K.gemm_sk_plan(prob, mode, a.tile))
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    K.gemm_sk(prob, mode, ws, a.tile)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(a.reps):
+        K.gemm_sk(prob, mode, ws, a.tile)
+    e.record()
+    torch.cuda.synchronize()
+    us = s.elapsed_time(e) * 1e3 / a.reps
+    print(f"{a.shape}: M={M} N={co} K={Kd}: {us:.1f} us/launch, {2.0 * M * co * Kd / us / 1e6:.1f} TFLOP/s")
+
+
+if __name__ == "__main__":
+    main()
