@@ -9,6 +9,12 @@ forward + backward, CE + doubly-stochastic loss, (DP: gradient all-reduce over R
 clamp + Adam. fp32 throughout (the reference's precision). Weights: torch.manual_seed(0)
 random init of the reference architecture (no checkpoints offline).
 
+Default launch: pipelined over two HIP streams -- call k runs the frozen encoder of batch k
+beside the decoder step of batch k-1 (bit-identical to the sequential order; the K timed
+calls run exactly K encoder passes and K decoder/optimizer passes: the pipeline is filled in
+warm-up and drained after the clock stops). ``--sequential`` runs the whole step as one HIP
+graph instead.
+
 Rank 0 prints ONE JSON line. ``roofline`` is for the dominant kernel: the conv implicit-GEMM
 instantiation with the most time per step (the conv family is 86% of the step's FLOPs; the
 family aggregate is reported beside it). achieved = that kernel's algorithmic conv FLOPs /
@@ -43,7 +49,10 @@ def parse():
     ap.add_argument("--caption-len", type=int, default=25)
     ap.add_argument("--vocab", type=int, default=8100)
     ap.add_argument("--no-roofline", action="store_true", help="skip per-conv event timing")
-    ap.add_argument("--eager", action="store_true", help="launch every kernel from Python (no HIP graph)")
+    ap.add_argument("--sequential", action="store_true",
+                    help="no encoder/decoder pipelining: the whole step in one HIP graph (or --eager)")
+    ap.add_argument("--eager", action="store_true",
+                    help="with --sequential: launch every kernel from Python (no HIP graph)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
@@ -146,7 +155,9 @@ def main():
     cdist.broadcast_module(decoder, ctx)
     opt = Adam(filter(lambda q: q.requires_grad, decoder.parameters()), lr=1e-4)
     opt.set_clip(5.0)
-    step = AttentionTrainStep(encoder, decoder, opt, ctx, alpha_c=1.0, graph=not args.eager, seed=77 + ctx.rank)
+    pipe = not args.sequential
+    step = AttentionTrainStep(encoder, decoder, opt, ctx, alpha_c=1.0, graph=not (args.eager or pipe),
+                              seed=77 + ctx.rank, pipeline=pipe)
     timer = ConvTimer()
     encoder._runner.conv_hook = None if args.no_roofline else timer
     B = args.batch
@@ -154,23 +165,28 @@ def main():
 
     for _ in range(args.warmup):
         step(imgs, caps, lens)
-    step.flush()
+    if not pipe:  # pipelined: keep one encoder pass in flight (its decoder runs in timed step 1)
+        step.flush()
     torch.cuda.synchronize()
     cdist.barrier(ctx)
     torch.cuda.synchronize()
-    timer.enabled = args.eager
+    timer.enabled = (args.eager or pipe) and not args.no_roofline
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step(imgs, caps, lens)
-    step.flush()
+    if not pipe:
+        step.flush()
     torch.cuda.synchronize()
     cdist.barrier(ctx)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     timer.enabled = False
     dt = cdist.max_over_ranks(dt, ctx)
+    if pipe:  # K encoder and K decoder passes were timed; drain the in-flight encoder pass
+        step.flush()
+        torch.cuda.synchronize()
     loss_v = float(loss.item())
-    if not args.eager and not args.no_roofline:
+    if not (args.eager or pipe) and not args.no_roofline:
         # graph replays cannot bracket single kernels: time the same conv launches (same shapes,
         # same inputs) in eager encoder forwards right after the timed region
         timer.enabled = True
@@ -202,7 +218,8 @@ def main():
                                 "frac": round(fam_flops / (fam_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF, 4),
                                 "conv_ms_per_step": round(fam_ms / args.steps, 3),
                                 "conv_gflop_per_image": round(per_img / 1e9, 3)},
-                "timing": "HIP events around each conv launch, " + (
+                "timing": "HIP events around each conv launch on its stream, " + (
+                    "inside the timed steps (pipelined: while the decoder step shares the GPU)" if pipe else
                     "inside the timed steps" if args.eager else
                     f"{args.steps} eager encoder forwards after the timed graph replays")}
     cpu = None
@@ -221,7 +238,7 @@ def main():
                        "vocab": args.vocab, "attention_dim": 512, "decoder_dim": 512, "embed_size": 512,
                        "parallelism": f"dp{N}"},
             "loss_last_step": round(loss_v, 5),
-            "launch": "eager" if args.eager else "hip_graph",
+            "launch": "pipelined_2stream_eager" if pipe else ("eager" if args.eager else "hip_graph"),
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -6,7 +6,13 @@
     params <- clamp(+-grad_clip) + Adam          (one kernel)
 
 Launch modes:
-  * eager: every call launches the ~640 kernels of the step from Python;
+  * eager: every call launches the ~530 kernels of the step from Python;
+  * pipelined (``pipeline=True``): call k runs the encoder of batch k on a low-priority stream
+    while the decoder step of batch k-1 runs on a high-priority one. The encoder is frozen and
+    reads no decoder state, so the result is bit-identical to the sequential order; the
+    decoder's latency-bound per-timestep kernels leave most CUs idle, which the encoder's
+    GEMMs fill. Each call returns the loss of the previous batch (None on the first);
+    ``flush()`` runs the last decoder step and returns its loss;
   * graph (``graph=True``): the step is captured once into a HIP graph (torch.cuda.CUDAGraph)
     and replayed; inputs are copied into static buffers first. Everything that changes from
     step to step lives on the device (Adam's step count, the dropout seed counter), so a
@@ -28,7 +34,7 @@ from .decoder_core import PNAMES
 
 class AttentionTrainStep:
     def __init__(self, encoder, decoder, optimizer, ctx=None, alpha_c=1.0, overlap=True, graph=False,
-                 seed=None):
+                 seed=None, pipeline=False):
         self.encoder, self.decoder, self.opt = encoder, decoder, optimizer
         dev = next(decoder.parameters()).device
         self.ctx = ctx or cdist.DistCtx(device=dev)
@@ -43,6 +49,19 @@ class AttentionTrainStep:
         self.seed_dev = torch.full((1,), s, dtype=torch.int64, device=dev)
         self._graph = None
         self._static = None
+        # pipelined mode: the frozen encoder of batch k runs on its own stream while the decoder
+        # step of batch k-1 runs (the encoder reads no decoder state); see _pipe_call
+        self.pipeline = pipeline
+        if pipeline:
+            if graph:
+                raise NotImplementedError("pipeline=True runs eagerly (two streams)")
+            lo, hi = torch.cuda.Stream.priority_range()
+            self.s_enc = torch.cuda.Stream(device=dev, priority=lo)
+            self.s_dec = torch.cuda.Stream(device=dev, priority=hi)
+            self._feats = [None, None]
+            self._slot = 0
+            self._pend = None
+            self._ev_dec = None
 
     def _grads(self):
         return {n: self.params[n].grad for n in self.need}
@@ -66,7 +85,60 @@ class AttentionTrainStep:
             self.opt.step()
         return loss
 
+    def _dec_body(self, feats, captions, caption_lengths, with_update):
+        K.counter_add(self.seed_dev, 1)
+        self._apply_pending()
+        loss, _, _ = DF.fused_loss_and_grads(self.decoder, feats, captions, caption_lengths,
+                                             self.alpha_c, self._grads(), need=self.need,
+                                             seed_dev=self.seed_dev)
+        if with_update:
+            self.opt.step()
+        return loss
+
+    def _pipe_call(self, imgs, captions, caption_lengths):
+        """Call k: encoder(batch k) on s_enc, concurrently decoder step of batch k-1 on s_dec.
+        Returns the loss of batch k-1 (None on the first call); flush() runs the last decoder.
+        The returned loss lives on s_dec: synchronize before reading it."""
+        cur = torch.cuda.current_stream()
+        slot = self._slot
+        self._slot ^= 1
+        N, _, H, W = imgs.shape
+        if self._feats[slot] is None or self._feats[slot].shape[0] != N:
+            self._feats[slot] = torch.empty(N, 14, 14, 2048, device=imgs.device, dtype=torch.float32)
+        # the slot's previous reader is the decoder of call k-1
+        self.s_enc.wait_stream(cur)
+        if self._ev_dec is not None:
+            self.s_enc.wait_event(self._ev_dec)
+        with torch.cuda.stream(self.s_enc):
+            self.encoder.forward_into(imgs, self._feats[slot])
+            ev_enc = torch.cuda.Event()
+            ev_enc.record(self.s_enc)
+        loss = self._pipe_decoder()
+        self._pend = (slot, captions, caption_lengths, ev_enc)
+        return loss
+
+    def _pipe_decoder(self):
+        if self._pend is None:
+            return None
+        pslot, caps, lens, ev = self._pend
+        self._pend = None
+        self.s_dec.wait_event(ev)
+        self.s_dec.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.s_dec):
+            if self.ctx.distributed:
+                loss = self._dec_body(self._feats[pslot], caps, lens, with_update=False)
+                cdist.allreduce_mean_(self.opt.grad_buffers(), self.ctx)
+                self.opt.step()
+            else:
+                loss = self._dec_body(self._feats[pslot], caps, lens, with_update=True)
+            loss = loss.detach().clone()  # the loss buffer is reused by the next decoder step
+            self._ev_dec = torch.cuda.Event()
+            self._ev_dec.record(self.s_dec)
+        return loss
+
     def __call__(self, imgs, captions, caption_lengths):
+        if self.pipeline:
+            return self._pipe_call(imgs, captions, caption_lengths)
         if self.graph_mode:
             return self._replay(imgs, captions, caption_lengths)
         return self._eager(imgs, captions, caption_lengths)
@@ -83,7 +155,15 @@ class AttentionTrainStep:
         return loss
 
     def flush(self):
+        """Complete all outstanding work (pipelined decoder step, pending DP update) and make the
+        current stream wait for it."""
+        loss = None
+        if self.pipeline:
+            loss = self._pipe_decoder()
+            torch.cuda.current_stream().wait_stream(self.s_dec)
+            torch.cuda.current_stream().wait_stream(self.s_enc)
         self._apply_pending()
+        return loss
 
     # ---------------------------------------------------------------- graph
     def _replay(self, imgs, captions, caption_lengths):

@@ -91,17 +91,33 @@ __global__ void __launch_bounds__(256) att_score_fwd_kernel(
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const float b0 = bf ? bf[0] : 0.f;
-  for (int p = p0 + wid; p < min(P, p0 + PCH); p += 4) {
-    const float* row = att_enc + ((long long)b * P + p) * A;
-    float acc = 0.f;
-    for (int a = lane * 4; a < A; a += 256) {
-      const float4 x = *reinterpret_cast<const float4*>(row + a);
-      const float4 d = *reinterpret_cast<const float4*>(ad + a);
-      const float4 w = *reinterpret_cast<const float4*>(wf + a);
-      acc += dot4(relu4(x + d), w);
+  // a wave owns rows p0+wid, p0+wid+4, ... (PCH/4 of them): all their loads are issued before
+  // any reduction, and the PCH/4 wave sums run interleaved
+  constexpr int R = PCH / 4;
+  const int pend = min(P, p0 + PCH);
+  float acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int p = p0 + wid + 4 * r;
+    acc[r] = 0.f;
+    if (p < pend) {
+      const float* row = att_enc + ((long long)b * P + p) * A;
+      for (int a = lane * 4; a < A; a += 256) {
+        const float4 x = *reinterpret_cast<const float4*>(row + a);
+        const float4 d = *reinterpret_cast<const float4*>(ad + a);
+        const float4 w = *reinterpret_cast<const float4*>(wf + a);
+        acc[r] += dot4(relu4(x + d), w);
+      }
     }
-    acc = wave_sum(acc);
-    if (lane == 0) e[(long long)b * P + p] = acc + b0;
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
+  if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int p = p0 + wid + 4 * r;
+      if (p < pend) e[(long long)b * P + p] = acc[r] + b0;
+    }
   }
 }
 

@@ -7,7 +7,6 @@ Same classes, constructor arguments, sub-module attributes and state-dict keys
 compute runs on libcapmi's HIP kernels (capmi.decoder_core): forward,
 backward-through-time, fused CE + regulariser and the clamp+Adam update.
 """
-import os
 import time
 
 import torch
@@ -181,7 +180,10 @@ def train(device, args):
                                   lr=args.decoder_lr)
     if opt_state is not None:
         decoder_optimizer.load_state_dict(opt_state)
-    step = AttentionTrainStep(encoder, decoder, decoder_optimizer, ctx, alpha_c=args.alpha_c)
+    # pipelined: the frozen encoder of batch k overlaps the decoder step of batch k-1
+    # (bit-identical results; losses arrive one batch late and are logged in order)
+    step = AttentionTrainStep(encoder, decoder, decoder_optimizer, ctx, alpha_c=args.alpha_c,
+                              pipeline=device.type == "cuda")
 
     decoder.train()
     encoder.train()
@@ -200,9 +202,15 @@ def train(device, args):
             captions = captions.to(device, non_blocking=True)
             clip_gradient(decoder_optimizer, args.grad_clip)
             loss = step(imgs, captions, caption_lengths)
-            pending.append(loss.detach().clone())
-            if batch_idx % args.print_freq == 0 or batch_idx == num_batches - 1:
-                for l in torch.stack(pending).view(-1).tolist():   # one sync per print
+            if batch_idx == num_batches - 1 and step.pipeline:
+                pending.append(loss)
+                loss = step.flush()  # the epoch's last decoder step
+            if loss is not None:
+                pending.append(loss if step.pipeline else loss.detach().clone())
+            if (batch_idx % args.print_freq == 0 or batch_idx == num_batches - 1) and pending:
+                if device.type == "cuda":
+                    torch.cuda.synchronize()  # losses live on the decoder stream
+                for l in torch.stack([p for p in pending if p is not None]).view(-1).tolist():
                     batch_losses.append(l)
                     accum_loss.update(l)
                 pending = []
@@ -226,4 +234,3 @@ def evaluate(device, args, encoder, decoder):
 
 
 __all__ = ["SoftAttention", "AttentionDecoderParams", "AttentionDecoder", "train", "evaluate"]
-_ = os

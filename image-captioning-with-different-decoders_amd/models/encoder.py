@@ -101,6 +101,15 @@ class EncoderAttention(nn.Module):
         return self._runner.forward(_ResNetView(self.resnet), imgs.contiguous(), out_hw,
                                     train=self.training)
 
+    def forward_into(self, imgs, out):
+        """forward() writing the (B,14,14,2048) features into a caller-owned buffer (the
+        pipelined training step keeps two of them)."""
+        _check_frozen(self.resnet)
+        out_hw = self.adaptive_pool.output_size
+        out_hw = (out_hw, out_hw) if isinstance(out_hw, int) else tuple(out_hw)
+        return self._runner.forward(_ResNetView(self.resnet), imgs.contiguous(), out_hw,
+                                    train=self.training, out=out)
+
     def fine_tune(self, on=True):
         for conv_block in list(self.resnet.children())[5:]:
             for param in conv_block.parameters():

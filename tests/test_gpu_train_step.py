@@ -91,3 +91,35 @@ def test_train_step_matches_oracle_end_to_end():
         agree = (torch.sign(upd[big]) == torch.sign(rupd[big])).float().mean().item()
         assert agree > 0.99, (n, agree)
     _ = copy
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.5])
+def test_pipelined_equals_eager(dropout):
+    """Two-stream pipelined step (encoder of batch k beside the decoder step of batch k-1) gives
+    bit-identical losses and parameters to the sequential step on the same batch sequence."""
+    B, L, V = 4, 7, 50
+    batches = [(t(gen.images(20 + i, B, 64, 64), DEV), t(gen.captions(20 + i, B, L, V), DEV)) for i in range(3)]
+    res = {}
+    for mode in ("eager", "pipe"):
+        enc, dec, opt, Step = _setup(dropout)
+        step = Step(enc, dec, opt, alpha_c=1.0, graph=False, seed=9, pipeline=(mode == "pipe"))
+        # eager/graph calls return the step's loss buffer (overwritten by the next call): clone
+        # it; the pipelined step returns its own copy, produced on the decoder stream (read it
+        # only after synchronizing)
+        out = []
+        for im, cp in batches:
+            x = step(im, cp, [L] * B)
+            out.append(x.clone() if mode == "eager" else x)
+        last = step.flush()
+        torch.cuda.synchronize()
+        losses = [float(x) for x in out if x is not None] + ([float(last)] if last is not None else [])
+        res[mode] = (losses, {n: q.detach().clone() for n, q in dec.named_parameters()},
+                     {k: v.clone() for k, v in enc.state_dict().items() if "running" in k})
+    le, pe, re_ = res["eager"]
+    lp, pp, rp = res["pipe"]
+    assert len(le) == len(lp) == 3
+    np.testing.assert_array_equal(np.array(lp), np.array(le))
+    for n in pe:
+        assert torch.equal(pe[n], pp[n]), n
+    for k in re_:
+        assert torch.equal(re_[k], rp[k]), k
