@@ -19,11 +19,13 @@ c_int, c_ll, c_float, c_double, c_vp = ctypes.c_int, ctypes.c_longlong, ctypes.c
 c_ull = ctypes.c_ulonglong
 
 CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_A_CONV_NHWC, CAPMI_A_CONV_NCHW, CAPMI_A_CONV_NHWC4 = 0, 1, 2, 3, 4
-CAPMI_B_NMAJOR_W, CAPMI_B_KROWS = 0, 1
+CAPMI_B_NMAJOR_W, CAPMI_B_KROWS, CAPMI_B_CONV_NHWC = 0, 1, 2
 CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO = 0, 1, 2, 3
 CAPMI_MAX_GROUP = 4
 CAPMI_COLSUM_GROUPS = 64
-ABI_VERSION = 5
+ABI_VERSION = 6
+CAPMI_BNB_RELU_Y, CAPMI_BNB_RELU_OUT = 0, 1
+CAPMI_BNB_MAX_SLABS = 256
 
 
 class GemmProblem(ctypes.Structure):
@@ -60,6 +62,13 @@ _SIGS = {
     "capmi_bn_add_relu": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_vp],
     "capmi_bn_relu_maxpool": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp],
     "capmi_adaptive_avgpool_nhwc": [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp],
+    "capmi_conv_weight_pack_dgrad": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
+    "capmi_conv_weight_unpack": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
+    "capmi_zero_upsample2_nhwc": [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp],
+    "capmi_bn_bwd_reduce": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_ll, c_int,
+                            c_vp, c_vp, c_int, c_vp, c_vp, c_vp],
+    "capmi_bn_bwd_apply": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_vp, c_vp, c_vp],
+    "capmi_adaptive_avgpool_bwd_nhwc": [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_embed_gather": [c_vp, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp, c_ll, c_vp],
     "capmi_mean_rows": [c_vp, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_att_score_fwd": [c_vp, c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp,
@@ -78,7 +87,8 @@ _SIGS = {
     "capmi_loss_finalize": [c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp],
     "capmi_lstm_cell_bwd": [c_vp, c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int,
                             c_vp, c_vp, c_vp],
-    "capmi_att_ctx_bwd": [c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp],
+    "capmi_att_ctx_bwd": [c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp],
+    "capmi_att_enc_dinput": [c_vp, c_ll, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_att_score_bwd": [c_vp, c_vp, c_ll, c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_int,
                             c_int, c_vp, c_vp, c_vp],
     "capmi_att_enc_grad": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,

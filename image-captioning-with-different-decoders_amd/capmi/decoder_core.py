@@ -210,14 +210,15 @@ class DecoderCore:
 
     # ------------------------------------------------------------------ backward
     def backward(self, p, st, grads, dpred, dpred_time_major=False, dreg=None, dalphas=None,
-                 need=None):
+                 need=None, denc=None):
         """Writes parameter gradients into ``grads`` (dict name->tensor, pre-allocated).
 
         dpred: gradient of the (B,T,V) predictions (batch-major), or time-major (T*B, V)
         when ``dpred_time_major``. dreg: (B,P) gradient added to every alphas[:, t]
         (the fused regulariser). dalphas: (B,T,P) gradient of the alphas output
         (generic autograd path). ``need``: names whose gradient is wanted (default: all
-        present in ``grads``)."""
+        present in ``grads``). ``denc``: (B,P,E) buffer receiving d(loss)/d(encoder_out) when
+        the encoder is fine-tuned (models/encoder.py:112-121), else None."""
         dm, ws = st["dm"], st["ws"]
         B, T, L, P, A, D, M, V, E, X = dm.B, dm.T, dm.L, dm.P, dm.A, dm.D, dm.M, dm.V, dm.E, dm.X
         enc, bt = st["enc"], st["bt"]
@@ -249,6 +250,9 @@ class DecoderCore:
         S_dh = sum(s_dh)
         W_ih_awe = W_ih[:, M:]
         wf = p["attention.full_att.weight"]
+        if denc is not None and getattr(ws, "DAWE", None) is None:
+            ws.DAWE = torch.empty(T, B, E, device=enc.device, dtype=torch.float32)
+            ws.DMEAN = torch.empty(B, E, device=enc.device, dtype=torch.float32)
         cur = 0
         for t in range(T - 1, -1, -1):
             K.lstm_cell_bwd(ws.DHD[t], ws.P_dh, S_dh if t < T - 1 else 0, B * D,
@@ -257,7 +261,8 @@ class DecoderCore:
             cur ^= 1
             K.gemm(K.problem(B, E, 4 * D, ws.DG[t], 4 * D, W_ih_awe, X, ws.P_dx, E, ksplit=dm.s_dx,
                              c_split_stride=B * E), AK, BKR, K.TILE_64)
-            K.att_ctx_bwd(ws.P_dx, dm.s_dx, B * E, ws.GATE[t], ws.AWE[t], enc, B, P, E, ws.DGP[t], ws.DALPHA)
+            K.att_ctx_bwd(ws.P_dx, dm.s_dx, B * E, ws.GATE[t], ws.AWE[t], enc, B, P, E, ws.DGP[t], ws.DALPHA,
+                          dawe_out=ws.DAWE[t] if denc is not None else None)
             if dalphas is not None:
                 dr, dr_ld = dalphas[:, t], T * P
             elif dreg is not None:
@@ -313,6 +318,13 @@ class DecoderCore:
             self._gemm_into(ws, grads["attention.enc_att.weight"], E, A, E, B * P, ws.DATT, A, enc, E, AMM, BKR)
         if "attention.enc_att.bias" in need:
             K.colsum(ws.DATT, B * P, A, A, grads["attention.enc_att.bias"], ws.work)
+        # d(encoder_out): init mean (:161) + context sums (:59-60) + enc_att (:54)
+        if denc is not None:
+            K.gemm([K.problem(B, E, D, ws.DH0, D, p["h_lin.weight"], E, ws.DMEAN, E)], AK, BKR, K.TILE_64)
+            K.gemm([K.problem(B, E, D, dc0, D, p["c_lin.weight"], E, ws.DMEAN, E, beta=1.0)], AK, BKR, K.TILE_64)
+            K.att_enc_dinput(st["alphas"], T * P, ws.DAWE, ws.DMEAN, B, T, P, E, denc)
+            self._gemm_into(ws, denc, E, B * P, E, A, ws.DATT, A, p["attention.enc_att.weight"], E, AK, BKR,
+                            beta=1.0)
         # embedding (only when fine-tuned, Q8): dX_emb = DG W_ih[:, :M] -> scatter-add by token
         if "embedding.weight" in need:
             demb = grads["embedding.weight"]

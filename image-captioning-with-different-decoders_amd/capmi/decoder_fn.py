@@ -56,6 +56,7 @@ class AttentionDecoderFn(torch.autograd.Function):
         st["gen"] = _GEN[0]
         ctx.st, ctx.p = st, p
         ctx.need = [n for n, t in zip(PNAMES, params) if t.requires_grad]
+        ctx.enc_grad = enc.requires_grad
         return preds, alphas
 
     @staticmethod
@@ -67,8 +68,10 @@ class AttentionDecoderFn(torch.autograd.Function):
         grads = {n: torch.empty_like(ctx.p[n]) for n in ctx.need}
         if dpred is None:
             dpred = torch.zeros(st["dm"].B, st["dm"].T, st["dm"].V, device=st["enc"].device)
-        CORE.backward(ctx.p, st, grads, dpred.contiguous(), dalphas=None if dalphas is None else dalphas.contiguous())
-        out = [None, None, None, None]
+        denc = torch.empty_like(st["enc"]) if ctx.enc_grad else None
+        CORE.backward(ctx.p, st, grads, dpred.contiguous(), dalphas=None if dalphas is None else dalphas.contiguous(),
+                      denc=denc)
+        out = [None, denc, None, None]
         for n in PNAMES:
             g = grads.get(n)
             if g is not None and n == "attention.full_att.weight":
@@ -80,8 +83,6 @@ class AttentionDecoderFn(torch.autograd.Function):
 def decoder_forward(dec, encoder_out, encoded_captions, caption_lengths):
     """models/attention.py:218-284 on the capmi kernels."""
     enc, caps = _prep_inputs(dec, encoder_out, encoded_captions)
-    if torch.is_grad_enabled() and encoder_out.requires_grad:
-        raise NotImplementedError("capmi: gradient w.r.t. encoder_out (encoder fine-tune) not built yet")
     decode_lengths = [int(l) - 1 for l in caption_lengths]
     params = [dict(dec.named_parameters())[n] for n in PNAMES]
     preds, alphas = AttentionDecoderFn.apply(dec, enc, caps, decode_lengths, *params)
@@ -111,12 +112,13 @@ _FS = FusedStepState()
 
 
 def fused_loss_and_grads(dec, encoder_out, captions, caption_lengths, alpha_c, grads, need=None,
-                         seed_dev=None):
+                         seed_dev=None, denc=None):
     """Forward + loss + backward of one decoder training step (models/attention.py:393-420).
 
     Writes d(loss)/d(param) into ``grads`` (name -> tensor, e.g. the optimizer's flat
     views); returns (loss (1,) device tensor, predictions, alphas). ``seed_dev``: an int64
-    device counter driving the dropout mask (graph-replayable); else a host seed is drawn."""
+    device counter driving the dropout mask (graph-replayable); else a host seed is drawn.
+    ``denc``: optional (B,14,14,2048)-sized buffer receiving d(loss)/d(encoder_out) (fine-tune)."""
     enc, caps = _prep_inputs(dec, encoder_out, captions)
     p = decoder_params(dec)
     decode_lengths = [int(l) - 1 for l in caption_lengths]
@@ -137,7 +139,8 @@ def fused_loss_and_grads(dec, encoder_out, captions, caption_lengths, alpha_c, g
     g = {n: grads[n] for n in (need if need is not None else grads)}
     if "attention.full_att.weight" in g:
         g["attention.full_att.weight"] = g["attention.full_att.weight"].view(-1)
-    CORE.backward(p, st, g, fs.dlogits, dpred_time_major=True, dreg=fs.dreg)
+    CORE.backward(p, st, g, fs.dlogits, dpred_time_major=True, dreg=fs.dreg,
+                  denc=None if denc is None else denc.view(B, P, -1))
     return fs.loss, preds, alphas
 
 

@@ -7,7 +7,7 @@ import ctypes
 
 import torch
 
-from ._lib import (CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W, CAPMI_COLSUM_GROUPS, CAPMI_TILE_128, CAPMI_TILE_64,
+from ._lib import (CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_COLSUM_GROUPS, CAPMI_TILE_128, CAPMI_TILE_64,
                    CAPMI_TILE_128x64, CAPMI_TILE_AUTO, GemmProblem, call, lib)
 
 F32 = torch.float32
@@ -175,6 +175,58 @@ def adaptive_avgpool_nhwc(inp, N, H, W, C, OH, OW, out):
 
 
 # --------------------------------------------------------------------------------------
+# encoder fine-tune backward
+# --------------------------------------------------------------------------------------
+def conv_weight_pack_dgrad(w, out):
+    """out[ci][kh][kw][co] = w[co][ci][KH-1-kh][KW-1-kw]"""
+    _cuda(w, out)
+    co, ci, kh, kw = w.shape
+    assert w.is_contiguous() and out.numel() == w.numel()
+    call("capmi_conv_weight_pack_dgrad", ptr(w), co, ci, kh, kw, ptr(out), stream())
+
+
+def conv_weight_unpack(packed, shape, out):
+    """[Cout][KH][KW][Cin] -> out [Cout][Cin][KH][KW] (``shape`` = nn.Conv2d weight shape)"""
+    _cuda(packed, out)
+    co, ci, kh, kw = shape
+    assert packed.numel() >= co * ci * kh * kw and out.numel() == co * ci * kh * kw and out.is_contiguous()
+    call("capmi_conv_weight_unpack", ptr(packed), co, ci, kh, kw, ptr(out), stream())
+
+
+def zero_upsample2_nhwc(dy, N, Ho, Wo, C, H, W, out):
+    _cuda(dy, out)
+    assert dy.numel() >= N * Ho * Wo * C and out.numel() >= N * H * W * C
+    call("capmi_zero_upsample2_nhwc", ptr(dy), N, Ho, Wo, C, H, W, ptr(out), stream())
+
+
+def bnb_work_floats(C):
+    return 2 * CAPMI_BNB_MAX_SLABS * C
+
+
+def bn_bwd_reduce(mode, d, y, mask_src, scale, shift, gamma, save_mean, save_var, eps, rows, C, dgamma,
+                  dbeta, coef, work, accumulate=False):
+    _cuda(d, y, mask_src, scale, shift, gamma, save_mean, save_var, dgamma, dbeta, coef, work)
+    assert work.numel() >= bnb_work_floats(C) and coef.numel() >= 4 * C
+    assert d.numel() >= rows * C and y.numel() >= rows * C
+    call("capmi_bn_bwd_reduce", int(mode), ptr(d), ptr(y), ptr(mask_src), ptr(scale), ptr(shift), ptr(gamma),
+         ptr(save_mean), ptr(save_var), float(eps), int(rows), int(C), ptr(dgamma), ptr(dbeta),
+         int(bool(accumulate)), ptr(coef), ptr(work), stream())
+
+
+def bn_bwd_apply(mode, d, y, mask_src, scale, shift, coef, rows, C, dy, dz_out=None):
+    _cuda(d, y, mask_src, scale, shift, coef, dy, dz_out)
+    assert d.numel() >= rows * C and dy.numel() >= rows * C
+    call("capmi_bn_bwd_apply", int(mode), ptr(d), ptr(y), ptr(mask_src), ptr(scale), ptr(shift), ptr(coef),
+         int(rows), int(C), ptr(dy), ptr(dz_out), stream())
+
+
+def adaptive_avgpool_bwd_nhwc(dout, N, H, W, C, OH, OW, din):
+    _cuda(dout, din)
+    assert dout.numel() >= N * OH * OW * C and din.numel() >= N * H * W * C
+    call("capmi_adaptive_avgpool_bwd_nhwc", ptr(dout), N, H, W, C, OH, OW, ptr(din), stream())
+
+
+# --------------------------------------------------------------------------------------
 # decoder
 # --------------------------------------------------------------------------------------
 def embed_gather(emb, caps, B, L, T, out, ld_out):
@@ -262,10 +314,17 @@ def lstm_cell_bwd(dhd, dh_part, S, slab, dc_in, act, c_prev, c_cur, B, D, bt, dg
          ptr(c_cur), B, D, bt, ptr(dgates), ptr(dc_out), stream())
 
 
-def att_ctx_bwd(part, S, slab, gate, awe, enc, B, P, E, dgp, dalpha):
-    _cuda(part, gate, awe, enc, dgp, dalpha)
+def att_ctx_bwd(part, S, slab, gate, awe, enc, B, P, E, dgp, dalpha, dawe_out=None):
+    _cuda(part, gate, awe, enc, dgp, dalpha, dawe_out)
     call("capmi_att_ctx_bwd", ptr(part), S, slab, ptr(gate), ptr(awe), ptr(enc), B, P, E, ptr(dgp),
-         ptr(dalpha), stream())
+         ptr(dalpha), ptr(dawe_out), stream())
+
+
+def att_enc_dinput(alpha, alpha_ld_b, dawe, dmean, B, T, P, E, denc):
+    _cuda(alpha, dawe, dmean, denc)
+    assert denc.numel() >= B * P * E and dawe.numel() >= T * B * E
+    call("capmi_att_enc_dinput", ptr(alpha), alpha_ld_b, ptr(dawe), ptr(dmean), B, T, P, E, ptr(denc),
+         stream())
 
 
 def att_score_bwd(dalpha, dreg, dreg_ld_b, alpha, alpha_ld_b, att_enc, att_dec, wf, B, P, A, bt, de,
@@ -308,3 +367,4 @@ def embed_scatter_add(dx, ld_dx, caps, B, L, T, bt_dev, M, demb):
 
 
 TILE_128, TILE_64, TILE_128x64, TILE_AUTO = CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO
+BNB_RELU_Y, BNB_RELU_OUT = 0, 1

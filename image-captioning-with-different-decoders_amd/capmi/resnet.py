@@ -17,7 +17,11 @@ import torch
 import torch.nn as nn
 
 from . import kernels as K
-from ._lib import CAPMI_A_CONV_NHWC, CAPMI_A_CONV_NHWC4, CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W
+from ._lib import CAPMI_A_CONV_NHWC, CAPMI_A_CONV_NHWC4, CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_B_CONV_NHWC
+from ._lib import CAPMI_B_KROWS, CAPMI_B_NMAJOR_W
+
+AK, AMM, AC = CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_A_CONV_NHWC
+BW, BKR, BCONV = CAPMI_B_NMAJOR_W, CAPMI_B_KROWS, CAPMI_B_CONV_NHWC
 
 
 class Bottleneck(nn.Module):
@@ -271,3 +275,261 @@ def conv_flops_per_image(net, H=224, W=224):
             h, w = h2, w2
     del convs
     return tot
+
+
+# ======================================================================================
+# fine-tune: forward that keeps the trainable stages' activations, and their backward
+# ======================================================================================
+class _Pool:
+    """Named device buffers, allocated once per (name, numel) and reused every step."""
+
+    def __init__(self):
+        self.bufs = {}
+
+    def get(self, name, n, device, dtype=torch.float32):
+        t = self.bufs.get(name)
+        if t is None or t.numel() < n or t.device != torch.device(device) or t.dtype != dtype:
+            t = torch.empty(n, device=device, dtype=dtype)
+            self.bufs[name] = t
+        return t[:n]
+
+
+class FineTuneRunner:
+    """EncoderAttention.fine_tune(True) (models/encoder.py:112-121): layer2, layer3 and layer4
+    (children()[5:]) are trainable, BatchNorm stays in train mode (batch statistics).
+
+    ``forward`` runs the same fused conv stack as EncoderRunner but writes every trainable
+    block's tensors (raw conv outputs y1/y2/y3/yd, block output, BN batch mean/var) into
+    buffers that live until ``backward``. ``backward`` walks the trainable blocks in reverse:
+    BN(train)+ReLU backward as reduce + apply kernels, conv weight gradients as
+    dY^T x im2col(X) GEMMs (the conv input re-derived from the saved pre-BN output through the
+    GEMM's BN-apply+ReLU prologue), data gradients as convs of dY with flipped weights
+    (zero-upsampled dY for the stride-2 3x3 convs, a strided-row GEMM store for the stride-2
+    downsample), residual gradients accumulated by the GEMM epilogue (beta = 1)."""
+
+    def __init__(self, runner, first_layer=2):
+        self.r = runner
+        self.first = first_layer
+        self.saved = _Pool()
+        self.grad = _Pool()
+        self.state = None
+
+    # ------------------------------------------------------------------ forward
+    def _bn_save(self, ws, bn, rows):
+        s, b = self.r._ss(ws, bn)
+        C = bn.num_features
+        ms = self.saved.get(f"ms.{id(bn)}", 2 * C, bn.weight.device).view(2, C)
+        mom = 0.1 if bn.momentum is None else bn.momentum
+        K.bn_finalize(ws["stats"], K.stat_tiles(rows), C, rows, bn.weight, bn.bias,
+                      bn.running_mean if bn.track_running_stats else None,
+                      bn.running_var if bn.track_running_stats else None, mom, bn.eps, s, b,
+                      ws["bnwork"], save_mean=ms[0], save_var=ms[1])
+        return s, b, ms
+
+    @torch.no_grad()
+    def forward(self, net, imgs, out_hw=(14, 14), out=None):
+        r = self.r
+        if imgs.dtype != torch.float32 or not imgs.is_contiguous():
+            raise TypeError("encoder input must be contiguous float32 (N,3,H,W)")
+        N, _, H, W = imgs.shape
+        dev = imgs.device
+        ws = r._workspace(N, H, W, dev)
+        # the optimizer updates trainable weights in place (same storage, same _version):
+        # drop their packed copies so this forward re-packs them
+        for li in range(self.first, 5):
+            for blk in getattr(net, f"layer{li}"):
+                r.packed.cache.pop(id(blk.conv2), None)
+        H1, W1, rows = r._conv("conv1", imgs, net.conv1, ws["y1"], N, H, W, True, nchw=True)
+        s, b = r._bn(ws, net.bn1, rows, True)
+        Hp, Wp = (H1 + 2 - 3) // 2 + 1, (W1 + 2 - 3) // 2 + 1
+        K.bn_relu_maxpool(ws["y1"], s, b, ws["x"], N, H1, W1, 64, Hp, Wp)
+        x, xo = ws["x"], ws["out"]
+        H, W, Cx = Hp, Wp, 64
+        bns = [net.bn1]
+        blocks = []
+        for li in range(1, 5):
+            for bi, blk in enumerate(getattr(net, f"layer{li}")):
+                tag = f"layer{li}.{bi}"
+                wd, Cout = blk.conv1.out_channels, blk.conv3.out_channels
+                st = blk.conv2.stride[0]
+                H2, W2 = (H + 2 - 3) // st + 1, (W + 2 - 3) // st + 1
+                r1, r3 = N * H * W, N * H2 * W2
+                if li < self.first:  # frozen stage: rotating workspace buffers
+                    y1, y2, y3, yd, o = ws["y1"], ws["y2"], ws["y3"], ws["yd"], xo
+                else:
+                    g = self.saved.get
+                    y1 = g(tag + ".y1", r1 * wd, dev)
+                    y2 = g(tag + ".y2", r3 * wd, dev)
+                    y3 = g(tag + ".y3", r3 * Cout, dev)
+                    yd = g(tag + ".yd", r3 * Cout, dev) if blk.downsample is not None else None
+                    o = g(tag + ".out", r3 * Cout, dev)
+                trainable = li >= self.first
+                bnf = (lambda bn, rows: self._bn_save(ws, bn, rows)) if trainable else \
+                    (lambda bn, rows: r._bn(ws, bn, rows, True) + (None,))
+                r._conv(tag + ".conv1", x, blk.conv1, y1, N, H, W, True)
+                s1, b1, m1 = bnf(blk.bn1, r1)
+                r._conv(tag + ".conv2", y1, blk.conv2, y2, N, H, W, True, in_ss=(s1, b1))
+                s2, b2, m2 = bnf(blk.bn2, r3)
+                r._conv(tag + ".conv3", y2, blk.conv3, y3, N, H2, W2, True, in_ss=(s2, b2))
+                s3, b3, m3 = bnf(blk.bn3, r3)
+                md = sd = bd = None
+                if blk.downsample is not None:
+                    r._conv(tag + ".downsample", x, blk.downsample[0], yd, N, H, W, True)
+                    sd, bd, md = bnf(blk.downsample[1], r3)
+                    K.bn_add_relu(y3, s3, b3, yd, o, r3, Cout, res_scale=sd, res_shift=bd)
+                    bns.append(blk.downsample[1])
+                else:
+                    K.bn_add_relu(y3, s3, b3, x, o, r3, Cout)
+                bns += [blk.bn1, blk.bn2, blk.bn3]
+                if trainable:
+                    blocks.append(dict(blk=blk, tag=tag, x=x, Cin=Cx, H=H, W=W, H2=H2, W2=W2, wd=wd, Cout=Cout,
+                                       stride=st, y1=y1, y2=y2, y3=y3, yd=yd, out=o,
+                                       ss=[(s1, b1, m1), (s2, b2, m2), (s3, b3, m3), (sd, bd, md)]))
+                    x = o
+                else:
+                    x, xo = o, x
+                H, W, Cx = H2, W2, Cout
+        nbt = [m.num_batches_tracked for m in bns if m.num_batches_tracked is not None]
+        if nbt:
+            torch._foreach_add_(nbt, 1)
+        OH, OW = out_hw
+        if out is None:
+            out = torch.empty(N, OH, OW, Cx, device=dev, dtype=torch.float32)
+        K.adaptive_avgpool_nhwc(x, N, H, W, Cx, OH, OW, out)
+        self.state = dict(N=N, H=H, W=W, C=Cx, OH=OH, OW=OW, blocks=blocks, device=dev)
+        return out
+
+    # ------------------------------------------------------------------ backward
+    def _gemm(self, prob, amode, bmode):
+        K.gemm_sk(prob, amode, self.r._ws["sk"], K.TILE_AUTO, bmode)
+
+    @torch.no_grad()
+    def backward(self, dfeat, grads, hook=None):
+        """dfeat: (N, OH, OW, 2048) gradient of the features. grads: dict id(param) -> tensor
+        receiving d(loss)/d(param) (conv weights in nn.Conv2d layout, BN weight/bias); missing
+        entries are skipped. ``hook(tag, flops, launch, key)`` optionally wraps every conv GEMM."""
+        stt = self.state
+        if stt is None:
+            raise RuntimeError("FineTuneRunner.backward without a saved forward")
+        N, dev = stt["N"], stt["device"]
+        gp = self.grad.get
+        blocks = stt["blocks"]
+        big = max(b["H"] * b["W"] * max(b["Cin"], b["Cout"], b["wd"]) for b in blocks) * N
+        dA = [gp("dA0", big, dev), gp("dA1", big, dev)]
+        dmid = gp("dmid", big, dev)
+        dy3 = gp("dy3", big, dev)
+        dyd = gp("dyd", big, dev)
+        up = gp("up", big, dev)
+        wmax = max(b["wd"] * 9 * b["wd"] for b in blocks)
+        dwp = gp("dw_packed", wmax, dev)
+        wdg = gp("w_dgrad", wmax, dev)
+        coef = gp("coef", 2 * 4 * 2048, dev).view(2, 4 * 2048)
+        work = gp("bnwork", K.bnb_work_floats(2048), dev)
+
+        def G(p):
+            return grads.get(id(p))
+
+        def run(tag, flops, prob, amode, bmode):
+            if hook is None:
+                self._gemm(prob, amode, bmode)
+            else:
+                bm, bn, sk, gen = K.gemm_sk_plan(prob, amode, K.TILE_AUTO, bmode)
+                hook(tag, flops, lambda: self._gemm(prob, amode, bmode),
+                     f"gemm_nt_kernel<{bm}, {bn}, {amode}, {bmode}, {'true' if prob.in_scale else 'false'}, "
+                     f"{'true' if sk else 'false'}>")
+
+        K.adaptive_avgpool_bwd_nhwc(dfeat.contiguous(), N, stt["H"], stt["W"], stt["C"], stt["OH"], stt["OW"],
+                                    dA[0])
+        cur = 0
+        for bi in range(len(blocks) - 1, -1, -1):
+            b = blocks[bi]
+            blk, tag = b["blk"], b["tag"]
+            H, W, H2, W2, s = b["H"], b["W"], b["H2"], b["W2"], b["stride"]
+            Cin, wd, Cout = b["Cin"], b["wd"], b["Cout"]
+            r1, r3 = N * H * W, N * H2 * W2
+            (s1, b1, m1), (s2, b2, m2), (s3, b3, m3), (sd, bd, md) = b["ss"]
+            dout = dA[cur]
+            need_dx = bi > 0
+            dx = dA[cur ^ 1] if need_dx else None
+            ds = blk.downsample
+            # ---- tail: out = relu(bn3(y3) + res)
+            bn3 = blk.bn3
+            K.bn_bwd_reduce(K.BNB_RELU_OUT, dout, b["y3"], b["out"], None, None, bn3.weight, m3[0], m3[1],
+                            bn3.eps, r3, Cout, G(bn3.weight), G(bn3.bias), coef[0], work)
+            if ds is not None:
+                bnd = ds[1]
+                K.bn_bwd_reduce(K.BNB_RELU_OUT, dout, b["yd"], b["out"], None, None, bnd.weight, md[0], md[1],
+                                bnd.eps, r3, Cout, G(bnd.weight), G(bnd.bias), coef[1], work)
+                K.bn_bwd_apply(K.BNB_RELU_OUT, dout, b["yd"], b["out"], None, None, coef[1], r3, Cout, dyd)
+            K.bn_bwd_apply(K.BNB_RELU_OUT, dout, b["y3"], b["out"], None, None, coef[0], r3, Cout, dy3,
+                           dz_out=dx if (need_dx and ds is None) else None)
+            # ---- conv3 (1x1): input relu(bn2(y2)) through the prologue
+            c3 = blk.conv3
+            geo3 = dict(N=N, H=H2, W=W2, Cin=wd, KH=1, KW=1, stride=1, pad=0, Ho=H2, Wo=W2)
+            if G(c3.weight) is not None:
+                run(tag + ".conv3.wgrad", 2.0 * r3 * Cout * wd,
+                    K.problem(Cout, wd, r3, dy3, Cout, b["y2"], 0, G(c3.weight), wd, conv=geo3, in_scale=s2,
+                              in_shift=b2), AMM, BCONV)
+            da2 = dmid[:r3 * wd]
+            run(tag + ".conv3.dgrad", 2.0 * r3 * Cout * wd,
+                K.problem(r3, wd, Cout, dy3, Cout, c3.weight, wd, da2, wd), AK, BKR)
+            # ---- bn2 + relu
+            bn2 = blk.bn2
+            K.bn_bwd_reduce(K.BNB_RELU_Y, da2, b["y2"], None, s2, b2, bn2.weight, m2[0], m2[1], bn2.eps, r3, wd,
+                            G(bn2.weight), G(bn2.bias), coef[0], work)
+            K.bn_bwd_apply(K.BNB_RELU_Y, da2, b["y2"], None, s2, b2, coef[0], r3, wd, da2)
+            # ---- conv2 (3x3, stride s): input relu(bn1(y1)) through the prologue
+            c2 = blk.conv2
+            geo2 = dict(N=N, H=H, W=W, Cin=wd, KH=3, KW=3, stride=s, pad=1, Ho=H2, Wo=W2)
+            if G(c2.weight) is not None:
+                run(tag + ".conv2.wgrad", 2.0 * r3 * wd * 9 * wd,
+                    K.problem(wd, 9 * wd, r3, da2, wd, b["y1"], 0, dwp, 9 * wd, conv=geo2, in_scale=s1,
+                              in_shift=b1), AMM, BCONV)
+                K.conv_weight_unpack(dwp, tuple(c2.weight.shape), G(c2.weight))
+            K.conv_weight_pack_dgrad(c2.weight.detach().contiguous(), wdg[:wd * 9 * wd])
+            if s == 1:
+                src = da2
+            else:
+                src = up[:r1 * wd]
+                K.zero_upsample2_nhwc(da2, N, H2, W2, wd, H, W, src)
+            da1 = dy3[:r1 * wd]  # dy3 is consumed
+            geod = dict(N=N, H=H, W=W, Cin=wd, KH=3, KW=3, stride=1, pad=1, Ho=H, Wo=W)
+            run(tag + ".conv2.dgrad", 2.0 * r3 * wd * 9 * wd,
+                K.problem(r1, wd, 9 * wd, src, 0, wdg, 9 * wd, da1, wd, conv=geod), AC, BW)
+            # ---- bn1 + relu
+            bn1 = blk.bn1
+            K.bn_bwd_reduce(K.BNB_RELU_Y, da1, b["y1"], None, s1, b1, bn1.weight, m1[0], m1[1], bn1.eps, r1, wd,
+                            G(bn1.weight), G(bn1.bias), coef[0], work)
+            K.bn_bwd_apply(K.BNB_RELU_Y, da1, b["y1"], None, s1, b1, coef[0], r1, wd, da1)
+            # ---- conv1 (1x1) on the block input x
+            c1 = blk.conv1
+            if G(c1.weight) is not None:
+                run(tag + ".conv1.wgrad", 2.0 * r1 * wd * Cin,
+                    K.problem(wd, Cin, r1, da1, wd, b["x"], Cin, G(c1.weight), Cin), AMM, BKR)
+            if need_dx:
+                run(tag + ".conv1.dgrad", 2.0 * r1 * wd * Cin,
+                    K.problem(r1, Cin, wd, da1, wd, c1.weight, Cin, dx, Cin, beta=1.0 if ds is None else 0.0),
+                    AK, BKR)
+            # ---- downsample (1x1, stride s) on x
+            if ds is not None:
+                cd = ds[0]
+                geodn = dict(N=N, H=H, W=W, Cin=Cin, KH=1, KW=1, stride=s, pad=0, Ho=H2, Wo=W2)
+                if G(cd.weight) is not None:
+                    run(tag + ".downsample.wgrad", 2.0 * r3 * Cout * Cin,
+                        K.problem(Cout, Cin, r3, dyd, Cout, b["x"], 0, G(cd.weight), Cin, conv=geodn), AMM, BCONV)
+                if need_dx:
+                    # dX[n, s*i, s*j, :] += dYd[n, i, j, :] W_d  (rows (n, i, j) -> strided NHWC rows)
+                    rm = dict(c_r1=W2, c_s2=s * W * Cin) if s > 1 else {}
+                    run(tag + ".downsample.dgrad", 2.0 * r3 * Cout * Cin,
+                        K.problem(r3, Cin, Cout, dyd, Cout, cd.weight, Cin, dx, s * Cin, beta=1.0, **rm),
+                        AK, BKR)
+            cur ^= 1
+        self.state = None
+
+
+def trainable_encoder_params(net, first_layer=2):
+    """Parameters of layer{first_layer}..layer4 (children()[5:] for first_layer = 2)."""
+    ps = []
+    for li in range(first_layer, 5):
+        ps += list(getattr(net, f"layer{li}").parameters())
+    return ps

@@ -34,8 +34,16 @@ from .decoder_core import PNAMES
 
 class AttentionTrainStep:
     def __init__(self, encoder, decoder, optimizer, ctx=None, alpha_c=1.0, overlap=True, graph=False,
-                 seed=None, pipeline=False):
+                 seed=None, pipeline=False, encoder_optimizer=None):
         self.encoder, self.decoder, self.opt = encoder, decoder, optimizer
+        # encoder fine-tune (config 4): the encoder's layer2-4 train with their own Adam
+        # (models/attention.py:332-335,424-430); the decoder then also returns d(features)
+        self.enc_opt = encoder_optimizer
+        self.fine_tune = encoder_optimizer is not None
+        if self.fine_tune:
+            pipeline = False  # the encoder of batch k needs the update of batch k-1
+            self._denc = None
+            self.enc_params = [q for grp in encoder_optimizer.param_groups for q in grp["params"]]
         dev = next(decoder.parameters()).device
         self.ctx = ctx or cdist.DistCtx(device=dev)
         self.alpha_c = alpha_c
@@ -66,15 +74,53 @@ class AttentionTrainStep:
     def _grads(self):
         return {n: self.params[n].grad for n in self.need}
 
+    def _grad_buffers(self):
+        bufs = list(self.opt.grad_buffers())
+        if self.fine_tune:
+            bufs += list(self.enc_opt.grad_buffers())
+        return bufs
+
+    def _step_all(self):
+        self.opt.step()
+        if self.fine_tune:
+            self.enc_opt.step()
+
     def _apply_pending(self):
         if self._pending is not None:
             for w in self._pending:
                 w.wait()
             self._pending = None
-            self.opt.step()
+            self._step_all()
 
     # ---------------------------------------------------------------- eager
+    def _body_ft(self, imgs, captions, caption_lengths, with_update):
+        """Fine-tune step: encoder forward keeping layer2-4 activations, decoder fwd/bwd also
+        producing d(features), encoder backward into the encoder optimizer's gradients."""
+        K.counter_add(self.seed_dev, 1)
+        self._apply_pending()
+        feats = self.encoder.ft_forward(imgs)
+        if self._denc is None or self._denc.shape != feats.shape:
+            self._denc = torch.empty_like(feats)
+        loss, _, _ = DF.fused_loss_and_grads(self.decoder, feats, captions, caption_lengths,
+                                             self.alpha_c, self._grads(), need=self.need,
+                                             seed_dev=self.seed_dev, denc=self._denc)
+        works = []
+        if self.ctx.distributed and not self.graph_mode:
+            # the decoder's gradients are final: their all-reduce overlaps the encoder backward
+            works = cdist.allreduce_mean_(self.opt.grad_buffers(), self.ctx, async_op=True)
+        self.encoder.ft_backward(self._denc, {id(q): q.grad for q in self.enc_params})
+        if self.ctx.distributed and not self.graph_mode:
+            works += cdist.allreduce_mean_(self.enc_opt.grad_buffers(), self.ctx, async_op=True)
+            for w in works:
+                w.wait()
+            self._step_all()
+        elif with_update:
+            self._step_all()
+        return loss
+
     def _body(self, imgs, captions, caption_lengths, with_update):
+        if self.fine_tune:
+            return self._body_ft(imgs, captions, caption_lengths, with_update)
         K.counter_add(self.seed_dev, 1)
         feats = self.encoder(imgs)
         self._apply_pending()
@@ -144,14 +190,14 @@ class AttentionTrainStep:
         return self._eager(imgs, captions, caption_lengths)
 
     def _eager(self, imgs, captions, caption_lengths):
-        if not self.ctx.distributed:
+        if not self.ctx.distributed or self.fine_tune:  # fine-tune: DP exchange inside _body_ft
             return self._body(imgs, captions, caption_lengths, with_update=True)
         loss = self._body(imgs, captions, caption_lengths, with_update=False)
-        works = cdist.allreduce_mean_(self.opt.grad_buffers(), self.ctx, async_op=self.overlap)
+        works = cdist.allreduce_mean_(self._grad_buffers(), self.ctx, async_op=self.overlap)
         if self.overlap:
             self._pending = works
         else:
-            self.opt.step()
+            self._step_all()
         return loss
 
     def flush(self):
@@ -181,8 +227,8 @@ class AttentionTrainStep:
             st["caps"].copy_(captions, non_blocking=True)
         self._graph.replay()
         if self.ctx.distributed:
-            cdist.allreduce_mean_(self.opt.grad_buffers(), self.ctx)
-            self.opt.step()
+            cdist.allreduce_mean_(self._grad_buffers(), self.ctx)
+            self._step_all()
         return st["loss"]
 
     def _capture(self, imgs, captions, caption_lengths, key, warmup=2):

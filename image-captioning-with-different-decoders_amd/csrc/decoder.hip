@@ -506,7 +506,7 @@ extern "C" int capmi_lstm_cell_bwd(const float* dhd, const float* dh_part, int S
 __global__ void __launch_bounds__(256) att_ctx_bwd_kernel(
     const float* __restrict__ part, int S, long long slab, const float* __restrict__ gate,
     const float* __restrict__ awe, const float* __restrict__ enc, int B, int P, int E,
-    float* __restrict__ dgp, float* __restrict__ dalpha) {
+    float* __restrict__ dgp, float* __restrict__ dalpha, float* __restrict__ dawe_out) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* dawe = smem;  // [E]
   const int b = blockIdx.y, p0 = blockIdx.x * PCH;
@@ -529,6 +529,7 @@ __global__ void __launch_bounds__(256) att_ctx_bwd_kernel(
       }
     }
     *reinterpret_cast<float4*>(dawe + c) = dw;
+    if (dawe_out && blockIdx.x == 0) *reinterpret_cast<float4*>(dawe_out + o) = dw;
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -545,15 +546,59 @@ __global__ void __launch_bounds__(256) att_ctx_bwd_kernel(
 
 extern "C" int capmi_att_ctx_bwd(const float* part, int S, long long slab, const float* gate,
                                  const float* awe, const float* enc, int B, int P, int E,
-                                 float* dgp, float* dalpha, void* stream) {
+                                 float* dgp, float* dalpha, float* dawe_out, void* stream) {
   CAPMI_REQUIRE(part && enc && dalpha && B > 0 && P > 0 && E > 0 && S >= 1, CAPMI_EINVAL);
+  CAPMI_REQUIRE(!dawe_out || aligned16(dawe_out), CAPMI_EALIGN);
   CAPMI_REQUIRE(E % 4 == 0 && E <= 16384 && slab % 4 == 0, CAPMI_ERANGE);
   CAPMI_REQUIRE(aligned16(part) && aligned16(enc) && (!gate || aligned16(gate)) &&
                     (!awe || aligned16(awe)) && (!dgp || aligned16(dgp)),
                 CAPMI_EALIGN);
   CAPMI_REQUIRE(!dgp || (gate && awe), CAPMI_EINVAL);
   hipLaunchKernelGGL(att_ctx_bwd_kernel, dim3(cdiv(P, PCH), B), dim3(256), E * sizeof(float),
-                     as_stream(stream), part, S, slab, gate, awe, enc, B, P, E, dgp, dalpha);
+                     as_stream(stream), part, S, slab, gate, awe, enc, B, P, E, dgp, dalpha, dawe_out);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
+// gradient w.r.t. encoder_out through the context sums and the init-state mean (fine-tune only):
+// denc[b][p][e] = sum_t alpha[b][t][p] * dawe[t][b][e] + dmean[b][e] / P      grid (P/8, B, E/1024)
+constexpr int DIN_PB = 8;
+__global__ void __launch_bounds__(256) att_enc_dinput_kernel(
+    const float* __restrict__ alpha, long long alpha_ld_b, const float* __restrict__ dawe,
+    const float* __restrict__ dmean, int B, int T, int P, int E, float* __restrict__ denc) {
+  extern __shared__ float al[];  // [T][DIN_PB]
+  const int b = blockIdx.y, p0 = blockIdx.x * DIN_PB;
+  for (int i = threadIdx.x; i < T * DIN_PB; i += 256) {
+    const int t = i / DIN_PB, j = i - t * DIN_PB;
+    al[i] = p0 + j < P ? alpha[(long long)b * alpha_ld_b + (long long)t * P + p0 + j] : 0.f;
+  }
+  __syncthreads();
+  const int e = (blockIdx.z * 256 + threadIdx.x) * 4;
+  if (e >= E) return;
+  float4 acc[DIN_PB];
+#pragma unroll
+  for (int j = 0; j < DIN_PB; ++j) acc[j] = f4(0.f);
+  for (int t = 0; t < T; ++t) {
+    const float4 d = *reinterpret_cast<const float4*>(dawe + ((long long)t * B + b) * E + e);
+#pragma unroll
+    for (int j = 0; j < DIN_PB; ++j) acc[j] = fma4(f4(al[t * DIN_PB + j]), d, acc[j]);
+  }
+  float4 dm = f4(0.f);
+  if (dmean) dm = *reinterpret_cast<const float4*>(dmean + (long long)b * E + e) * f4(1.f / (float)P);
+#pragma unroll
+  for (int j = 0; j < DIN_PB; ++j)
+    if (p0 + j < P) *reinterpret_cast<float4*>(denc + ((long long)b * P + p0 + j) * E + e) = acc[j] + dm;
+}
+
+extern "C" int capmi_att_enc_dinput(const float* alpha, long long alpha_ld_b, const float* dawe,
+                                    const float* dmean, int B, int T, int P, int E, float* denc,
+                                    void* stream) {
+  CAPMI_REQUIRE(alpha && dawe && denc && B > 0 && T > 0 && P > 0 && E > 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE(E % 4 == 0 && T <= 1024, CAPMI_ERANGE);
+  CAPMI_REQUIRE(aligned16(dawe) && aligned16(denc) && (!dmean || aligned16(dmean)), CAPMI_EALIGN);
+  hipLaunchKernelGGL(att_enc_dinput_kernel, dim3(cdiv(P, DIN_PB), B, cdiv(E, 1024)), dim3(256),
+                     T * DIN_PB * sizeof(float), as_stream(stream), alpha, alpha_ld_b, dawe, dmean, B, T, P, E,
+                     denc);
   CAPMI_LAUNCH_CHECK();
   return 0;
 }

@@ -1,0 +1,321 @@
+// Backward of the fine-tuned ResNet-101 stages (EncoderAttention.fine_tune, models/encoder.py:112-121:
+// layer2, layer3, layer4 get requires_grad; BASELINE config 4). The convolutions' data and weight
+// gradients run on the implicit-GEMM kernels (gemm_nt.hip: dgrad = NHWC conv of dY with the
+// flipped, transposed weights; wgrad = dY^T x implicit-im2col(X), BMODE 2). This file holds the
+// memory-bound rest, all NHWC with float4 I/O:
+//   * weight re-layouts for dgrad / gradient unpacking,
+//   * zero-upsampling of a stride-2 conv's output gradient (the transposed conv becomes a
+//     stride-1 conv),
+//   * BatchNorm2d(train) backward split into a per-channel reduction (which also yields the
+//     gamma/beta gradients) and an element-wise apply, with the ReLU mask recomputed from the
+//     saved pre-BN conv output (in-block BN+ReLU) or from the saved block output (bottleneck tail),
+//   * AdaptiveAvgPool2d backward (models/encoder.py:92,108).
+// BN backward (autograd of F.batch_norm(training=True)): with x^ = (y - mean) * invstd over the
+// N = rows samples of a channel, dz the gradient at the BN output,
+//   dbeta = sum dz, dgamma = sum dz * x^,  dy = gamma*invstd * (dz - dbeta/N - x^ * dgamma/N).
+#include "common.h"
+
+// ---------------------------------------------------------------------------------
+// weights
+// ---------------------------------------------------------------------------------
+// out[ci][kh][kw][co] = w[co][ci][KH-1-kh][KW-1-kw]: the B operand (W[N = Cin][K = (kh, kw, co)])
+// of the data-gradient conv dX = conv(dY, flip(W)^T)
+__global__ void conv_weight_pack_dgrad_kernel(const float* __restrict__ w, int Cout, int Cin, int KH, int KW,
+                                              float* __restrict__ out) {
+  const long long n = (long long)Cout * Cin * KH * KW;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int co = (int)(i % Cout);
+    long long r = i / Cout;
+    const int kw = (int)(r % KW);
+    r /= KW;
+    const int kh = (int)(r % KH);
+    const int ci = (int)(r / KH);
+    out[i] = w[(((long long)co * Cin + ci) * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)];
+  }
+}
+
+extern "C" int capmi_conv_weight_pack_dgrad(const float* w, int Cout, int Cin, int KH, int KW, float* out,
+                                            void* stream) {
+  CAPMI_REQUIRE(w && out && Cout > 0 && Cin > 0 && KH > 0 && KW > 0, CAPMI_EINVAL);
+  const long long n = (long long)Cout * Cin * KH * KW;
+  hipLaunchKernelGGL(conv_weight_pack_dgrad_kernel, dim3(std::min<long long>(cdiv(n, 256), 8192)), dim3(256),
+                     0, as_stream(stream), w, Cout, Cin, KH, KW, out);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
+// out[co][ci][kh][kw] (= nn.Conv2d weight layout) from the GEMM layout g[co][kh][kw][ci]
+__global__ void conv_weight_unpack_kernel(const float* __restrict__ g, int Cout, int Cin, int KH, int KW,
+                                          float* __restrict__ out) {
+  const long long n = (long long)Cout * Cin * KH * KW;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int kw = (int)(i % KW);
+    long long r = i / KW;
+    const int kh = (int)(r % KH);
+    r /= KH;
+    const int ci = (int)(r % Cin);
+    const int co = (int)(r / Cin);
+    out[i] = g[(((long long)co * KH + kh) * KW + kw) * Cin + ci];
+  }
+}
+
+extern "C" int capmi_conv_weight_unpack(const float* packed, int Cout, int Cin, int KH, int KW, float* out,
+                                        void* stream) {
+  CAPMI_REQUIRE(packed && out && Cout > 0 && Cin > 0 && KH > 0 && KW > 0, CAPMI_EINVAL);
+  const long long n = (long long)Cout * Cin * KH * KW;
+  hipLaunchKernelGGL(conv_weight_unpack_kernel, dim3(std::min<long long>(cdiv(n, 256), 8192)), dim3(256), 0,
+                     as_stream(stream), packed, Cout, Cin, KH, KW, out);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------
+// out (N,H,W,C) = dy (N,Ho,Wo,C) at even (h, w) positions, zero elsewhere
+// ---------------------------------------------------------------------------------
+__global__ void zero_upsample2_kernel(const float4* __restrict__ dy, int N, int Ho, int Wo, int C4, int H, int W,
+                                      float4* __restrict__ out) {
+  const long long n = (long long)N * H * W * C4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4);
+    long long r = i / C4;
+    const int w = (int)(r % W);
+    r /= W;
+    const int h = (int)(r % H);
+    const int img = (int)(r / H);
+    float4 v = f4(0.f);
+    if (((h | w) & 1) == 0 && (h >> 1) < Ho && (w >> 1) < Wo)
+      v = dy[(((long long)img * Ho + (h >> 1)) * Wo + (w >> 1)) * C4 + c];
+    out[i] = v;
+  }
+}
+
+extern "C" int capmi_zero_upsample2_nhwc(const float* dy, int N, int Ho, int Wo, int C, int H, int W, float* out,
+                                         void* stream) {
+  CAPMI_REQUIRE(dy && out && N > 0 && Ho > 0 && Wo > 0 && C > 0 && C % 4 == 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE(H >= 2 * Ho - 1 && W >= 2 * Wo - 1, CAPMI_EINVAL);
+  CAPMI_REQUIRE(aligned16(dy) && aligned16(out), CAPMI_EALIGN);
+  const long long n = (long long)N * H * W * C / 4;
+  hipLaunchKernelGGL(zero_upsample2_kernel, dim3(std::min<long long>(cdiv(n, 256), 16384)), dim3(256), 0,
+                     as_stream(stream), (const float4*)dy, N, Ho, Wo, C / 4, H, W, (float4*)out);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------
+// BatchNorm2d(train) backward
+// ---------------------------------------------------------------------------------
+// dz = d * relu'(.) with the mask of the forward's ReLU:
+//   CAPMI_BNB_RELU_Y   : in-block BN + ReLU, mask [fma(y, scale, shift) > 0] (the GEMM prologue's
+//                        exact expression, so the mask matches the forward bit for bit);
+//   CAPMI_BNB_RELU_OUT : bottleneck tail relu(bn3(y3) + residual), mask [out > 0] of the saved output.
+__device__ __forceinline__ float4 bnb_dz(int mode, float4 d, float4 y, const float* __restrict__ msrc,
+                                         long long i4, float4 sc, float4 sh) {
+  float4 m;
+  if (mode == CAPMI_BNB_RELU_OUT) {
+    m = reinterpret_cast<const float4*>(msrc)[i4];
+  } else {
+    m = fma4(y, sc, sh);
+  }
+  d.x = m.x > 0.f ? d.x : 0.f;
+  d.y = m.y > 0.f ? d.y : 0.f;
+  d.z = m.z > 0.f ? d.z : 0.f;
+  d.w = m.w > 0.f ? d.w : 0.f;
+  return d;
+}
+
+// stage 1: block (cb, slab): CB float4 channel groups x RL row lanes; partial (sum dz, sum dz*(y-mean))
+// per channel of the slab -> part[slab][c][2]
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(int mode, const float* __restrict__ d,
+                                                            const float* __restrict__ y,
+                                                            const float* __restrict__ msrc,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ shift,
+                                                            const float* __restrict__ mean, long long rows, int C,
+                                                            int CB, int rows_per_slab, float* __restrict__ part) {
+  __shared__ float4 rs[256], rq[256];
+  const int C4 = C / 4, RL = 256 / CB;
+  const int cg = threadIdx.x % CB, rl = threadIdx.x / CB;
+  const int c4 = blockIdx.x * CB + cg;
+  const long long r0 = (long long)blockIdx.y * rows_per_slab;
+  const long long r1 = min(rows, r0 + rows_per_slab);
+  float4 s = f4(0.f), q = f4(0.f);
+  if (c4 < C4) {
+    const int c = c4 * 4;
+    const float4 sc = *reinterpret_cast<const float4*>(scale + c);
+    const float4 sh = *reinterpret_cast<const float4*>(shift + c);
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+#pragma unroll 4
+    for (long long r = r0 + rl; r < r1; r += RL) {
+      const long long i4 = r * C4 + c4;
+      const float4 yv = reinterpret_cast<const float4*>(y)[i4];
+      const float4 dz = bnb_dz(mode, reinterpret_cast<const float4*>(d)[i4], yv, msrc, i4, sc, sh);
+      s = s + dz;
+      const float4 xc = make_float4(yv.x - mu.x, yv.y - mu.y, yv.z - mu.z, yv.w - mu.w);
+      q = fma4(dz, xc, q);
+    }
+  }
+  rs[threadIdx.x] = s;
+  rq[threadIdx.x] = q;
+  __syncthreads();
+  if (rl == 0 && c4 < C4) {
+    for (int l = 1; l < RL; ++l) {
+      s = s + rs[l * CB + cg];
+      q = q + rq[l * CB + cg];
+    }
+    float* p = part + ((long long)blockIdx.y * C + c4 * 4) * 2;
+    *reinterpret_cast<float4*>(p) = make_float4(s.x, q.x, s.y, q.y);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(s.z, q.z, s.w, q.w);
+  }
+}
+
+// stage 2: one thread per channel sums the slabs in fp64 (slab order: deterministic)
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int slabs, int C, long long count,
+                                       const float* __restrict__ gamma, const float* __restrict__ mean,
+                                       const float* __restrict__ var, float eps, float* dgamma, float* dbeta,
+                                       int accumulate, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int k = 0; k < slabs; ++k) {
+    const float2 v = *reinterpret_cast<const float2*>(part + ((long long)k * C + c) * 2);
+    s += v.x;
+    q += v.y;
+  }
+  const double inv = 1.0 / sqrt((double)var[c] + (double)eps);
+  const double dg = q * inv, db = s;
+  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)dg : (float)dg;
+  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)db : (float)db;
+  const double n = (double)count;
+  const double k1 = (double)gamma[c] * inv;
+  coef[c] = (float)k1;                      // gamma * invstd
+  coef[C + c] = (float)(k1 * inv * dg / n); // multiplies (y - mean)
+  coef[2 * C + c] = (float)(k1 * db / n);   // constant term
+  coef[3 * C + c] = mean[c];
+}
+
+extern "C" int capmi_bn_bwd_reduce(int mode, const float* d, const float* y, const float* mask_src,
+                                   const float* scale, const float* shift, const float* gamma,
+                                   const float* save_mean, const float* save_var, float eps, long long rows,
+                                   int C, float* dgamma, float* dbeta, int accumulate, float* coef, float* work,
+                                   void* stream) {
+  CAPMI_REQUIRE(mode == CAPMI_BNB_RELU_Y || mode == CAPMI_BNB_RELU_OUT, CAPMI_EINVAL);
+  CAPMI_REQUIRE(d && y && gamma && save_mean && save_var && coef && work && rows > 0 && C > 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE(mode != CAPMI_BNB_RELU_OUT || mask_src, CAPMI_EINVAL);
+  CAPMI_REQUIRE(mode != CAPMI_BNB_RELU_Y || (scale && shift), CAPMI_EINVAL);
+  CAPMI_REQUIRE(C % 4 == 0, CAPMI_ERANGE);
+  CAPMI_REQUIRE(aligned16(d) && aligned16(y) && (!mask_src || aligned16(mask_src)) && aligned16(save_mean) &&
+                    aligned16(work) && (!scale || (aligned16(scale) && aligned16(shift))),
+                CAPMI_EALIGN);
+  const int C4 = C / 4;
+  const int CB = std::min(64, C4);
+  const int gx = (C4 + CB - 1) / CB;
+  long long slabs = std::min<long long>(CAPMI_BNB_MAX_SLABS, std::max<long long>(1, 2048 / gx));
+  slabs = std::min<long long>(slabs, (rows + 31) / 32);
+  const int per = (int)((rows + slabs - 1) / slabs);
+  slabs = (rows + per - 1) / per;
+  hipStream_t s = as_stream(stream);
+  // mode RELU_OUT never reads scale/shift: pass the mean as a harmless valid pointer
+  const float* sc = scale ? scale : save_mean;
+  const float* sh = shift ? shift : save_mean;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(gx, (unsigned)slabs), dim3(256), 0, s, mode, d, y, mask_src, sc,
+                     sh, save_mean, rows, C, CB, per, work);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, work, (int)slabs, C, rows,
+                     gamma, save_mean, save_var, eps, dgamma, dbeta, accumulate, coef);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
+// dy = k1*dz - k2*(y - mean) - k0; dz_out (optional) = dz (the residual branch's gradient)
+__global__ void bn_bwd_apply_kernel(int mode, const float4* __restrict__ d, const float4* __restrict__ y,
+                                    const float* __restrict__ msrc, const float* __restrict__ scale,
+                                    const float* __restrict__ shift, const float* __restrict__ coef, long long n4,
+                                    int C4, float4* dy, float4* dz_out) {
+  const int C = C4 * 4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    const float4 yv = y[i];
+    float4 sc = f4(0.f), sh = f4(0.f);
+    if (mode == CAPMI_BNB_RELU_Y) {
+      sc = *reinterpret_cast<const float4*>(scale + c);
+      sh = *reinterpret_cast<const float4*>(shift + c);
+    }
+    const float4 dz = bnb_dz(mode, d[i], yv, msrc, i, sc, sh);
+    const float4 k1 = *reinterpret_cast<const float4*>(coef + c);
+    const float4 k2 = *reinterpret_cast<const float4*>(coef + C + c);
+    const float4 k0 = *reinterpret_cast<const float4*>(coef + 2 * C + c);
+    const float4 mu = *reinterpret_cast<const float4*>(coef + 3 * C + c);
+    float4 r;
+    r.x = fmaf(k1.x, dz.x, -fmaf(k2.x, yv.x - mu.x, k0.x));
+    r.y = fmaf(k1.y, dz.y, -fmaf(k2.y, yv.y - mu.y, k0.y));
+    r.z = fmaf(k1.z, dz.z, -fmaf(k2.z, yv.z - mu.z, k0.z));
+    r.w = fmaf(k1.w, dz.w, -fmaf(k2.w, yv.w - mu.w, k0.w));
+    if (dz_out) dz_out[i] = dz;
+    dy[i] = r;
+  }
+}
+
+extern "C" int capmi_bn_bwd_apply(int mode, const float* d, const float* y, const float* mask_src,
+                                  const float* scale, const float* shift, const float* coef, long long rows, int C,
+                                  float* dy, float* dz_out, void* stream) {
+  CAPMI_REQUIRE(mode == CAPMI_BNB_RELU_Y || mode == CAPMI_BNB_RELU_OUT, CAPMI_EINVAL);
+  CAPMI_REQUIRE(d && y && coef && dy && rows >= 0 && C > 0 && C % 4 == 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE(mode != CAPMI_BNB_RELU_OUT || mask_src, CAPMI_EINVAL);
+  CAPMI_REQUIRE(mode != CAPMI_BNB_RELU_Y || (scale && shift), CAPMI_EINVAL);
+  CAPMI_REQUIRE(aligned16(d) && aligned16(y) && aligned16(coef) && aligned16(dy) && (!dz_out || aligned16(dz_out)) &&
+                    (!mask_src || aligned16(mask_src)) && (!scale || (aligned16(scale) && aligned16(shift))),
+                CAPMI_EALIGN);
+  const long long n4 = rows * C / 4;
+  if (n4 == 0) return 0;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(std::min<long long>(cdiv(n4, 256), 16384)), dim3(256), 0,
+                     as_stream(stream), mode, (const float4*)d, (const float4*)y, mask_src, scale, shift, coef,
+                     n4, C / 4, (float4*)dy, (float4*)dz_out);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------
+// AdaptiveAvgPool2d backward on NHWC: din[n][h][w] = sum over the output cells whose window
+// [floor(o*H/OH), ceil((o+1)*H/OH)) contains (h, w) of dout / window area
+// ---------------------------------------------------------------------------------
+__global__ void adaptive_avgpool_bwd_kernel(const float4* __restrict__ dout, int N, int H, int W, int C4, int OH,
+                                            int OW, float4* __restrict__ din) {
+  const long long n = (long long)N * H * W * C4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4);
+    long long r = i / C4;
+    const int w = (int)(r % W);
+    r /= W;
+    const int h = (int)(r % H);
+    const int img = (int)(r / H);
+    float4 acc = f4(0.f);
+    const int oh_lo = max(0, (h * OH) / H - 1), oh_hi = min(OH - 1, ((h + 1) * OH + H - 1) / H);
+    const int ow_lo = max(0, (w * OW) / W - 1), ow_hi = min(OW - 1, ((w + 1) * OW + W - 1) / W);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int h0 = (oh * H) / OH, h1 = ((oh + 1) * H + OH - 1) / OH;
+      if (h < h0 || h >= h1) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int w0 = (ow * W) / OW, w1 = ((ow + 1) * W + OW - 1) / OW;
+        if (w < w0 || w >= w1) continue;
+        const float inv = 1.f / (float)((h1 - h0) * (w1 - w0));
+        acc = fma4(dout[(((long long)img * OH + oh) * OW + ow) * C4 + c], f4(inv), acc);
+      }
+    }
+    din[i] = acc;
+  }
+}
+
+extern "C" int capmi_adaptive_avgpool_bwd_nhwc(const float* dout, int N, int H, int W, int C, int OH, int OW,
+                                               float* din, void* stream) {
+  CAPMI_REQUIRE(dout && din && N > 0 && H > 0 && W > 0 && OH > 0 && OW > 0 && C > 0 && C % 4 == 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE(aligned16(dout) && aligned16(din), CAPMI_EALIGN);
+  const long long n = (long long)N * H * W * C / 4;
+  hipLaunchKernelGGL(adaptive_avgpool_bwd_kernel, dim3(std::min<long long>(cdiv(n, 256), 16384)), dim3(256), 0,
+                     as_stream(stream), (const float4*)dout, N, H, W, C / 4, OH, OW, (float4*)din);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}

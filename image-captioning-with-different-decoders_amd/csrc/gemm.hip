@@ -391,7 +391,8 @@ struct GemmPlan {
 
 int gemm_plan(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, int tile, GemmPlan& g) {
   CAPMI_REQUIRE(probs != nullptr && nprob >= 1 && nprob <= CAPMI_MAX_GROUP, CAPMI_EINVAL);
-  CAPMI_REQUIRE(amode >= 0 && amode <= 4 && bmode >= 0 && bmode <= 1, CAPMI_EINVAL);
+  CAPMI_REQUIRE(amode >= 0 && amode <= 4 && bmode >= 0 && bmode <= 2, CAPMI_EINVAL);
+  CAPMI_REQUIRE(bmode != 2 || amode == 1, CAPMI_EINVAL);
   CAPMI_REQUIRE(tile >= CAPMI_TILE_128 && tile <= CAPMI_TILE_AUTO, CAPMI_EINVAL);
   CAPMI_REQUIRE(amode != 4 || bmode == 0, CAPMI_EINVAL);
   GemmArgs& a = g.a;
@@ -400,7 +401,8 @@ int gemm_plan(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, 
   bool vec = true;
   // v2 kernel eligible: row-major A (dense / conv) with B = W[N][K], or the transposed-staging
   // forms (A stored as k rows and/or B stored as k rows) of the backward GEMMs
-  bool nt_ok = ((amode == 0 || amode == 2 || amode == 4) && bmode == 0) || ((amode == 0 || amode == 1) && bmode == 1);
+  bool nt_ok = ((amode == 0 || amode == 2 || amode == 4) && bmode == 0) || ((amode == 0 || amode == 1) && bmode == 1) ||
+               (amode == 1 && bmode == 2);
   int maxN = 0;
   for (int i = 0; i < nprob; ++i) {
     const capmi_gemm_problem& p = probs[i];
@@ -422,6 +424,15 @@ int gemm_plan(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, 
       CAPMI_REQUIRE(aligned16(p.A) && aligned16(p.B) && p.ldb % 4 == 0 && p.in_scale == nullptr,
                     CAPMI_EALIGN);
     }
+    if (bmode == 2) {
+      // weight gradient of a conv: B[k = output pixel][n = (kh, kw, ci)] = X (implicit im2col)
+      CAPMI_REQUIRE(p.cCin % 4 == 0 && p.N == p.cKH * p.cKW * p.cCin && p.K == p.cN * p.cHo * p.cWo,
+                    CAPMI_EINVAL);
+      CAPMI_REQUIRE(p.K < (1 << 24), CAPMI_ERANGE);
+      CAPMI_REQUIRE(aligned16(p.B), CAPMI_EALIGN);
+      CAPMI_REQUIRE(p.in_scale == nullptr || (aligned16(p.in_scale) && aligned16(p.in_shift)),
+                    CAPMI_EALIGN);
+    }
     if (amode == 3) {
       CAPMI_REQUIRE(p.K == p.cKH * p.cKW * p.cCin && p.M == p.cN * p.cHo * p.cWo, CAPMI_EINVAL);
     }
@@ -432,12 +443,15 @@ int gemm_plan(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, 
     }
     if (bmode == 0)
       vec = vec && aligned16(p.B) && p.ldb % 4 == 0 && p.K % 4 == 0;
+    else if (bmode == 2)
+      vec = vec && p.N % 4 == 0;
     else
       vec = vec && aligned16(p.B) && p.ldb % 4 == 0 && p.N % 4 == 0;
     a.p[i] = p;
     maxN = std::max(maxN, p.N);
   }
   nt_ok = nt_ok && (vec || ((amode == 2 || amode == 4) && bmode == 0));
+  CAPMI_REQUIRE(bmode != 2 || nt_ok, CAPMI_EALIGN);  // no generic-kernel form of the im2col B
   int bm = 128, bn = 128;
   if (tile == CAPMI_TILE_64) {
     bm = bn = 64;

@@ -18,7 +18,10 @@
 //     every problem field is read once into registers before the loop;
 //   * tile shapes 128x128 / 128x64 / 64x64 (4 waves, 2x2) so grids of the small-M layers
 //     (ResNet layer3/layer4, M = 64*196 / 64*49) still fill 256 CUs with >= 2 WGs each;
-//   * XCD-aware block order: consecutive tiles (same A rows) land on one XCD's L2.
+//   * XCD-aware block order: consecutive tiles (same A rows) land on one XCD's L2;
+//   * BMODE 2 (conv weight gradient dW = dY^T im2col(X)): B is the implicit im2col of an NHWC
+//     input read as k rows (k = output pixel, n = (kh, kw, ci)), staged like BMODE 1; the
+//     optional BN-apply+ReLU prologue then acts on B (the conv's input is relu(bn(y_prev))).
 // Numerics: unchanged (exact fp32 fmaf chains, different k order than any CPU library).
 #include "gemm_args.h"
 
@@ -46,6 +49,14 @@ __device__ __forceinline__ void store_t4(float* d, const float4 v, int tid) {
     const float x = c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
     d[c * S2] = x;
   }
+}
+
+// q = a / b for 0 <= a < 2^24, b > 0, from a float reciprocal plus one correction step
+__device__ __forceinline__ int fdivq(int a, int b, float inv_b) {
+  int q = (int)((float)a * inv_b);
+  const int r = a - q * b;
+  q += r < 0 ? -1 : (r >= b ? 1 : 0);
+  return q;
 }
 
 // resident workgroups per SIMD the register budget is sized for (== gemm_nt_wg_per_cu)
@@ -127,9 +138,33 @@ gemm_nt_kernel(const GemmArgs args) {
     long long b_base[NB];
     int b_k[NB];
     bool b_ok[NB];
+    // BMODE 2 (wgrad): the n column (kh, kw, ci..ci+3) of a slot is fixed for the whole k loop
+    int b_kh[NB], b_kw[NB];
+    float4 b_sc[NB], b_sh[NB];
+    const int cWo = P.cWo, cHW = P.cHo * P.cWo, cStr = P.cStride, cPd = P.cPad;
+    const float inv_hw = 1.f / (float)cHW, inv_wo = 1.f / (float)cWo;
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int f = tid + i * 256;
+      b_kh[i] = b_kw[i] = 0;
+      b_sc[i] = f4(1.f);
+      b_sh[i] = f4(0.f);
+      if (BMODE == 2) {
+        const int jq = (tid & 15) + 16 * (i % BQ16);
+        const int n = n0 + jq * 4;
+        b_ok[i] = n < N;  // N % 4 == 0, Cin % 4 == 0: a float4 never straddles (kh, kw)
+        const int nn = b_ok[i] ? n : 0;
+        const int kpos = nn / cCin, ci = nn - kpos * cCin;
+        b_kh[i] = kpos / cKW;
+        b_kw[i] = kpos - b_kh[i] * cKW;
+        b_base[i] = ci;
+        b_k[i] = (tid >> 4) + 16 * (i / BQ16);
+        if (PRO) {
+          b_sc[i] = *reinterpret_cast<const float4*>(isc + ci);
+          b_sh[i] = *reinterpret_cast<const float4*>(ish + ci);
+        }
+        continue;
+      }
       if (BMODE == 1) {
         const int jq = (tid & 15) + 16 * (i % BQ16);
         const int n = n0 + jq * 4;
@@ -216,7 +251,17 @@ gemm_nt_kernel(const GemmArgs args) {
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        if (BMODE == 1) {
+        if (BMODE == 2) {
+          // k row = output pixel (img, oh, ow) of the forward conv; the column is (kh, kw, ci)
+          const int kr = k_lo + kt * BK2 + b_k[i];
+          const int img = fdivq(kr, cHW, inv_hw), rem = kr - img * cHW;
+          const int oh = fdivq(rem, cWo, inv_wo), ow = rem - oh * cWo;
+          const int ih = oh * cStr - cPd + b_kh[i], iw = ow * cStr - cPd + b_kw[i];
+          const bool ok = b_ok[i] && kr < k_hi && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
+          const long long off = (((long long)img * cH + ih) * cW + iw) * cCin + b_base[i];
+          st.rb[i] = *reinterpret_cast<const float4*>(Bg + (ok ? off : 0));
+          st.bm |= (unsigned)ok << i;
+        } else if (BMODE == 1) {
           const int kr = k_lo + kt * BK2 + b_k[i];
           const bool ok = b_ok[i] && kr < k_hi;
           st.rb[i] = *reinterpret_cast<const float4*>(Bg + (ok ? (long long)kr * ldb + b_base[i] : 0));
@@ -232,7 +277,7 @@ gemm_nt_kernel(const GemmArgs args) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         float4 v = st.ra[i];
-        if (PRO) v = relu4(fma4(v, st.sc, st.sh));
+        if (PRO && AMODE == 2) v = relu4(fma4(v, st.sc, st.sh));
         if (!((st.am >> i) & 1u)) v = f4(0.f);
         const int f = tid + i * 256;
         if (AMODE == 1) {
@@ -244,9 +289,10 @@ gemm_nt_kernel(const GemmArgs args) {
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
         float4 v = st.rb[i];
+        if (PRO && BMODE == 2) v = relu4(fma4(v, b_sc[i], b_sh[i]));
         if (!((st.bm >> i) & 1u)) v = f4(0.f);
         const int f = tid + i * 256;
-        if (BMODE == 1) {
+        if (BMODE >= 1) {
           store_t4(&Bs[buf][(i % BQ16 * 16 + (tid & 15)) * 4 * S2 + (tid >> 4) + 16 * (i / BQ16)], v, tid);
         } else {
           *reinterpret_cast<float4*>(&Bs[buf][(f >> 3) * S2 + kq]) = v;
@@ -496,7 +542,12 @@ gemm_nt_kernel(const GemmArgs args) {
 template <int BM, int BN, bool SK>
 void launch_sk(const GemmArgs& a, int amode, int bmode, bool pro, int blocks, hipStream_t s) {
   const dim3 g(blocks), b(256);
-  if (bmode == 1) {
+  if (bmode == 2) {  // weight gradient: A = dY stored as k rows, B = implicit im2col k rows
+    if (pro)
+      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 1, 2, true, SK>), g, b, 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 1, 2, false, SK>), g, b, 0, s, a);
+  } else if (bmode == 1) {
     if (amode == 1)
       hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 1, 1, false, SK>), g, b, 0, s, a);
     else
@@ -531,7 +582,8 @@ int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int 
   for (int i = 0; i < a.nprob; ++i) pro = pro || a.p[i].in_scale != nullptr;
   for (int i = 0; i < a.nprob; ++i)
     if (pro && a.p[i].in_scale == nullptr) return CAPMI_EINVAL;  // grouped: all or none
-  if (pro && amode != 2) return CAPMI_EINVAL;
+  if (pro && !((amode == 2 && bmode == 0) || (amode == 1 && bmode == 2))) return CAPMI_EINVAL;
+  if (bmode == 2 && amode != 1) return CAPMI_EINVAL;
   if (bm == 128 && bn == 128) return launch_bmbn<128, 128>(a, amode, bmode, pro, blocks, s);
   if (bm == 128 && bn == 64) return launch_bmbn<128, 64>(a, amode, bmode, pro, blocks, s);
   if (bm == 64 && bn == 64) return launch_bmbn<64, 64>(a, amode, bmode, pro, blocks, s);

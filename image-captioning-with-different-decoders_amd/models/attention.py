@@ -143,7 +143,9 @@ def train(device, args):
     if args.checkpoint is None:
         encoder = EncoderAttention()
         if args.fine_tune_encoder:
-            raise NotImplementedError("capmi: encoder fine-tuning is not built yet (config 4)")
+            # the reference builds Adam over an all-frozen encoder here and crashes (Q9);
+            # fine-tuning means fine_tune(True): layer2-4 trainable (models/encoder.py:112-121)
+            encoder.fine_tune(True)
         decoder_params = AttentionDecoderParams()
         decoder_params.attention_dim = args.attention_dim
         decoder_params.decoder_dim = args.decoder_dim
@@ -159,10 +161,12 @@ def train(device, args):
         start_epoch, metrics, opt_state = 0, {}, None
     else:
         chkpt = load_checkpoint(device, args)
-        start_epoch, enc_sd, dec_sd, _, opt_state, metrics = unpack_checkpoint(chkpt)
+        start_epoch, enc_sd, dec_sd, enc_opt_state, opt_state, metrics = unpack_checkpoint(chkpt)
         start_epoch += 1
         encoder = EncoderAttention()
         encoder.load_state_dict(enc_sd)
+        if args.fine_tune_encoder:
+            encoder.fine_tune(True)
         decoder_params = AttentionDecoderParams()
         decoder_params.attention_dim, decoder_params.decoder_dim = args.attention_dim, args.decoder_dim
         decoder_params.embed_size, decoder_params.dropout = args.embed_size, args.decoder_dropout
@@ -180,10 +184,19 @@ def train(device, args):
                                   lr=args.decoder_lr)
     if opt_state is not None:
         decoder_optimizer.load_state_dict(opt_state)
+    encoder_optimizer = None
+    if args.fine_tune_encoder:
+        cdist.broadcast_module(encoder, ctx)
+        encoder_optimizer = FusedAdam(filter(lambda p: p.requires_grad, encoder.parameters()),
+                                      lr=args.encoder_lr)
+        if args.checkpoint is not None and enc_opt_state is not None:
+            encoder_optimizer.load_state_dict(enc_opt_state)
     # pipelined: the frozen encoder of batch k overlaps the decoder step of batch k-1
-    # (bit-identical results; losses arrive one batch late and are logged in order)
+    # (bit-identical results; losses arrive one batch late and are logged in order).
+    # Fine-tuning runs the sequential step (the encoder needs the previous update).
     step = AttentionTrainStep(encoder, decoder, decoder_optimizer, ctx, alpha_c=args.alpha_c,
-                              pipeline=device.type == "cuda")
+                              pipeline=device.type == "cuda" and encoder_optimizer is None,
+                              encoder_optimizer=encoder_optimizer)
 
     decoder.train()
     encoder.train()
@@ -201,6 +214,8 @@ def train(device, args):
             imgs = imgs.to(device, non_blocking=True)
             captions = captions.to(device, non_blocking=True)
             clip_gradient(decoder_optimizer, args.grad_clip)
+            if encoder_optimizer is not None:
+                clip_gradient(encoder_optimizer, args.grad_clip)
             loss = step(imgs, captions, caption_lengths)
             if batch_idx == num_batches - 1 and step.pipeline:
                 pending.append(loss)
@@ -222,7 +237,7 @@ def train(device, args):
         epoch_losses.append(batch_losses)
         metrics = {'epoch_losses': epoch_losses}
         if ctx.rank == 0:
-            save_checkpoint(args, epoch, encoder, decoder, None, decoder_optimizer, metrics)
+            save_checkpoint(args, epoch, encoder, decoder, encoder_optimizer, decoder_optimizer, metrics)
     if ctx.rank == 0:
         print(f'Model {args.model_name} finished training for {args.epochs} epochs.')
 

@@ -14,7 +14,7 @@ import torch
 from torch import nn
 
 from capmi import kernels as K
-from capmi.resnet import EncoderRunner, resnet101
+from capmi.resnet import EncoderRunner, FineTuneRunner, resnet101, trainable_encoder_params
 
 _LOCAL_WEIGHTS = os.path.join("models", "resnet101.pth")
 
@@ -40,8 +40,38 @@ class _ResNetView:
 def _check_frozen(module):
     if torch.is_grad_enabled() and any(p.requires_grad for p in module.parameters()):
         raise NotImplementedError(
-            "capmi: encoder fine-tuning (conv dgrad/wgrad, BASELINE config 4) is not built yet; "
-            "the frozen-encoder forward is")
+            "capmi: a trainable Encoder (baseline model) is not on the capmi path; EncoderAttention "
+            "supports fine_tune() (layer2-4)")
+
+
+def _fine_tuned(seq):
+    """True when any parameter of the resnet requires grad; only children()[5:] (layer2-4, what
+    fine_tune() switches, models/encoder.py:112-121) may: the stem and layer1 stay frozen."""
+    if not any(p.requires_grad for p in seq.parameters()):
+        return False
+    for i in range(5):
+        if any(p.requires_grad for p in seq[i].parameters()):
+            raise NotImplementedError("capmi: only layer2-4 (EncoderAttention.fine_tune) can be trained")
+    return True
+
+
+class EncoderFineTuneFn(torch.autograd.Function):
+    """Differentiable EncoderAttention.forward for fine_tune(True): the fused forward keeps the
+    trainable stages' activations, backward runs capmi's conv dgrad/wgrad + BN backward."""
+
+    @staticmethod
+    def forward(ctx, module, imgs, *params):
+        ctx.module = module
+        ctx.n = len(params)
+        return module.ft_forward(imgs)
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        m = ctx.module
+        plist = trainable_encoder_params(_ResNetView(m.resnet))
+        grads = {id(p): torch.empty_like(p) for p in plist if p.requires_grad}
+        m.ft_backward(dfeat.contiguous(), grads)
+        return (None, None) + tuple(grads.get(id(p)) for p in plist)
 
 
 class Encoder(nn.Module):
@@ -91,15 +121,38 @@ class EncoderAttention(nn.Module):
             param.requires_grad = False
         self._runner = EncoderRunner()
 
+    def _out_hw(self):
+        out_hw = self.adaptive_pool.output_size
+        return (out_hw, out_hw) if isinstance(out_hw, int) else tuple(out_hw)
+
     def forward(self, imgs):
         if not imgs.is_cuda:
             features = self.adaptive_pool(self.resnet(imgs))
             return features.permute(0, 2, 3, 1)
-        _check_frozen(self.resnet)
-        out_hw = self.adaptive_pool.output_size
-        out_hw = (out_hw, out_hw) if isinstance(out_hw, int) else tuple(out_hw)
-        return self._runner.forward(_ResNetView(self.resnet), imgs.contiguous(), out_hw,
+        if torch.is_grad_enabled() and _fine_tuned(self.resnet):
+            if not self.training:
+                raise NotImplementedError("capmi: fine-tuning runs BatchNorm in train mode (encoder.train())")
+            plist = trainable_encoder_params(_ResNetView(self.resnet))
+            return EncoderFineTuneFn.apply(self, imgs.contiguous(), *plist)
+        return self._runner.forward(_ResNetView(self.resnet), imgs.contiguous(), self._out_hw(),
                                     train=self.training)
+
+    # ---- fine-tune path (capmi's train step calls these directly) -------------------
+    def _ft(self):
+        ft = getattr(self, "_ft_runner", None)
+        if ft is None:
+            ft = FineTuneRunner(self._runner)
+            self._ft_runner = ft
+        return ft
+
+    def ft_forward(self, imgs, out=None):
+        """Train-mode forward that keeps layer2-4's activations for ft_backward."""
+        return self._ft().forward(_ResNetView(self.resnet), imgs.contiguous(), self._out_hw(), out=out)
+
+    def ft_backward(self, dfeat, grads, hook=None):
+        """d(loss)/d(features) (B,14,14,2048) -> parameter gradients of layer2-4 written into
+        ``grads`` (dict id(param) -> tensor)."""
+        self._ft().backward(dfeat, grads, hook=hook)
 
     def forward_into(self, imgs, out):
         """forward() writing the (B,14,14,2048) features into a caller-owned buffer (the

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 5
+#define CAPMI_ABI_VERSION 6
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -50,7 +50,11 @@ enum capmi_amode {
 };
 enum capmi_bmode {
   CAPMI_B_NMAJOR_W = 0, /* B[k][n] = W[n][k] (nn.Linear weight / packed conv weight), ldb = row stride of W */
-  CAPMI_B_KROWS = 1     /* B[k][n] row-major, ldb = row stride */
+  CAPMI_B_KROWS = 1,    /* B[k][n] row-major, ldb = row stride */
+  CAPMI_B_CONV_NHWC = 2 /* conv weight gradient: B[k][n] = implicit im2col of the NHWC input (conv geometry
+                           fields), k = output pixel (img, oh, ow), n = (kh, kw, ci); A must be CAPMI_A_MMAJOR
+                           (dY stored as [pixel][Cout]); C = dW[Cout][KH][KW][Cin]; in_scale/in_shift, when
+                           set, are the BN-apply+ReLU prologue of the conv's input (Cin % 4 == 0) */
 };
 /* tile: 128x128, 64x64, 128x64, or AUTO (chosen from the grid size; what the encoder uses) */
 enum capmi_tile { CAPMI_TILE_128 = 0, CAPMI_TILE_64 = 1, CAPMI_TILE_128x64 = 2, CAPMI_TILE_AUTO = 3 };
@@ -143,6 +147,41 @@ int capmi_adaptive_avgpool_nhwc(const float* in, int N, int H, int W, int C, int
                                 float* out, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Encoder fine-tune backward (EncoderAttention.fine_tune, models/encoder.py:112-121: layer2-4
+ * trainable; BASELINE config 4). Conv dgrad = capmi_gemm_sk over CAPMI_A_CONV_NHWC of dY (zero-
+ * upsampled first for stride 2) with the weights from capmi_conv_weight_pack_dgrad; conv wgrad =
+ * capmi_gemm_sk(CAPMI_A_MMAJOR, CAPMI_B_CONV_NHWC).
+ * ---------------------------------------------------------------------------------------- */
+/* out[ci][kh][kw][co] = w[co][ci][KH-1-kh][KW-1-kw] (B operand of the data-gradient conv) */
+int capmi_conv_weight_pack_dgrad(const float* w, int Cout, int Cin, int KH, int KW, float* out, void* stream);
+/* [Cout][KH][KW][Cin] (GEMM layout of a weight gradient) -> [Cout][Cin][KH][KW] (nn.Conv2d layout) */
+int capmi_conv_weight_unpack(const float* packed, int Cout, int Cin, int KH, int KW, float* out, void* stream);
+/* out (N,H,W,C) = dy (N,Ho,Wo,C) at even (h, w), zero elsewhere (stride-2 conv data gradient) */
+int capmi_zero_upsample2_nhwc(const float* dy, int N, int Ho, int Wo, int C, int H, int W, float* out,
+                              void* stream);
+/* BatchNorm2d(train) backward, rows x C NHWC. dz = d * relu mask:
+ *   CAPMI_BNB_RELU_Y   mask = [y*scale + shift > 0] (BN + ReLU inside a bottleneck),
+ *   CAPMI_BNB_RELU_OUT mask = [mask_src > 0]        (mask_src = saved relu(bn3 + residual) output).
+ * reduce: dbeta = sum dz, dgamma = sum dz*(y-mean)*invstd (written, or added when accumulate) and
+ * coef[4][C] for apply; work >= CAPMI_BNB_WORK_FLOATS(C) floats. invstd = rsqrt(save_var + eps),
+ * save_mean / save_var = the forward's batch statistics (capmi_bn_finalize outputs, biased var).
+ * apply: dy = gamma*invstd*(dz - dbeta/N - x^*dgamma/N); dz_out = dz when non-NULL. */
+#define CAPMI_BNB_RELU_Y 0
+#define CAPMI_BNB_RELU_OUT 1
+#define CAPMI_BNB_MAX_SLABS 256
+#define CAPMI_BNB_WORK_FLOATS(C) (2LL * CAPMI_BNB_MAX_SLABS * (C))
+int capmi_bn_bwd_reduce(int mode, const float* d, const float* y, const float* mask_src, const float* scale,
+                        const float* shift, const float* gamma, const float* save_mean, const float* save_var,
+                        float eps, long long rows, int C, float* dgamma, float* dbeta, int accumulate,
+                        float* coef, float* work, void* stream);
+int capmi_bn_bwd_apply(int mode, const float* d, const float* y, const float* mask_src, const float* scale,
+                       const float* shift, const float* coef, long long rows, int C, float* dy, float* dz_out,
+                       void* stream);
+/* AdaptiveAvgPool2d backward, NHWC: din (N,H,W,C) from dout (N,OH,OW,C) */
+int capmi_adaptive_avgpool_bwd_nhwc(const float* dout, int N, int H, int W, int C, int OH, int OW, float* din,
+                                    void* stream);
+
+/* ------------------------------------------------------------------------
  * Attention decoder (models/attention.py:43-61, 151-164, 218-284).
  * Per-step state is time-major: X[t][b][M+E], H[t][b][D], ...
  * ---------------------------------------------------------------------- */
@@ -205,10 +244,16 @@ int capmi_lstm_cell_bwd(const float* dhd, const float* dh_part, int S, long long
                         const float* c_cur, int B, int D, int bt, float* dgates, float* dc_out,
                         void* stream);
 /* d(awe_g) = sum_s part[s]; dawe = d*gate; dgp = d*awe*gate*(1-gate) (if gate != NULL)
- * dalpha[b][p] = dawe . enc[b][p][:] */
+ * dalpha[b][p] = dawe . enc[b][p][:]; dawe -> dawe_out[b][E] when non-NULL (encoder fine-tune) */
 int capmi_att_ctx_bwd(const float* part, int S, long long slab, const float* gate,
                       const float* awe, const float* enc, int B, int P, int E, float* dgp,
-                      float* dalpha, void* stream);
+                      float* dalpha, float* dawe_out, void* stream);
+/* gradient w.r.t. encoder_out (B,P,E) when the encoder is fine-tuned (models/encoder.py:112-121):
+ * the context sums (:59-60) and the init-state mean (:161) contribute
+ *   denc[b][p][e] = sum_t alpha[b*alpha_ld_b + t*P + p] * dawe[t][b][e] + dmean[b][e] / P
+ * (dmean may be NULL); the enc_att term (:54) is a GEMM added on top (beta = 1). */
+int capmi_att_enc_dinput(const float* alpha, long long alpha_ld_b, const float* dawe, const float* dmean,
+                         int B, int T, int P, int E, float* denc, void* stream);
 /* softmax backward with an extra dalpha term (dreg[b*dreg_ld_b + p], may be NULL: the alphas
  * output's own gradient) and the ReLU score backward:
  *   da = dalpha + dreg; de = alpha*(da - sum_p alpha*da); dad[b][a] = wf[a] sum_p de[p] [att_enc+ad > 0]

@@ -334,18 +334,151 @@ def encoder_wrapper_cases():
                    "ref": "models/encoder.py:72-110 around oracle/resnet_ref.py (parity unpinned for conv arithmetic)"})
 
 
+def decoder_denc_cases():
+    """d(loss)/d(encoder_out) through the reference decoder's own autograd (what flows into the
+    encoder when it is fine-tuned): AttentionDecoder.forward (models/attention.py:218-284) in
+    train mode (dropout p = 0), the loss of :401-414 (pack_padded CE + alpha regulariser)."""
+    import models.attention as RA
+    from torch.nn.utils.rnn import pack_padded_sequence
+    cases = {
+        # tag: (A, D, M, V, B, L, lengths, seed)
+        "small": (32, 32, 16, 50, 3, 7, [7, 5, 4], 35),
+        "prod": (512, 512, 512, 8100, 2, 25, None, 36),
+    }
+    for tag, (A, D, M, V, B, L, lengths, seed) in cases.items():
+        dec = RA.AttentionDecoder(torch.device("cpu"), _params(A, D, M, V))
+        _load(dec, gen.decoder_params(seed, A, D, M, V))
+        dec.train()
+        enc = _t(gen.encoder_features(seed, B)).requires_grad_()
+        caps = gen.captions(seed, B, L, V, lengths)
+        lens = list(lengths) if lengths else [L] * B
+        scores, caps_sorted, dl, alphas = dec(enc, _t(caps), lens)
+        targets = caps_sorted[:, 1:]
+        scores = pack_padded_sequence(scores, dl, batch_first=True).data
+        targets = pack_padded_sequence(targets, dl, batch_first=True).data
+        loss = torch.nn.CrossEntropyLoss()(scores, targets)
+        loss = loss + ((1.0 - alphas.sum(dim=1)) ** 2).mean()
+        loss.backward()
+        g = enc.grad.numpy()
+        out = {"captions": caps, "loss": np.array(loss.item())}
+        out.update(_samples("denc", g, 8192))
+        out["denc__absmax"] = np.array(np.abs(g).max())
+        _save(f"decoder_denc_{tag}", out,
+              {"A": A, "D": D, "M": M, "V": V, "B": B, "L": L, "lengths": lens, "seed": seed,
+               "ref": "models/attention.py:43-61,151-164,218-284 (autograd to encoder_out), :401-414"})
+
+
+def finetune_train_step_cases():
+    """One batch of the reference train() (models/attention.py:287-452) with
+    --fine_tune_encoder. Q9: the reference builds the encoder optimizer over
+    filter(requires_grad, encoder.parameters()) while every parameter is frozen and
+    fine_tune() is never called (ValueError: empty parameter list); the only patch here is
+    EncoderAttention.__init__ calling fine_tune(True) (models/encoder.py:112-121), i.e. what
+    BASELINE config 4 means. Everything else is the reference loop: encoder.train(),
+    decoder, CE + alpha reg, backward, clip_gradient on both optimizers, both Adam steps."""
+    import models.attention as RA
+    import models.encoder as RE
+    A, D, M, V, B, lengths, seed = 32, 32, 16, 50, 2, [6, 6], 45
+    _RESNET_SEED[0] = 1234 + seed
+    vocab = _vocab(V)
+    ds = _FakeCOCO(vocab, B, lengths, seed, V)
+    prm = gen.decoder_params(seed, A, D, M, V)
+    cap = {"clip": []}
+    orig = dict(init=RA.AttentionDecoder.__init__, fwd=RA.AttentionDecoder.forward,
+                einit=RE.EncoderAttention.__init__, efwd=RE.EncoderAttention.forward, clip=RA.clip_gradient,
+                adam=torch.optim.Adam)
+
+    def init(self, device, params, _o=orig["init"]):
+        _o(self, device, params)
+        _load(self, prm)
+        cap["decoder"] = self
+
+    def einit(self, _o=orig["einit"]):
+        _o(self)
+        self.fine_tune(True)  # Q9
+        cap["encoder"] = self
+
+    def fwd(self, enc, caps, lens, _o=orig["fwd"]):
+        cap["dec_in_enc"] = enc.detach().numpy().copy()
+        return _o(self, enc, caps, lens)
+
+    def clip(opt, c, _o=orig["clip"]):
+        cap["clip"].append({id(p): p.grad.detach().numpy().copy() for grp in opt.param_groups
+                            for p in grp["params"] if p.grad is not None})
+        _o(opt, c)
+
+    def save_ckpt(args, epoch, encoder, decoder, eo, do, metrics):
+        cap["post_enc"] = {k: v.detach().numpy().copy() for k, v in encoder.state_dict().items()}
+        cap["post_dec"] = {k: v.detach().numpy().copy() for k, v in decoder.state_dict().items()}
+        cap["loss"] = metrics["epoch_losses"][-1][-1]
+
+    def adam(params, lr, _o=orig["adam"]):
+        return _o(list(params), lr=lr)
+
+    RA.AttentionDecoder.__init__ = init
+    RA.AttentionDecoder.forward = fwd
+    RE.EncoderAttention.__init__ = einit
+    RA.EncoderAttention = RE.EncoderAttention
+    RA.clip_gradient = clip
+    RA.COCODataset = lambda mode, img_transform=None, caption_max_len=50: ds
+    RA.save_checkpoint = save_ckpt
+    RA.torch.optim.Adam = adam
+    args = types.SimpleNamespace(
+        attention_dim=A, decoder_dim=D, embed_size=M, decoder_dropout=0.0, epochs=1, batch_size=B, workers=0,
+        encoder_lr=1e-4, decoder_lr=1e-4, grad_clip=5.0, alpha_c=1.0, fine_tune_encoder=True,
+        fine_tune_embedding=False, checkpoint=None, print_freq=1, use_glove=False, max_caption_length=-1,
+        use_bert=False, model_name="golden_finetune")
+    torch.manual_seed(seed)
+    try:
+        RA.train(torch.device("cpu"), args)
+    finally:
+        RA.AttentionDecoder.__init__ = orig["init"]
+        RA.AttentionDecoder.forward = orig["fwd"]
+        RE.EncoderAttention.__init__ = orig["einit"]
+        RA.clip_gradient = orig["clip"]
+        RA.torch.optim.Adam = orig["adam"]
+    enc_named = dict(cap["encoder"].named_parameters())
+    dec_named = dict(cap["decoder"].named_parameters())
+    raw = {}
+    for d in cap["clip"]:
+        for nm, prm_ in list(enc_named.items()) + [("dec." + k, v) for k, v in dec_named.items()]:
+            if id(prm_) in d:
+                raw[nm] = d[id(prm_)]
+    out = {"order": np.array(ds.requested), "loss": np.array(cap["loss"])}
+    out.update(_samples("enc", cap["dec_in_enc"], 2048))
+    enc_grads = sorted(k for k in raw if not k.startswith("dec."))
+    for k in sorted(raw):
+        out.update(_samples("grad." + k, raw[k], 64))
+        out["gradnorm." + k] = np.array(np.linalg.norm(raw[k].astype(np.float64)))
+    for k, v in cap["post_enc"].items():
+        if v.size > 1 and (k in enc_named or "running" in k):
+            out.update(_samples("post_enc." + k, v, 64))
+    for k, v in cap["post_dec"].items():
+        out.update(_samples("post_dec." + k, v, 64))
+    _save("train_step_finetune", out,
+          {"A": A, "D": D, "M": M, "V": V, "B": B, "lengths": lengths, "seed": seed, "resnet_seed": 1234 + seed,
+           "enc_trainable": enc_grads, "n_enc_trainable": len(enc_grads),
+           "dec_trainable": sorted(k[4:] for k in raw if k.startswith("dec.")),
+           "ref": "models/attention.py:287-452 with --fine_tune_encoder (+ fine_tune(True), Q9), "
+                  "models/encoder.py:72-121, train_utils.py:2-12"})
+
+
+CASES = {"soft_attention": soft_attention_cases, "decoder_forward": decoder_forward_cases,
+         "baseline": baseline_cases, "train_step": train_step_cases, "encoder_wrapper": encoder_wrapper_cases,
+         "decoder_denc": decoder_denc_cases, "train_step_finetune": finetune_train_step_cases}
+
+
 def main():
+    """python make_golden.py [case ...]   (default: every case)"""
     _install_stubs()
     cwd = os.getcwd()
+    todo = sys.argv[1:] or list(CASES)
     with tempfile.TemporaryDirectory() as td:
         os.chdir(td)
         try:
             torch.set_num_threads(8)
-            soft_attention_cases()
-            decoder_forward_cases()
-            baseline_cases()
-            train_step_cases()
-            encoder_wrapper_cases()
+            for c in todo:
+                CASES[c]()
         finally:
             os.chdir(cwd)
 

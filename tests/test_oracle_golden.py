@@ -138,3 +138,43 @@ def test_encoder_wrapper(golden, case):
         y = encoder_attention_forward(net, t(x))
     assert list(y.shape) == list(fx["shape"])
     check_samples(fx, "features", y.numpy(), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("tag", ["small", "prod"])
+def test_decoder_denc(golden, tag):
+    """The oracle decoder's autograd to encoder_out vs the reference's (golden decoder_denc_*)."""
+    fx = golden(f"decoder_denc_{tag}")
+    m = fx["meta"]
+    p = {k: t(v) for k, v in gen.decoder_params(m["seed"], m["A"], m["D"], m["M"], m["V"]).items()}
+    enc = t(gen.encoder_features(m["seed"], m["B"])).requires_grad_()
+    preds, caps, dl, alphas = R.decoder_forward(p, enc, t(fx["captions"]), m["lengths"])
+    loss = R.attention_loss(preds, caps, dl, alphas)
+    loss.backward()
+    np.testing.assert_allclose(loss.item(), float(fx["loss"]), rtol=1e-6)
+    check_samples(fx, "denc", enc.grad.numpy(), rtol=1e-5, atol=1e-9)
+
+
+def test_finetune_train_step(golden):
+    """oracle/finetune_ref.py vs the reference's own train() with --fine_tune_encoder (Q9 patched)."""
+    from oracle.finetune_ref import finetune_train_step
+    fx = golden("train_step_finetune")
+    m = fx["meta"]
+    torch.set_num_threads(8)
+    order = fx["order"]
+    imgs = np.concatenate([gen.images(m["seed"], 1, name=f"img{i}") for i in order])
+    caps = np.concatenate([gen.captions(m["seed"] + 1000 + i, 1, m["lengths"][i], m["V"]) for i in order])
+    p = {k: t(v) for k, v in gen.decoder_params(m["seed"], m["A"], m["D"], m["M"], m["V"]).items()}
+    out = finetune_train_step(gen.resnet101_params(m["resnet_seed"]), p, set(m["dec_trainable"]), t(imgs),
+                              t(caps), [caps.shape[1]] * m["B"])
+    check_samples(fx, "enc", out["feats"].numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(out["loss"].item(), float(fx["loss"]), rtol=1e-5)
+    enc_names = ["resnet." + _resnet_child_key(n) for n in out["enc_raw"]]
+    assert sorted(enc_names) == m["enc_trainable"]
+    for n, g in out["enc_raw"].items():
+        key = "resnet." + _resnet_child_key(n)
+        gn = float(fx["gradnorm." + key])
+        check_samples(fx, "grad." + key, g.numpy(), rtol=1e-3, atol=1e-4 * gn / np.sqrt(g.numel()))
+        check_samples(fx, "post_enc." + key, out["enc_new"][n].numpy(), rtol=1e-5, atol=2e-6)
+    for k, g in out["dec_raw"].items():
+        check_samples(fx, "grad.dec." + k, g.numpy(), rtol=1e-3, atol=1e-6)
+        check_samples(fx, "post_dec." + k, out["dec_new"][k].numpy(), rtol=1e-5, atol=1e-6)
