@@ -34,6 +34,7 @@ for _p in (PKG, REPO):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 FP32_MFMA_PEAK_TF = 157.3   # MI355X fp32 matrix peak (MI355X_MICROARCH.md)
@@ -53,6 +54,9 @@ def parse():
                     help="no encoder/decoder pipelining: the whole step in one HIP graph (or --eager)")
     ap.add_argument("--eager", action="store_true",
                     help="with --sequential: launch every kernel from Python (no HIP graph)")
+    ap.add_argument("--config", default="attention", choices=["attention", "glove_finetune"],
+                    help="attention = BASELINE config 2/3 (frozen encoder, the headline); glove_finetune = "
+                         "config 4 (GloVe-300 fp64 embedding fine-tuned + encoder layer2-4 fine-tuned)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
@@ -133,6 +137,34 @@ def cpu_baseline(args, seconds):
                       f"clamp/Adam, L={L}, V={V}), torch CPU fp32, {threads} threads, {dt:.1f} s"}
 
 
+def cpu_baseline_finetune(args, seconds):
+    """Oracle fine-tune step (oracle/finetune_ref.py: ResNet-101 fwd+bwd of layer2-4, decoder
+    fwd/bwd with fp64 GloVe-300 embedding, clamp + two Adams) at B=2 on the host cores."""
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    import gen
+    from oracle.finetune_ref import finetune_train_step
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    B, L, V = 2, args.caption_len, args.vocab
+    rp = gen.resnet101_params(5)
+    p = {k: torch.from_numpy(v) for k, v in gen.decoder_params(5, 512, 512, 300, V, emb_dtype=np.float64).items()}
+    imgs = torch.from_numpy(gen.images(5, B))
+    caps = torch.from_numpy(gen.captions(5, B, L, V))
+    n, t0 = 0, None
+    while True:
+        finetune_train_step(rp, p, set(p), imgs, caps, [L] * B)
+        n += 1
+        if t0 is None:
+            t0, n = time.perf_counter(), 0
+        elif time.perf_counter() - t0 > seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(B * n / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} oracle fine-tune train steps at B={B} (ResNet-101 fwd + layer2-4 bwd, unhoisted "
+                      f"decoder fwd/bwd, fp64 GloVe-300 embedding, clamp/2x Adam, L={L}, V={V}), torch CPU fp32, "
+                      f"{threads} threads, {dt:.1f} s"}
+
+
 def main():
     args = parse()
     from capmi import dist as cdist
@@ -140,24 +172,36 @@ def main():
     dev = ctx.device
     from capmi.data import synthetic_batch
     from capmi.optim import Adam
-    from capmi.resnet import conv_flops_per_image
     from capmi.train_step import AttentionTrainStep
     from models.attention import AttentionDecoder, AttentionDecoderParams
     from models.encoder import EncoderAttention
     from vocabulary import synthetic_vocab
 
     torch.manual_seed(0)
+    ft = args.config == "glove_finetune"
     encoder = EncoderAttention().to(dev).train()
     prm = AttentionDecoderParams()
     prm.vocab = synthetic_vocab(args.vocab)
-    decoder = AttentionDecoder(dev, prm).to(dev).train()
-    decoder.fine_tune_embeddings(False)  # reference default (--fine_tune_embedding False, Q8)
+    prm.embed_size = 300 if ft else 512
+    decoder = AttentionDecoder(dev, prm)
+    if ft:
+        # synthetic GloVe-300 table, fp64 like load_glove_vectors (embed.py:64-68, Q7)
+        g = torch.Generator().manual_seed(300)
+        decoder.load_pretrained_embeddins((torch.rand(args.vocab, 300, generator=g, dtype=torch.float64) - 0.5))
+    decoder = decoder.to(dev).train()
+    decoder.fine_tune_embeddings(ft)  # glove_att: --fine_tune_embedding True (Makefile:13); else Q8 default
     cdist.broadcast_module(decoder, ctx)
     opt = Adam(filter(lambda q: q.requires_grad, decoder.parameters()), lr=1e-4)
     opt.set_clip(5.0)
-    pipe = not args.sequential
+    enc_opt = None
+    if ft:
+        encoder.fine_tune(True)
+        cdist.broadcast_module(encoder, ctx)
+        enc_opt = Adam(filter(lambda q: q.requires_grad, encoder.parameters()), lr=1e-4)
+        enc_opt.set_clip(5.0)
+    pipe = not args.sequential and not ft
     step = AttentionTrainStep(encoder, decoder, opt, ctx, alpha_c=1.0, graph=not (args.eager or pipe),
-                              seed=77 + ctx.rank, pipeline=pipe)
+                              seed=77 + ctx.rank, pipeline=pipe, encoder_optimizer=enc_opt)
     timer = ConvTimer()
     encoder._runner.conv_hook = None if args.no_roofline else timer
     B = args.batch
@@ -192,7 +236,12 @@ def main():
         timer.enabled = True
         with torch.no_grad():
             for _ in range(args.steps):
-                encoder(imgs)
+                if ft:  # fine-tune: the forward and the layer2-4 backward GEMMs
+                    f = encoder.ft_forward(imgs)
+                    encoder.ft_backward(torch.ones_like(f) * 1e-4, {id(q): q.grad for q in enc_opt.param_groups[0]["params"]},
+                                        hook=timer)
+                else:
+                    encoder(imgs)
         torch.cuda.synchronize()
         timer.enabled = False
 
@@ -207,7 +256,7 @@ def main():
         ach = flops / (ms * 1e-3) / 1e12
         fam_flops = sum(v[1] for v in per.values())
         fam_ms = sum(v[2] for v in per.values())
-        per_img = conv_flops_per_image(_view(encoder))
+        per_img = sum(v[1] for v in per.values()) / args.steps / B
         roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
                 "frac": round(ach / FP32_MFMA_PEAK_TF, 4), "traffic": _traffic(key),
                 "kernel": key,
@@ -224,7 +273,7 @@ def main():
                     f"{args.steps} eager encoder forwards after the timed graph replays")}
     cpu = None
     if ctx.rank == 0 and N == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, args.cpu_seconds)
+        cpu = (cpu_baseline_finetune if ft else cpu_baseline)(args, args.cpu_seconds)
     if ctx.rank == 0:
         line = {
             "metric": "training images/sec (whole node), 'attention' decoder, at 1/2/4/8 MI355X",
@@ -232,10 +281,13 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (resident in HBM; random-init weights, torch.manual_seed(0))",
-            "config": {"workload": "'attention' decoder + frozen ResNet-101 encoder (BN train mode), "
-                                   "one training step per batch", "per_gpu_batch": B, "global_batch": B * N,
+            "config": {"workload": ("'glove_att' decoder (GloVe-300 fp64 embedding, fine-tuned) + ResNet-101 "
+                                    "encoder fine-tuned (layer2-4, BN train mode), one training step per batch")
+                       if ft else ("'attention' decoder + frozen ResNet-101 encoder (BN train mode), "
+                                   "one training step per batch"),
+                       "per_gpu_batch": B, "global_batch": B * N,
                        "caption_len": args.caption_len, "decode_steps": args.caption_len - 1,
-                       "vocab": args.vocab, "attention_dim": 512, "decoder_dim": 512, "embed_size": 512,
+                       "vocab": args.vocab, "attention_dim": 512, "decoder_dim": 512, "embed_size": 300 if ft else 512,
                        "parallelism": f"dp{N}"},
             "loss_last_step": round(loss_v, 5),
             "launch": "pipelined_2stream_eager" if pipe else ("eager" if args.eager else "hip_graph"),
@@ -243,11 +295,6 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-
-
-def _view(enc):
-    from models.encoder import _ResNetView
-    return _ResNetView(enc.resnet)
 
 
 if __name__ == "__main__":

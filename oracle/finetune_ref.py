@@ -55,9 +55,10 @@ def finetune_train_step(resnet_params, dec_params, dec_trainable, imgs, captions
                 dec_new=dec_new, net=net)
 
 
-def encoder_backward(resnet_params, imgs, dfeat, dtype=torch.float64):
-    """Encoder-only: features and d(<features, dfeat>)/d(layer2-4 params) by autograd."""
-    net = build_resnet101(resnet_params).to(dtype)
+def encoder_backward(resnet_params, imgs, dfeat, dtype=torch.float64, layers=(3, 4, 23, 3)):
+    """Encoder-only: features and d(<features, dfeat>)/d(layer2-4 params) by autograd
+    (``layers``: blocks per stage; shallower stacks are better conditioned in train-mode BN)."""
+    net = build_resnet101(resnet_params, layers).to(dtype)
     net.train()
     names = trainable_names(net)
     for n, q in net.named_parameters():
