@@ -54,9 +54,10 @@ def parse():
                     help="no encoder/decoder pipelining: the whole step in one HIP graph (or --eager)")
     ap.add_argument("--eager", action="store_true",
                     help="with --sequential: launch every kernel from Python (no HIP graph)")
-    ap.add_argument("--config", default="attention", choices=["attention", "glove_finetune"],
+    ap.add_argument("--config", default="attention", choices=["attention", "glove_finetune", "bert_attention"],
                     help="attention = BASELINE config 2/3 (frozen encoder, the headline); glove_finetune = "
-                         "config 4 (GloVe-300 fp64 embedding fine-tuned + encoder layer2-4 fine-tuned)")
+                         "config 4 (GloVe-300 fp64 embedding fine-tuned + encoder layer2-4 fine-tuned); "
+                         "bert_attention = config 5 (768-d word features instead of the table, synthetic)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
@@ -114,16 +115,22 @@ def cpu_baseline(args, seconds):
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     B, L, V = 2, args.caption_len, args.vocab
+    bert = args.config == "bert_attention"
+    M = 768 if bert else 512
     net = build_resnet101(gen.resnet101_params(5)).train()
-    p = {k: torch.from_numpy(v) for k, v in gen.decoder_params(5, 512, 512, 512, V).items()}
+    p = {k: torch.from_numpy(v) for k, v in gen.decoder_params(5, 512, 512, M, V).items()}
     trainable = set(k for k in p if k != "embedding.weight")
     imgs = torch.from_numpy(gen.images(5, B))
     caps = torch.from_numpy(gen.captions(5, B, L, V))
+    emb = None
+    if bert:
+        from capmi.data import SyntheticBertEmbedder
+        emb = SyntheticBertEmbedder(V, 768)(caps)
     state, n, t0 = {}, 0, None
     while True:
         with torch.no_grad():
             feats = encoder_attention_forward(net, imgs)
-        out = R.train_step(p, trainable, feats, caps, [L] * B, state=state)
+        out = R.train_step(p, trainable, feats, caps, [L] * B, state=state, embeddings=emb)
         p.update(out[5])
         state = out[6]
         n += 1
@@ -134,7 +141,7 @@ def cpu_baseline(args, seconds):
     dt = time.perf_counter() - t0
     return {"value": round(B * n / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"{n} oracle train steps at B={B} (ResNet-101 fwd + unhoisted decoder fwd/bwd + "
-                      f"clamp/Adam, L={L}, V={V}), torch CPU fp32, {threads} threads, {dt:.1f} s"}
+                      f"clamp/Adam, L={L}, V={V}, M={M}), torch CPU fp32, {threads} threads, {dt:.1f} s"}
 
 
 def cpu_baseline_finetune(args, seconds):
@@ -179,17 +186,23 @@ def main():
 
     torch.manual_seed(0)
     ft = args.config == "glove_finetune"
+    bert = args.config == "bert_attention"
     encoder = EncoderAttention().to(dev).train()
     prm = AttentionDecoderParams()
     prm.vocab = synthetic_vocab(args.vocab)
-    prm.embed_size = 300 if ft else 512
+    prm.embed_size = 300 if ft else (768 if bert else 512)
+    prm.use_bert = bert
     decoder = AttentionDecoder(dev, prm)
+    if bert:
+        from capmi.data import SyntheticBertEmbedder
+        decoder.bert_embedder = SyntheticBertEmbedder(args.vocab, 768, device=dev)
     if ft:
         # synthetic GloVe-300 table, fp64 like load_glove_vectors (embed.py:64-68, Q7)
         g = torch.Generator().manual_seed(300)
         decoder.load_pretrained_embeddins((torch.rand(args.vocab, 300, generator=g, dtype=torch.float64) - 0.5))
     decoder = decoder.to(dev).train()
-    decoder.fine_tune_embeddings(ft)  # glove_att: --fine_tune_embedding True (Makefile:13); else Q8 default
+    # glove_att: --fine_tune_embedding True (Makefile:13); bert: the table is unused; else Q8 default
+    decoder.fine_tune_embeddings(ft)
     cdist.broadcast_module(decoder, ctx)
     opt = Adam(filter(lambda q: q.requires_grad, decoder.parameters()), lr=1e-4)
     opt.set_clip(5.0)
@@ -283,11 +296,13 @@ def main():
             "data": "synthetic (resident in HBM; random-init weights, torch.manual_seed(0))",
             "config": {"workload": ("'glove_att' decoder (GloVe-300 fp64 embedding, fine-tuned) + ResNet-101 "
                                     "encoder fine-tuned (layer2-4, BN train mode), one training step per batch")
-                       if ft else ("'attention' decoder + frozen ResNet-101 encoder (BN train mode), "
-                                   "one training step per batch"),
+                       if ft else ("'bert_attention' decoder (768-d synthetic BERT word features) + frozen "
+                                   "ResNet-101 encoder (BN train mode), one training step per batch") if bert else
+                       ("'attention' decoder + frozen ResNet-101 encoder (BN train mode), "
+                        "one training step per batch"),
                        "per_gpu_batch": B, "global_batch": B * N,
                        "caption_len": args.caption_len, "decode_steps": args.caption_len - 1,
-                       "vocab": args.vocab, "attention_dim": 512, "decoder_dim": 512, "embed_size": 300 if ft else 512,
+                       "vocab": args.vocab, "attention_dim": 512, "decoder_dim": 512, "embed_size": prm.embed_size,
                        "parallelism": f"dp{N}"},
             "loss_last_step": round(loss_v, 5),
             "launch": "pipelined_2stream_eager" if pipe else ("eager" if args.eager else "hip_graph"),

@@ -70,6 +70,7 @@ _SIGS = {
     "capmi_bn_bwd_apply": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_vp, c_vp, c_vp],
     "capmi_adaptive_avgpool_bwd_nhwc": [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_embed_gather": [c_vp, c_int, c_int, c_vp, c_int, c_int, c_int, c_vp, c_ll, c_vp],
+    "capmi_embed_dense": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_ll, c_vp],
     "capmi_mean_rows": [c_vp, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_att_score_fwd": [c_vp, c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp,
                             c_vp, c_vp],

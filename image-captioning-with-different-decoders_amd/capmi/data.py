@@ -58,3 +58,24 @@ class SyntheticCOCO(torch.utils.data.Dataset):
         cap[0] = self.V - 3
         cap[-1] = self.V - 2
         return img, cap
+
+
+class SyntheticBertEmbedder:
+    """Stand-in for the reference's BERT features (models/attention.py:166-215): bert-base-uncased
+    cannot be fetched offline, so the (B, L+1, 768) word-level features are a seeded per-token
+    vector plus a per-position vector, with a fixed [CLS] row prepended (:170 prepends '[CLS] ').
+    Deterministic for a given caption; frozen (no gradient), as the reference's no_grad BERT."""
+
+    def __init__(self, V, dim=768, max_len=64, seed=768, device="cpu", scale=0.5):
+        g = torch.Generator().manual_seed(seed)
+        self.tok = ((torch.rand(V, dim, generator=g) - 0.5) * 2 * scale).to(device)
+        self.pos = ((torch.rand(max_len + 1, dim, generator=g) - 0.5) * 2 * scale * 0.2).to(device)
+        self.cls = ((torch.rand(dim, generator=g) - 0.5) * 2 * scale).to(device)
+
+    def __call__(self, encoded_captions):
+        caps = encoded_captions.to(self.tok.device)
+        B, L = caps.shape
+        out = torch.empty(B, L + 1, self.tok.shape[1], device=self.tok.device, dtype=torch.float32)
+        out[:, 0] = self.cls
+        out[:, 1:] = self.tok[caps] + self.pos[1:L + 1]
+        return out

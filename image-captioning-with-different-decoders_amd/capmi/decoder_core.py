@@ -135,15 +135,17 @@ class DecoderCore:
 
     # ------------------------------------------------------------------ forward
     def forward(self, p, enc, caps, decode_lengths, *, dropout_p=0.0, training=False, seed=0,
-                seed_dev=None):
+                seed_dev=None, emb_dense=None):
         """p: dict name->tensor (PNAMES). enc: (B,P,E) contiguous fp32. caps: (B,L) int64.
+        emb_dense: optional (B, Le, M) fp32 word embeddings used instead of the embedding table
+        (the BERT variant, :242-244; frozen: no gradient flows into it).
         Returns (predictions (B,T,V), alphas (B,T,P), state)."""
         B, P, E = enc.shape
         L = caps.shape[1]
         T = max(decode_lengths)
         A = p["attention.enc_att.weight"].shape[0]
         D = p["decode_step.weight_hh"].shape[1]
-        M = p["embedding.weight"].shape[1]
+        M = p["embedding.weight"].shape[1] if emb_dense is None else emb_dense.shape[2]
         V = p["fc.weight"].shape[0]
         dm = DecoderDims(B, T, L, P, A, D, M, V, E)
         ws = self.workspace(dm, enc.device)
@@ -154,7 +156,12 @@ class DecoderCore:
 
         W_ih = p["decode_step.weight_ih"]
         # embeddings of the caption tokens -> X[:, :, :M]      (:247, :273)
-        K.embed_gather(p["embedding.weight"], caps, B, L, T, ws.X, X)
+        if emb_dense is None:
+            K.embed_gather(p["embedding.weight"], caps, B, L, T, ws.X, X)
+        else:
+            if emb_dense.shape[0] != B or emb_dense.shape[1] < T:
+                raise ValueError(f"dense embeddings {tuple(emb_dense.shape)} do not cover (B={B}, T={T})")
+            K.embed_dense(emb_dense, T, ws.X, X)
         # init_hidden_state (:151-164)
         K.mean_rows(enc, B, P, E, ws.mean)
         sh = min(8, max(1, E // 256))
@@ -205,6 +212,7 @@ class DecoderCore:
         if ragged:
             K.mask_rows_tb(preds, bt_dev, T, B, V, T * V, B, V)
         state = dict(dm=dm, ws=ws, enc=enc, caps=caps, bt=bt, bt_dev=bt_dev, ragged=ragged, alphas=alphas,
+                     dense_emb=emb_dense is not None,
                      Hd=Hd, dropout_p=dropout_p if training else 0.0, seed=seed, seed_dev=seed_dev)
         return preds, alphas, state
 
@@ -326,7 +334,7 @@ class DecoderCore:
             self._gemm_into(ws, denc, E, B * P, E, A, ws.DATT, A, p["attention.enc_att.weight"], E, AK, BKR,
                             beta=1.0)
         # embedding (only when fine-tuned, Q8): dX_emb = DG W_ih[:, :M] -> scatter-add by token
-        if "embedding.weight" in need:
+        if "embedding.weight" in need and not st["dense_emb"]:
             demb = grads["embedding.weight"]
             demb.zero_()
             dxe = ws.scratch[:TB * M].view(TB, M)

@@ -40,6 +40,18 @@ def _prep_inputs(dec, encoder_out, encoded_captions):
     return enc, caps
 
 
+def dense_embeddings(dec, caps):
+    """The BERT variant (use_bert, models/attention.py:166-215,242-244): (B, L+1, 768) word-level
+    features from the decoder's ``bert_embedder`` (frozen, computed without grad), else None."""
+    if not getattr(dec, "use_bert", False):
+        return None
+    with torch.no_grad():
+        e = dec.bert_embeddings(caps)
+    if e.dtype != torch.float32 or not e.is_cuda:
+        raise TypeError("BERT embeddings must be float32 device tensors")
+    return e.contiguous()
+
+
 def _seed():
     return int(torch.randint(0, 2 ** 62, (1,)).item())
 
@@ -51,7 +63,8 @@ class AttentionDecoderFn(torch.autograd.Function):
         p["attention.full_att.weight"] = p["attention.full_att.weight"].view(-1)
         drop = dec.dropout.p if dec.training else 0.0
         preds, alphas, st = CORE.forward(p, enc, caps, decode_lengths, dropout_p=drop,
-                                         training=dec.training, seed=_seed() if drop > 0 else 0)
+                                         training=dec.training, seed=_seed() if drop > 0 else 0,
+                                         emb_dense=dense_embeddings(dec, caps))
         _GEN[0] += 1
         st["gen"] = _GEN[0]
         ctx.st, ctx.p = st, p
@@ -65,7 +78,9 @@ class AttentionDecoderFn(torch.autograd.Function):
         if st["gen"] != _GEN[0]:
             raise RuntimeError("capmi decoder: another forward of the same shape ran before this "
                                "backward and overwrote its saved per-step state")
-        grads = {n: torch.empty_like(ctx.p[n]) for n in ctx.need}
+        # the BERT variant's embeddings are frozen features: the (unused) table gets no gradient
+        grads = {n: torch.empty_like(ctx.p[n]) for n in ctx.need
+                 if not (st["dense_emb"] and n == "embedding.weight")}
         if dpred is None:
             dpred = torch.zeros(st["dm"].B, st["dm"].T, st["dm"].V, device=st["enc"].device)
         denc = torch.empty_like(st["enc"]) if ctx.enc_grad else None
@@ -125,7 +140,7 @@ def fused_loss_and_grads(dec, encoder_out, captions, caption_lengths, alpha_c, g
     drop = dec.dropout.p if dec.training else 0.0
     host_seed = 0x5EED if seed_dev is not None else (_seed() if drop > 0 else 0)
     preds, alphas, st = CORE.forward(p, enc, caps, decode_lengths, dropout_p=drop, training=dec.training,
-                                     seed=host_seed, seed_dev=seed_dev)
+                                     seed=host_seed, seed_dev=seed_dev, emb_dense=dense_embeddings(dec, caps))
     _GEN[0] += 1
     dm = st["dm"]
     B, T, V, P, L = dm.B, dm.T, dm.V, dm.P, dm.L
@@ -136,7 +151,8 @@ def fused_loss_and_grads(dec, encoder_out, captions, caption_lengths, alpha_c, g
                  dl_time_major=True)
     K.alpha_reg(alphas, B, T, P, alpha_c, fs.reg, fs.dreg)
     K.loss_finalize(fs.loss_rows, B * T, nrows, fs.reg, fs.loss)
-    g = {n: grads[n] for n in (need if need is not None else grads)}
+    g = {n: grads[n] for n in (need if need is not None else grads)
+         if not (st["dense_emb"] and n == "embedding.weight")}
     if "attention.full_att.weight" in g:
         g["attention.full_att.weight"] = g["attention.full_att.weight"].view(-1)
     CORE.backward(p, st, g, fs.dlogits, dpred_time_major=True, dreg=fs.dreg,

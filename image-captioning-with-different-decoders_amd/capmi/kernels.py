@@ -238,6 +238,14 @@ def embed_gather(emb, caps, B, L, T, out, ld_out):
          T, ptr(out), ld_out, stream())
 
 
+def embed_dense(emb, T, out, ld_out):
+    """emb (B, Le, M) fp32 contiguous -> out[t][b][0:M], t < T"""
+    _cuda(emb, out)
+    B, Le, M = emb.shape
+    assert emb.is_contiguous()
+    call("capmi_embed_dense", ptr(emb), B, Le, M, T, ptr(out), ld_out, stream())
+
+
 def mean_rows(enc, B, P, E, out):
     _cuda(enc, out)
     call("capmi_mean_rows", ptr(enc), B, P, E, ptr(out), stream())

@@ -41,6 +41,32 @@ extern "C" int capmi_embed_gather(const void* emb, int emb_is_f64, int M, const 
   return 0;
 }
 
+// dense (precomputed) word embeddings, e.g. BERT layer-11 features (models/attention.py:166-215,242-244):
+// out[t][b][0:M] = emb[b][t][0:M], float4 per thread
+__global__ void embed_dense_kernel(const float4* __restrict__ emb, int B, int Le, int M4, int T,
+                                   float* __restrict__ out, long long ld_out) {
+  const long long n = (long long)T * B * M4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int m = (int)(i % M4);
+    const long long tb = i / M4;
+    const int b = (int)(tb % B), t = (int)(tb / B);
+    *reinterpret_cast<float4*>(out + tb * ld_out + 4 * m) = emb[((long long)b * Le + t) * M4 + m];
+  }
+}
+
+extern "C" int capmi_embed_dense(const float* emb, int B, int Le, int M, int T, float* out, long long ld_out,
+                                 void* stream) {
+  CAPMI_REQUIRE(emb && out && M > 0 && B > 0 && T >= 0 && T <= Le, CAPMI_EINVAL);
+  CAPMI_REQUIRE(M % 4 == 0 && ld_out % 4 == 0 && aligned16(emb) && aligned16(out), CAPMI_EALIGN);
+  const long long n = (long long)T * B * (M / 4);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(embed_dense_kernel, dim3(std::min<long long>(cdiv(n, 256), 4096)), dim3(256), 0,
+                     as_stream(stream), reinterpret_cast<const float4*>(emb), B, Le, M / 4, T, out, ld_out);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
 // --------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) mean_rows_kernel(const float* __restrict__ enc, int B, int P,
                                                         int E, float* __restrict__ out) {

@@ -62,9 +62,11 @@ class AttentionDecoder(nn.Module):
         self.vocab_size = len(self.vocab)
         self.dropout = params.dropout
         self.use_bert = params.use_bert
-        if self.use_bert:
-            # reference :96-100 fetches bert-base-uncased by name (network); not available offline
-            raise NotImplementedError("BERT embeddings need bert-base-uncased (not available offline)")
+        # reference :96-100 loads bert-base-uncased by name (a network fetch, unavailable offline).
+        # The BERT variant is kept as its interface: ``bert_embedder(encoded_captions)`` returns
+        # the (B, L+1, 768) word-level layer-11 features that _create_bert_embeddings (:166-215)
+        # builds; plug in a local BERT, or capmi.data.SyntheticBertEmbedder for benchmarks.
+        self.bert_embedder = None
 
         self.attention = SoftAttention(self.encoder_dim, self.decoder_dim, self.attention_dim)
         self.dropout = nn.Dropout(p=self.dropout)
@@ -89,6 +91,13 @@ class AttentionDecoder(nn.Module):
     def fine_tune_embeddings(self, on=True):
         for param in self.embedding.parameters():
             param.requires_grad = on
+
+    def bert_embeddings(self, encoded_captions):
+        """Reference _create_bert_embeddings (:166-215): (B, L) tokens -> (B, L+1, 768) features."""
+        if self.bert_embedder is None:
+            raise RuntimeError("use_bert=True needs decoder.bert_embedder (bert-base-uncased cannot be "
+                               "fetched offline; see capmi.data.SyntheticBertEmbedder)")
+        return self.bert_embedder(encoded_captions)
 
     def init_hidden_state(self, encoder_out):
         """(B,P,E) -> h, c (B,D) (reference :151-164)."""

@@ -188,6 +188,9 @@ int capmi_adaptive_avgpool_bwd_nhwc(const float* dout, int N, int H, int W, int 
 /* out[t][b][0:M] (row stride ld_out) = emb[caps[b*L + t]] for t < T; emb fp32 or fp64 (emb_is_f64) */
 int capmi_embed_gather(const void* emb, int emb_is_f64, int M, const long long* caps, int B, int L,
                        int T, float* out, long long ld_out, void* stream);
+/* dense word embeddings (the BERT variant's per-caption features, :166-215,242-244; no gather):
+ * out[t][b][0:M] (row stride ld_out) = emb[b][t][0:M] for t < T, emb (B, Le, M) fp32, M % 4 == 0 */
+int capmi_embed_dense(const float* emb, int B, int Le, int M, int T, float* out, long long ld_out, void* stream);
 /* out[b][e] = mean_p enc[b][p][e]  (encoder_out.mean(dim=1), :161) */
 int capmi_mean_rows(const float* enc, int B, int P, int E, float* out, void* stream);
 /* Soft-attention score (:54-58 without the softmax): ad = sum_s dec_part[s][b][:] + bias_da;

@@ -45,8 +45,9 @@ def lstm_cell(x, h, c, p):
 
 
 def decoder_forward(p, encoder_out, encoded_captions, caption_lengths, dropout_p=0.0,
-                    dropout_masks=None):
-    """models/attention.py:218-284 (regular-embedding branch, :247).
+                    dropout_masks=None, embeddings=None):
+    """models/attention.py:218-284 (regular-embedding branch, :247; ``embeddings`` (B, L', M)
+    given = the BERT branch, :242-244, which uses precomputed features instead of the table).
 
     ``dropout_masks`` (optional, (T,B,D) of 0/1/(1-p) scale) replaces the
     reference's RNG-driven nn.Dropout so a GPU run's mask can be replayed."""
@@ -56,8 +57,8 @@ def decoder_forward(p, encoder_out, encoded_captions, caption_lengths, dropout_p
     P = enc.size(1)
     decode_lengths = [l - 1 for l in caption_lengths]                      # :236-237
     T = max(decode_lengths)
-    emb_w = p["embedding.weight"]
-    embeddings = F.embedding(encoded_captions, emb_w)                      # :247
+    if embeddings is None:
+        embeddings = F.embedding(encoded_captions, p["embedding.weight"])  # :247
     h, c = init_hidden_state(p, enc)                                       # :250
     V = p["fc.weight"].shape[0]
     wdt = p["decode_step.weight_ih"].dtype  # fp32 as in the reference; fp64 only for diagnostics
@@ -117,14 +118,14 @@ def adam_step(params, grads, state, lr=1e-4, betas=(0.9, 0.999), eps=1e-8):
 
 
 def train_step(p, trainable, encoder_out, captions, caption_lengths, alpha_c=1.0,
-               grad_clip=5.0, lr=1e-4, state=None, dropout_masks=None):
+               grad_clip=5.0, lr=1e-4, state=None, dropout_masks=None, embeddings=None):
     """One decoder step of models/attention.py:386-430 (dropout off unless
     masks are given). ``p``: dict of float tensors; ``trainable``: names that
     require grad (the reference's filter(requires_grad), :352-355).
     Returns (loss, predictions, alphas, grads(clamped), new_params, state)."""
     leaves = {k: (v.detach().clone().requires_grad_(k in trainable)) for k, v in p.items()}
     preds, caps, dl, alphas = decoder_forward(leaves, encoder_out, captions, caption_lengths,
-                                              dropout_masks=dropout_masks)
+                                              dropout_masks=dropout_masks, embeddings=embeddings)
     loss = attention_loss(preds, caps, dl, alphas, alpha_c)
     loss.backward()
     raw = {k: leaves[k].grad.detach().clone() for k in trainable}
