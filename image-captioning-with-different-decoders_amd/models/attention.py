@@ -251,10 +251,64 @@ def train(device, args):
         print(f'Model {args.model_name} finished training for {args.epochs} epochs.')
 
 
-def evaluate(device, args, encoder, decoder):
-    """Reference :454-567 (teacher-forced validation + caption metrics): evaluation is
-    outside the training hot path this round builds."""
-    raise NotImplementedError("evaluation / caption scoring is not part of the training path")
+def evaluate(device, args, encoder, decoder, val_loader=None):
+    """Reference :454-567: one teacher-forced pass over the validation set (batch 1 in the
+    reference), loss = CE over the packed rows + ((1 - sum_t alpha)^2).mean(), greedy argmax
+    hypotheses and the START/END/PAD-stripped references, then caption scores.
+
+    The forward runs on the capmi kernels (no grad). ``val_loader`` defaults to the reference's
+    COCO 'val' loader (needs the dataset); caption scoring (metric.get_eval_score -> the
+    reference's eval_func BLEU/METEOR/ROUGE/CIDEr) is attempted and skipped when unavailable:
+    the returned dict then holds the losses, references and hypotheses."""
+    from torch.nn.utils.rnn import pack_padded_sequence
+    from metric import get_eval_score
+    from vocabulary import END_TOKEN, START_TOKEN
+    if val_loader is None:
+        from dataset import COCODataset  # real COCO path (pycocotools, nltk, images)
+        dataset = COCODataset(mode='val', caption_max_len=args.max_caption_length)
+        pad_idx = dataset.vocab(PAD_TOKEN)
+
+        def collate_fn(data):
+            from torch.nn.utils.rnn import pad_sequence
+            imgs, captions = list(zip(*data))[:2]
+            captions = pad_sequence(captions, batch_first=True, padding_value=pad_idx)
+            return torch.stack(imgs, dim=0), captions, [len(c) for c in captions]
+        val_loader = torch.utils.data.DataLoader(dataset=dataset, batch_size=1, shuffle=True,
+                                                 num_workers=1, collate_fn=collate_fn)
+    vocab = decoder.vocab
+    drop = {vocab(START_TOKEN), vocab(END_TOKEN), vocab(PAD_TOKEN)}
+    references, hypotheses, losses = [], [], []
+    accum_loss = AccumulatingMetric()
+    decoder.eval()
+    encoder.eval()
+    num_batches = len(val_loader)
+    start_time = time.time()
+    with torch.no_grad():
+        for batch_idx, (imgs, captions, caption_lengths) in enumerate(val_loader):
+            imgs = imgs.to(device)
+            captions = captions.to(device)
+            scores, caps_sorted, decode_lengths, alphas = decoder(encoder(imgs), captions, caption_lengths)
+            targets = caps_sorted[:, 1:]
+            sp = pack_padded_sequence(scores, decode_lengths, batch_first=True).data
+            tp = pack_padded_sequence(targets, decode_lengths, batch_first=True).data
+            loss = nn.functional.cross_entropy(sp, tp) + ((1. - alphas.sum(dim=1)) ** 2).mean()
+            accum_loss.update(loss.item(), sum(decode_lengths))
+            losses.append(loss.item())
+            for j in range(targets.shape[0]):
+                ref = [w for w in targets[j].tolist() if w not in drop]
+                references.append([ref for _ in targets[j].tolist()])  # reference :527-528
+            preds = torch.max(scores, dim=2)[1].tolist()
+            hypotheses.extend([[w for w in p[:decode_lengths[j]] if w not in drop] for j, p in enumerate(preds)])
+            if batch_idx % args.print_freq == 0:
+                print(f'Batch {batch_idx+1}/{num_batches}, Loss {accum_loss.avg():.4f}')
+    try:
+        metrics = get_eval_score(references, hypotheses)
+    except (NotImplementedError, ImportError):
+        metrics = {"references": references, "hypotheses": hypotheses}
+    metrics['losses'] = losses
+    print(f'Checkpoint {getattr(args, "checkpoint", None)} finished evaluation in '
+          f'{time.time() - start_time:.4f} seconds.')
+    return metrics
 
 
 __all__ = ["SoftAttention", "AttentionDecoderParams", "AttentionDecoder", "train", "evaluate"]

@@ -463,9 +463,42 @@ def finetune_train_step_cases():
                   "models/encoder.py:72-121, train_utils.py:2-12"})
 
 
+def beam_search_cases():
+    """The reference's own beam search (gen_captions.py:16-131) on seeded weights. fc.weight is
+    scaled (fc_scale) and fc.bias of <end> raised (end_bias) so that some beams finish early and
+    others run to the 50-step cap, exercising the finished-beam bookkeeping over many steps;
+    'noend' never finishes (the failure return)."""
+    _stub("imageio")
+    import gen_captions as RG
+    import models.attention as RA
+    for tag, (A, D, M, V, k, fc_scale, end_bias, seed) in {
+        "small": (32, 32, 16, 50, 3, 10.0, 1.0, 61),
+        "k5": (64, 48, 32, 120, 5, 10.0, 3.0, 62),
+        "noend": (32, 32, 16, 50, 2, 1.0, -50.0, 63),
+    }.items():
+        vocab = _vocab(V)
+        dec = RA.AttentionDecoder(torch.device("cpu"), _params(A, D, M, V))
+        prm = gen.decoder_params(seed, A, D, M, V)
+        prm["fc.weight"] = prm["fc.weight"] * np.float32(fc_scale)
+        prm["fc.bias"] = prm["fc.bias"].copy()
+        prm["fc.bias"][vocab("<end>")] += end_bias
+        _load(dec, prm)
+        dec.eval()
+        feats = _t(gen.encoder_features(seed, 1)).view(1, 14, 14, 2048)
+        args = types.SimpleNamespace(beam_size=k)
+        seq, alphas, ok = RG.attention_caption_image_beam_search(torch.device("cpu"), args, None,
+                                                                lambda img: feats, dec, vocab)
+        _save(f"beam_search_{tag}", {"seq": np.array(seq), "alphas": np.array(alphas, dtype=np.float32),
+                                     "ok": np.array(ok), "end_bias": np.array(end_bias),
+                                     "fc_scale": np.array(fc_scale)},
+              {"A": A, "D": D, "M": M, "V": V, "k": k, "seed": seed, "start": vocab("<start>"),
+               "end": vocab("<end>"), "ref": "gen_captions.py:16-131"})
+
+
 CASES = {"soft_attention": soft_attention_cases, "decoder_forward": decoder_forward_cases,
          "baseline": baseline_cases, "train_step": train_step_cases, "encoder_wrapper": encoder_wrapper_cases,
-         "decoder_denc": decoder_denc_cases, "train_step_finetune": finetune_train_step_cases}
+         "decoder_denc": decoder_denc_cases, "train_step_finetune": finetune_train_step_cases,
+         "beam_search": beam_search_cases}
 
 
 def main():

@@ -178,3 +178,21 @@ def test_finetune_train_step(golden):
     for k, g in out["dec_raw"].items():
         check_samples(fx, "grad.dec." + k, g.numpy(), rtol=1e-3, atol=1e-6)
         check_samples(fx, "post_dec." + k, out["dec_new"][k].numpy(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("tag", ["small", "k5", "noend"])
+def test_beam_search(golden, tag):
+    """oracle/beam_ref.py vs the reference's gen_captions.attention_caption_image_beam_search."""
+    from oracle.beam_ref import beam_search
+    fx = golden(f"beam_search_{tag}")
+    m = fx["meta"]
+    p = {k: t(v) for k, v in gen.decoder_params(m["seed"], m["A"], m["D"], m["M"], m["V"]).items()}
+    p["fc.weight"] = p["fc.weight"] * float(fx["fc_scale"])
+    p["fc.bias"] = p["fc.bias"].clone()
+    p["fc.bias"][m["end"]] += float(fx["end_bias"])
+    feats = t(gen.encoder_features(m["seed"], 1)).view(1, 14, 14, 2048)
+    seq, alphas, ok = beam_search(p, feats, m["k"], m["start"], m["end"])
+    assert bool(ok) == bool(fx["ok"])
+    assert seq == fx["seq"].tolist()
+    np.testing.assert_allclose(np.array(alphas, dtype=np.float32).reshape(fx["alphas"].shape), fx["alphas"],
+                               rtol=1e-5, atol=1e-7)
