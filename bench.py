@@ -38,6 +38,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 FP32_MFMA_PEAK_TF = 157.3   # MI355X fp32 matrix peak (MI355X_MICROARCH.md)
+BF16_MFMA_PEAK_TF = 2500.0  # MI355X dense bf16 matrix peak (MI355X_MICROARCH.md; no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -58,6 +59,7 @@ def parse():
                     help="attention = BASELINE config 2/3 (frozen encoder, the headline); glove_finetune = "
                          "config 4 (GloVe-300 fp64 embedding fine-tuned + encoder layer2-4 fine-tuned); "
                          "bert_attention = config 5 (768-d word features instead of the table, synthetic)")
+    ap.add_argument("--fp32", action="store_true", help="bert_attention: keep the encoder convs fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
@@ -196,6 +198,8 @@ def main():
     if bert:
         from capmi.data import SyntheticBertEmbedder
         decoder.bert_embedder = SyntheticBertEmbedder(args.vocab, 768, device=dev)
+        if not args.fp32:
+            encoder.set_compute_precision("bf16")  # config 5 is the bf16 config
     if ft:
         # synthetic GloVe-300 table, fp64 like load_glove_vectors (embed.py:64-68, Q7)
         g = torch.Generator().manual_seed(300)
@@ -270,14 +274,15 @@ def main():
         fam_flops = sum(v[1] for v in per.values())
         fam_ms = sum(v[2] for v in per.values())
         per_img = sum(v[1] for v in per.values()) / args.steps / B
-        roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                "frac": round(ach / FP32_MFMA_PEAK_TF, 4), "traffic": _traffic(key),
+        peak = BF16_MFMA_PEAK_TF if encoder._runner.bf16 else FP32_MFMA_PEAK_TF
+        roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(ach / peak, 4), "traffic": _traffic(key),
                 "kernel": key,
                 "launches_per_step": n // args.steps,
                 "flops_per_launch": round(flops / n), "avg_launch_us": round(ms * 1e3 / n, 2),
                 "traffic_unit": "HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, profiles/r01_pmc_traffic.json)",
                 "conv_family": {"achieved_tflops": round(fam_flops / (fam_ms * 1e-3) / 1e12, 3),
-                                "frac": round(fam_flops / (fam_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF, 4),
+                                "frac": round(fam_flops / (fam_ms * 1e-3) / 1e12 / peak, 4),
                                 "conv_ms_per_step": round(fam_ms / args.steps, 3),
                                 "conv_gflop_per_image": round(per_img / 1e9, 3)},
                 "timing": "HIP events around each conv launch on its stream, " + (
@@ -292,12 +297,15 @@ def main():
             "metric": "training images/sec (whole node), 'attention' decoder, at 1/2/4/8 MI355X",
             "value": round(value, 2), "unit": "images/s", "n_gpus": N, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if encoder._runner.bf16 else "fp32",
             "data": "synthetic (resident in HBM; random-init weights, torch.manual_seed(0))",
             "config": {"workload": ("'glove_att' decoder (GloVe-300 fp64 embedding, fine-tuned) + ResNet-101 "
                                     "encoder fine-tuned (layer2-4, BN train mode), one training step per batch")
                        if ft else ("'bert_attention' decoder (768-d synthetic BERT word features) + frozen "
-                                   "ResNet-101 encoder (BN train mode), one training step per batch") if bert else
+                                   "ResNet-101 encoder (BN train mode), one training step per batch" +
+                                   ("; encoder convs bf16 MFMA (fp32 accumulate), decoder fp32 (the reference "
+                                    "forces fp32 at the LSTM input)" if encoder._runner.bf16 else "")) if bert else
                        ("'attention' decoder + frozen ResNet-101 encoder (BN train mode), "
                         "one training step per batch"),
                        "per_gpu_batch": B, "global_batch": B * N,

@@ -26,6 +26,7 @@ CAPMI_COLSUM_GROUPS = 64
 ABI_VERSION = 6
 CAPMI_BNB_RELU_Y, CAPMI_BNB_RELU_OUT = 0, 1
 CAPMI_BNB_MAX_SLABS = 256
+CAPMI_GEMM_BF16 = 1
 
 
 class GemmProblem(ctypes.Structure):
@@ -50,6 +51,7 @@ _SIGS = {
     "capmi_gemm_stat_tiles": [c_int, c_int],
     "capmi_gemm_workspace_bytes": [],
     "capmi_gemm_sk": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_vp, c_ll, c_vp],
+    "capmi_gemm_sk_ex": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_int, c_vp, c_ll, c_vp],
     "capmi_gemm_sk_plan": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp],
     "capmi_splitk_reduce": [c_vp, c_int, c_ll, c_int, c_int, c_ll, c_vp, c_vp, c_ll, c_vp],
     "capmi_colsum": [c_vp, c_int, c_int, c_ll, c_float, c_vp, c_vp, c_int, c_vp],

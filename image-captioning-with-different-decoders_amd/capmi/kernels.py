@@ -74,10 +74,11 @@ def gemm_workspace(device):
     return torch.zeros(n, device=device, dtype=torch.int32)
 
 
-def gemm_sk(prob, amode, workspace, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W):
+def gemm_sk(prob, amode, workspace, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W, bf16=False):
+    """bf16: operands rounded to bf16 in LDS, bf16 MFMA with fp32 accumulation (CAPMI_GEMM_BF16)."""
     _cuda(workspace, dtype=torch.int32)
-    call("capmi_gemm_sk", ctypes.byref(prob), amode, bmode, tile, ptr(workspace), workspace.numel() * 4,
-         stream())
+    call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, bmode, tile, 1 if bf16 else 0, ptr(workspace),
+         workspace.numel() * 4, stream())
 
 
 def gemm_sk_plan(prob, amode, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W):

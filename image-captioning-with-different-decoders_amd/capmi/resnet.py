@@ -126,6 +126,9 @@ class EncoderRunner:
         self._ws = None
         self._ws_key = None
         self.conv_hook = None  # optional callable(tag, flops, launch_fn, kernel_key) (bench timing)
+        # bf16 MFMA for the forward convs (operands rounded to bf16 in LDS, fp32 accumulation and
+        # fp32 activations/BN): the bf16 config (BASELINE config 5); fp32 is the reference's precision
+        self.bf16 = False
 
     def _workspace(self, N, H, W, device):
         key = (N, H, W, str(device))
@@ -193,12 +196,14 @@ class EncoderRunner:
             sc, sh = in_ss if in_ss is not None else (None, None)
             prob = K.problem(rows, co, Kd, x, 0, w, Kd, out, co, conv=geo, in_scale=sc, in_shift=sh, **kw_)
             mode = CAPMI_A_CONV_NHWC
-        launch = lambda: K.gemm_sk(prob, mode, self._ws["sk"], K.TILE_AUTO)  # noqa: E731
+        bf = self.bf16
+        launch = lambda: K.gemm_sk(prob, mode, self._ws["sk"], K.TILE_AUTO, bf16=bf)  # noqa: E731
         if self.conv_hook is not None:
             bm, bn, sk, generic = K.gemm_sk_plan(prob, mode, K.TILE_AUTO)
             b = lambda v: "true" if v else "false"  # noqa: E731
             key = "gemm_kernel (generic)" if generic else \
-                f"gemm_nt_kernel<{bm}, {bn}, {mode}, 0, {b(in_ss is not None and not nchw)}, {b(sk)}>"
+                f"gemm_nt_kernel<{bm}, {bn}, {mode}, 0, {b(in_ss is not None and not nchw)}, {b(sk)}" + \
+                (", true>" if bf else ">")
             self.conv_hook(tag, 2.0 * rows * co * Kd, launch, key)
         else:
             launch()

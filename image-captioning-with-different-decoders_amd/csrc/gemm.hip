@@ -565,14 +565,21 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
   return 0;
 }
 
-extern "C" int capmi_gemm_sk(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
-                             void* workspace, long long ws_bytes, void* stream) {
+extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int bmode, int tile, int flags,
+                                void* workspace, long long ws_bytes, void* stream) {
   GemmPlan g;
   bool sk = false;
+  CAPMI_REQUIRE((flags & ~CAPMI_GEMM_BF16) == 0, CAPMI_EINVAL);
+  const bool bf16 = (flags & CAPMI_GEMM_BF16) != 0;
   const int rc = sk_decide(prob, amode, bmode, tile, g, sk);
   if (rc) return rc;
+  CAPMI_REQUIRE(!bf16 || (g.nt_ok && bmode == 0 && (amode == 0 || amode == 2 || amode == 4)), CAPMI_EINVAL);
   hipStream_t s = as_stream(stream);
-  if (!sk) return gemm_launch_dp(g, amode, bmode, s);
+  if (!sk) {
+    if (g.total == 0) return 0;
+    return bf16 ? gemm_nt_launch(g.a, amode, bmode, g.bm, g.bn, (int)g.total, s, true)
+                : gemm_launch_dp(g, amode, bmode, s);
+  }
   CAPMI_REQUIRE(workspace != nullptr && aligned16(workspace), CAPMI_EINVAL);
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
   const int cus = cu_count();
@@ -583,7 +590,12 @@ extern "C" int capmi_gemm_sk(const capmi_gemm_problem* prob, int amode, int bmod
   a.sk_workers = (int)std::min<long long>(slots, a.sk_units);
   a.sk_flags = static_cast<int*>(workspace);
   a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
-  return gemm_nt_launch(a, amode, bmode, g.bm, g.bn, a.sk_workers, s);
+  return gemm_nt_launch(a, amode, bmode, g.bm, g.bn, a.sk_workers, s, bf16);
+}
+
+extern "C" int capmi_gemm_sk(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
+                             void* workspace, long long ws_bytes, void* stream) {
+  return capmi_gemm_sk_ex(prob, amode, bmode, tile, 0, workspace, ws_bytes, stream);
 }
 
 // ------------------------------------------------------------------------------------

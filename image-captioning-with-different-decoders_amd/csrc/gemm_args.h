@@ -25,6 +25,7 @@ __device__ __forceinline__ long long remap(long long r, long long r1, long long 
 
 // v2 kernel: A K-major dense / NHWC conv / NHWC4 conv1 / M-major (k rows), B = W[N][K] or k rows;
 // BM x BN in {128x128, 128x64, 64x64}
-int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int blocks, hipStream_t s);
+int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int blocks, hipStream_t s,
+                   bool bf16 = false);
 // resident workgroups per CU of the NT kernel for a tile shape (LDS / register bound)
 inline int gemm_nt_wg_per_cu(int bm, int bn) { return bm == 64 && bn == 64 ? 4 : 2; }

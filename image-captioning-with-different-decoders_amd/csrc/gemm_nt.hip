@@ -63,9 +63,29 @@ __device__ __forceinline__ int fdivq(int a, int b, float inv_b) {
 template <int BM, int BN>
 constexpr int kWavesPerEu = (BM == 64 && BN == 64) ? 4 : 2;
 
-template <int BM, int BN, int AMODE, int BMODE, bool PRO, bool SK>
+// bf16 staging (BF = true): the fp32 operands are rounded to bf16 (RNE, v_cvt_pk_bf16_f32) when
+// a k-tile is written to LDS, in natural k order with a 40-element (80 B) row stride; lane
+// (r, h) reads 8 consecutive k (one ds_read_b128) at k = 16g + 8h of row r, the operand layout
+// of v_mfma_f32_32x32x16_bf16 (32 cycles per MFMA instead of 64 per 32x32x2 f32 for 8x the k).
+// 16 lanes x 16 B at stride 80 B touch 64 distinct banks. Accumulation stays fp32; the
+// epilogue, BN statistics and stream-K hand-off are the fp32 kernel's.
+constexpr int SB = BK2 + 8;  // bf16 LDS row stride (elements)
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x4 to_bf16x4(float4 v) {
+  bf16x4 r;
+  r.x = (__bf16)v.x;
+  r.y = (__bf16)v.y;
+  r.z = (__bf16)v.z;
+  r.w = (__bf16)v.w;
+  return r;
+}
+
+template <int BM, int BN, int AMODE, int BMODE, bool PRO, bool SK, bool BF = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWavesPerEu<BM, BN>)))
 gemm_nt_kernel(const GemmArgs args) {
+  static_assert(!BF || (BMODE == 0 && AMODE != 1), "bf16 staging: row-major A (dense / conv) x W[N][K] only");
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
   constexpr int NA = BM * BK2 / 4 / 256, NB = BN * BK2 / 4 / 256;
   static_assert(NA >= 1 && NB >= 1, "tile");
@@ -274,6 +294,26 @@ gemm_nt_kernel(const GemmArgs args) {
       }
     };
     auto store_tile = [&](const Stage& st, int buf) {
+      if (BF) {
+        __bf16* Ah = reinterpret_cast<__bf16*>(As[buf]);
+        __bf16* Bh = reinterpret_cast<__bf16*>(Bs[buf]);
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+          float4 v = st.ra[i];
+          if (PRO && AMODE == 2) v = relu4(fma4(v, st.sc, st.sh));
+          if (!((st.am >> i) & 1u)) v = f4(0.f);
+          const int f = tid + i * 256;
+          *reinterpret_cast<bf16x4*>(Ah + (f >> 3) * SB + kq) = to_bf16x4(v);
+        }
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          float4 v = st.rb[i];
+          if (!((st.bm >> i) & 1u)) v = f4(0.f);
+          const int f = tid + i * 256;
+          *reinterpret_cast<bf16x4*>(Bh + (f >> 3) * SB + kq) = to_bf16x4(v);
+        }
+        return;
+      }
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         float4 v = st.ra[i];
@@ -300,6 +340,24 @@ gemm_nt_kernel(const GemmArgs args) {
       }
     };
     auto compute = [&](int buf) {
+      if (BF) {
+        const __bf16* Ah = reinterpret_cast<const __bf16*>(As[buf]) + (wm0 + lr) * SB + 8 * lh;
+        const __bf16* Bh = reinterpret_cast<const __bf16*>(Bs[buf]) + (wn0 + lr) * SB + 8 * lh;
+#pragma unroll
+        for (int g = 0; g < BK2 / 16; ++g) {
+          bf16x8 a[TM], b[TN];
+#pragma unroll
+          for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const bf16x8*>(Ah + 32 * i * SB + 16 * g);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Bh + 32 * j * SB + 16 * g);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        return;
+      }
       const float* Ab = As[buf] + (wm0 + lr) * S2 + 4 * lh;
       const float* Bb = Bs[buf] + (wn0 + lr) * S2 + 4 * lh;
 #pragma unroll
@@ -540,6 +598,19 @@ gemm_nt_kernel(const GemmArgs args) {
 }
 
 template <int BM, int BN, bool SK>
+void launch_sk_bf16(const GemmArgs& a, int amode, bool pro, int blocks, hipStream_t s) {
+  const dim3 g(blocks), b(256);
+  if (amode == 4)
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 4, 0, false, SK, true>), g, b, 0, s, a);
+  else if (amode == 0)
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 0, 0, false, SK, true>), g, b, 0, s, a);
+  else if (pro)
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 2, 0, true, SK, true>), g, b, 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 2, 0, false, SK, true>), g, b, 0, s, a);
+}
+
+template <int BM, int BN, bool SK>
 void launch_sk(const GemmArgs& a, int amode, int bmode, bool pro, int blocks, hipStream_t s) {
   const dim3 g(blocks), b(256);
   if (bmode == 2) {  // weight gradient: A = dY stored as k rows, B = implicit im2col k rows
@@ -566,8 +637,13 @@ void launch_sk(const GemmArgs& a, int amode, int bmode, bool pro, int blocks, hi
 }
 
 template <int BM, int BN>
-int launch_bmbn(const GemmArgs& a, int amode, int bmode, bool pro, int blocks, hipStream_t s) {
-  if (a.sk_workers > 0)
+int launch_bmbn(const GemmArgs& a, int amode, int bmode, bool pro, bool bf16, int blocks, hipStream_t s) {
+  if (bf16) {
+    if (a.sk_workers > 0)
+      launch_sk_bf16<BM, BN, true>(a, amode, pro, blocks, s);
+    else
+      launch_sk_bf16<BM, BN, false>(a, amode, pro, blocks, s);
+  } else if (a.sk_workers > 0)
     launch_sk<BM, BN, true>(a, amode, bmode, pro, blocks, s);
   else
     launch_sk<BM, BN, false>(a, amode, bmode, pro, blocks, s);
@@ -577,15 +653,17 @@ int launch_bmbn(const GemmArgs& a, int amode, int bmode, bool pro, int blocks, h
 
 }  // namespace
 
-int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int blocks, hipStream_t s) {
+int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int blocks, hipStream_t s,
+                   bool bf16) {
   bool pro = false;
   for (int i = 0; i < a.nprob; ++i) pro = pro || a.p[i].in_scale != nullptr;
   for (int i = 0; i < a.nprob; ++i)
     if (pro && a.p[i].in_scale == nullptr) return CAPMI_EINVAL;  // grouped: all or none
   if (pro && !((amode == 2 && bmode == 0) || (amode == 1 && bmode == 2))) return CAPMI_EINVAL;
   if (bmode == 2 && amode != 1) return CAPMI_EINVAL;
-  if (bm == 128 && bn == 128) return launch_bmbn<128, 128>(a, amode, bmode, pro, blocks, s);
-  if (bm == 128 && bn == 64) return launch_bmbn<128, 64>(a, amode, bmode, pro, blocks, s);
-  if (bm == 64 && bn == 64) return launch_bmbn<64, 64>(a, amode, bmode, pro, blocks, s);
+  if (bf16 && !(bmode == 0 && (amode == 0 || amode == 2 || amode == 4))) return CAPMI_EINVAL;
+  if (bm == 128 && bn == 128) return launch_bmbn<128, 128>(a, amode, bmode, pro, bf16, blocks, s);
+  if (bm == 128 && bn == 64) return launch_bmbn<128, 64>(a, amode, bmode, pro, bf16, blocks, s);
+  if (bm == 64 && bn == 64) return launch_bmbn<64, 64>(a, amode, bmode, pro, bf16, blocks, s);
   return CAPMI_EINVAL;
 }

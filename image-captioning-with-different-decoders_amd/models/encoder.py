@@ -121,6 +121,13 @@ class EncoderAttention(nn.Module):
             param.requires_grad = False
         self._runner = EncoderRunner()
 
+    def set_compute_precision(self, precision):
+        """'fp32' (the reference's) or 'bf16': bf16 MFMA for the frozen forward convs (fp32
+        accumulation, activations and BatchNorm stay fp32) -- the bf16 config (BASELINE config 5)."""
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(precision)
+        self._runner.bf16 = precision == "bf16"
+
     def _out_hw(self):
         out_hw = self.adaptive_pool.output_size
         return (out_hw, out_hw) if isinstance(out_hw, int) else tuple(out_hw)
@@ -146,7 +153,9 @@ class EncoderAttention(nn.Module):
         return ft
 
     def ft_forward(self, imgs, out=None):
-        """Train-mode forward that keeps layer2-4's activations for ft_backward."""
+        """Train-mode forward that keeps layer2-4's activations for ft_backward (fp32)."""
+        if self._runner.bf16:
+            raise NotImplementedError("capmi: the fine-tune path runs fp32 (set_compute_precision('fp32'))")
         return self._ft().forward(_ResNetView(self.resnet), imgs.contiguous(), self._out_hw(), out=out)
 
     def ft_backward(self, dfeat, grads, hook=None):

@@ -94,6 +94,13 @@ int capmi_gemm_stat_tiles(int M, int tile);
 long long capmi_gemm_workspace_bytes(void);
 int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int tile, void* workspace,
                   long long ws_bytes, void* stream);
+/* capmi_gemm_sk with flags: CAPMI_GEMM_BF16 = operands rounded to bf16 (RNE) when staged to LDS,
+ * v_mfma_f32_32x32x16_bf16 with fp32 accumulation (the bf16 configs, BASELINE config 5); A row-major
+ * (CAPMI_A_KMAJOR / CAPMI_A_CONV_NHWC / CAPMI_A_CONV_NHWC4) x B = W[N][K] (CAPMI_B_NMAJOR_W) only.
+ * Inputs, outputs, statistics and the prologue stay fp32. */
+#define CAPMI_GEMM_BF16 1
+int capmi_gemm_sk_ex(const capmi_gemm_problem* problem, int amode, int bmode, int tile, int flags, void* workspace,
+                     long long ws_bytes, void* stream);
 /* the launch capmi_gemm_sk would make (no GPU work): tile bm x bn, stream_k 0/1, generic = 1
  * when the problem falls back to the generic kernel. Used by the benchmark to attribute time. */
 int capmi_gemm_sk_plan(const capmi_gemm_problem* problem, int amode, int bmode, int tile, int* bm, int* bn,

@@ -1,0 +1,110 @@
+"""GPU: the bf16-staged implicit-GEMM conv (CAPMI_GEMM_BF16; BASELINE config 5 is the bf16
+config). The kernel rounds each operand to bf16 (RNE) when it stages a k-tile into LDS and
+accumulates bf16 x bf16 products (exact in fp32) in fp32, so against the fp64 product of the
+SAME bf16-rounded operands it must agree to fp32 summation error: relative L2 <= 1e-5 (this pins
+the kernel, not the precision). The bf16 encoder as a whole is compared with the fp64 oracle at a
+bf16-sized tolerance (documented in the test)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import rel_err, t
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).to(torch.float64)
+
+
+def _rand(shape, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(shape, generator=g, dtype=torch.float64) * 2 - 1) * scale
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,k,s,pro,tile", [
+    (2, 14, 256, 256, 3, 1, True, 3),    # layer3 conv2 shape class, stream-K / auto tile
+    (2, 14, 64, 128, 1, 1, True, 1),     # 1x1 with prologue, 64x64 data-parallel
+    (1, 28, 128, 128, 3, 2, True, 2),    # stride-2 3x3
+    (2, 14, 128, 64, 1, 2, False, 3),    # stride-2 1x1 downsample (no prologue)
+])
+def test_bf16_conv_gemm_exact_on_rounded_operands(N, H, Cin, Cout, k, s, pro, tile):
+    from capmi import kernels as K
+    from capmi._lib import CAPMI_A_CONV_NHWC
+    pad = k // 2
+    Ho = (H + 2 * pad - k) // s + 1
+    x = _rand((N, H, H, Cin), 1, 2.0)
+    w = _rand((Cout, k, k, Cin), 2, 0.1)
+    sc, sh = _rand((Cin,), 3, 1.5), _rand((Cin,), 4, 0.5)
+    xf = x.float()
+    a = torch.relu(xf * sc.float() + sh.float()) if pro else xf  # the prologue runs in fp32, then rounds
+    a = a.double().permute(0, 3, 1, 2)
+    ref = F.conv2d(_bf(a), _bf(w).permute(0, 3, 1, 2), stride=s, padding=pad).permute(0, 2, 3, 1)
+    out = torch.empty(N, Ho, Ho, Cout, device=DEV)
+    geo = dict(N=N, H=H, W=H, Cin=Cin, KH=k, KW=k, stride=s, pad=pad, Ho=Ho, Wo=Ho)
+    prob = K.problem(N * Ho * Ho, Cout, k * k * Cin, x.float().to(DEV), 0, w.float().to(DEV).contiguous(),
+                     k * k * Cin, out, Cout, conv=geo, in_scale=sc.float().to(DEV) if pro else None,
+                     in_shift=sh.float().to(DEV) if pro else None)
+    K.gemm_sk(prob, CAPMI_A_CONV_NHWC, K.gemm_workspace(DEV), tile, bf16=True)
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 1e-5, rel_err(out, ref)
+
+
+def test_bf16_dense_and_conv1_modes():
+    from capmi import kernels as K
+    from capmi._lib import CAPMI_A_CONV_NHWC4, CAPMI_A_KMAJOR
+    ws = K.gemm_workspace(DEV)
+    M, N, Kd = 1000, 192, 320
+    a, b = _rand((M, Kd), 5), _rand((N, Kd), 6)
+    c = torch.empty(M, N, device=DEV)
+    K.gemm_sk(K.problem(M, N, Kd, a.float().to(DEV), Kd, b.float().to(DEV), Kd, c, N), CAPMI_A_KMAJOR, ws,
+              K.TILE_AUTO, bf16=True)
+    torch.cuda.synchronize()
+    assert rel_err(c, _bf(a) @ _bf(b).T) < 1e-5
+    # conv1: 7x7/2 over NHWC4 images (4th channel zero)
+    img = _rand((2, 3, 64, 64), 7)
+    w = _rand((64, 3, 7, 7), 8, 0.1)
+    img4 = torch.empty(2 * 64 * 64 * 4, device=DEV)
+    K.image_nhwc4(img.float().to(DEV).contiguous(), img4)
+    wp = torch.empty(64, 7, 7, 4, device=DEV)
+    K.conv_weight_pack_pad(w.float().to(DEV).contiguous(), 4, wp)
+    out = torch.empty(2, 32, 32, 64, device=DEV)
+    geo = dict(N=2, H=64, W=64, Cin=4, KH=7, KW=7, stride=2, pad=3, Ho=32, Wo=32)
+    K.gemm_sk(K.problem(2 * 32 * 32, 64, 196, img4, 0, wp, 196, out, 64, conv=geo), CAPMI_A_CONV_NHWC4, ws,
+              K.TILE_AUTO, bf16=True)
+    torch.cuda.synchronize()
+    ref = F.conv2d(_bf(img), _bf(w), stride=2, padding=3).permute(0, 2, 3, 1)
+    assert rel_err(out, ref) < 1e-5
+
+
+def test_bf16_encoder_vs_oracle():
+    """Whole frozen ResNet-101 forward with bf16 convs vs the fp64 oracle. Each conv rounds its
+    operands to 8 significant bits (rel. 2^-9); over 104 convs the features stay at the 1e-2
+    level when the network is well conditioned: eval-mode BN, and train-mode BN with the residual
+    branches' last BN scaled down (bn3.weight x 0.1, the regime of trained ResNets and of
+    torchvision's zero_init_residual). With gamma ~ U(0.5, 1.5) everywhere, train-mode BN at
+    random init is chaotic -- the fp32 CPU path is already 4e-4 from fp64 there and a bf16
+    perturbation is amplified to O(1) -- so that regime is not a meaningful bf16 test."""
+    import gen
+    from oracle.resnet_ref import build_resnet101, encoder_attention_forward
+    from test_gpu_encoder import _encoder
+    torch.set_num_threads(16)
+    params = gen.resnet101_params(71)
+    for k in params:
+        if k.endswith("bn3.weight"):
+            params[k] = params[k] * 0.1
+    enc = _encoder(params)
+    enc.set_compute_precision("bf16")
+    x = gen.images(71, 2)
+    for mode, bound in (("eval", 1e-2), ("train", 3e-2)):
+        r64 = build_resnet101(params).double()
+        enc.train(mode == "train")
+        r64.train(mode == "train")
+        with torch.no_grad():
+            y = enc(t(x, DEV))
+            y64 = encoder_attention_forward(r64, t(x).double())
+        torch.cuda.synchronize()
+        e = rel_err(y, y64)
+        print(f"bf16 encoder {mode}: rel L2 vs fp64 {e:.3g}")
+        assert e < bound, (mode, e)
