@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (load torch's HIP runtime before libcapmi)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcapmi.so")
+LIB_PATH = os.environ.get("CAPMI_LIB") or os.path.join(_HERE, "libcapmi.so")  # CAPMI_LIB: kernel A/B builds
 
 c_int, c_ll, c_float, c_double, c_vp = ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
 c_ull = ctypes.c_ulonglong

@@ -1,0 +1,140 @@
+"""GPU, world_size 2 on ONE device (gloo backend, two processes sharing cuda:0): the data-parallel
+training steps run end to end (RCCL refuses two ranks on one GPU, and the 8-GPU node is the
+driver's), i.e. capmi.train_step's DP logic with real HIP kernels:
+
+  * frozen encoder (config 3), pipelined two-stream step: after the step the gradient buffer of
+    every rank equals the mean of the per-shard gradients, computed in the same process by the
+    non-DP fused path on each shard; parameters are identical on both ranks;
+  * encoder fine-tune (config 4): the same for the decoder AND the encoder gradient buffers
+    (decoder all-reduce issued before the encoder backward, encoder all-reduce after it).
+
+Equality is to fp32 summation order (rtol 1e-6 relative to max|g|): the only difference is
+(g0 + g1) / 2 vs the gloo SUM-then-scale."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _setup(fine_tune, seed=3):
+    import gen
+    from capmi.optim import Adam
+    from helpers import make_decoder, t
+    from models.encoder import EncoderAttention
+    torch.manual_seed(seed)
+    enc = EncoderAttention()
+    sd = enc.state_dict()
+    names = ["conv1", "bn1", "relu", "maxpool", "layer1", "layer2", "layer3", "layer4"]
+    for k, v in gen.resnet101_params(seed).items():
+        head, rest = k.split(".", 1)
+        sd[f"resnet.{names.index(head)}.{rest}"] = t(v).clone()
+    enc.load_state_dict(sd)
+    if fine_tune:
+        enc.fine_tune(True)
+    enc = enc.cuda().train()
+    dec, _ = make_decoder(32, 32, 16, 50, seed, "cuda")
+    dec.train()
+    dopt = Adam([q for q in dec.parameters() if q.requires_grad], lr=1e-4)
+    eopt = Adam([q for q in enc.parameters() if q.requires_grad], lr=1e-4) if fine_tune else None
+    for o in (dopt, eopt):
+        if o is not None:
+            o.set_clip(5.0)
+    return enc, dec, dopt, eopt
+
+
+def _worker(rank, world, port, fine_tune, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(os.path.dirname(here), "image-captioning-with-different-decoders_amd"),
+              os.path.dirname(here), os.path.join(here, "golden"), here):
+        sys.path.insert(0, p)
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    try:
+        import gen
+        from capmi import decoder_fn as DF
+        from capmi import dist as cdist
+        from capmi.train_step import AttentionTrainStep
+        from helpers import t
+        ctx = cdist.init_from_env("cuda", backend="gloo")
+        B, L, V = 2, 6, 50
+        imgs = t(gen.images(11, B * world, 64, 64), "cuda")
+        caps = t(gen.captions(11, B * world, L, V), "cuda")
+        # reference: non-DP fused gradients of each shard, on a fresh copy of the same model
+        enc, dec, dopt, eopt = _setup(fine_tune)
+        ref_d, ref_e = [], []
+        for r in range(world):
+            sl = slice(r * B, (r + 1) * B)
+            g = {n: torch.zeros_like(q) for n, q in dec.named_parameters() if q.requires_grad}
+            if fine_tune:
+                f = enc.ft_forward(imgs[sl])
+                denc = torch.empty_like(f)
+                DF.fused_loss_and_grads(dec, f, caps[sl], [L] * B, 1.0, g, denc=denc)
+                eg = {id(q): torch.zeros_like(q) for q in enc.parameters() if q.requires_grad}
+                enc.ft_backward(denc, eg)
+                ref_e.append(torch.cat([eg[id(q)].reshape(-1) for q in enc.parameters() if q.requires_grad]))
+            else:
+                with torch.no_grad():
+                    f = enc(imgs[sl])
+                DF.fused_loss_and_grads(dec, f, caps[sl], [L] * B, 1.0, g)
+            ref_d.append(torch.cat([g[n].reshape(-1) for n, q in dec.named_parameters() if q.requires_grad]))
+        torch.cuda.synchronize()
+        # the DP step on this rank's shard (fresh model: BN running stats / weights as above)
+        enc, dec, dopt, eopt = _setup(fine_tune)
+        step = AttentionTrainStep(enc, dec, dopt, ctx, seed=9, pipeline=not fine_tune, encoder_optimizer=eopt)
+        sl = slice(rank * B, (rank + 1) * B)
+        step(imgs[sl], caps[sl], [L] * B)
+        step.flush()
+        torch.cuda.synchronize()
+        got_d = torch.cat([q.grad.reshape(-1) for q in dec.parameters() if q.requires_grad])
+        want_d = (ref_d[0] + ref_d[1]) / 2
+        err_d = float((got_d - want_d).abs().max() / want_d.abs().max())
+        err_e = 0.0
+        if fine_tune:
+            got_e = torch.cat([q.grad.reshape(-1) for q in enc.parameters() if q.requires_grad])
+            want_e = (ref_e[0] + ref_e[1]) / 2
+            err_e = float((got_e - want_e).abs().max() / want_e.abs().max())
+        p = torch.cat([q.detach().reshape(-1) for q in dec.parameters()]).cpu()
+        q.put((rank, err_d, err_e, p))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "error", traceback.format_exc(), None))
+        raise e
+    finally:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fine_tune", [False, True])
+def test_dp_two_ranks_one_gpu(fine_tune):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, fine_tune, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r = q.get(timeout=180)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=60)
+    for r in res.values():
+        assert r[1] != "error", r[2]
+    for r in (0, 1):
+        assert res[r][1] < 1e-6, ("decoder grads", res[r][1])
+        assert res[r][2] < 1e-6, ("encoder grads", res[r][2])
+    assert torch.equal(res[0][3], res[1][3])  # identical parameters after the update

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--tile", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--bf16", action="store_true")
     a = ap.parse_args()
     dev = "cuda"
     ci, H, W, co, k, pro = SHAPES[a.shape]
@@ -46,11 +47,11 @@ def main():
     ws = K.gemm_workspace(dev)
     print("plan (bm, bn, stream_k, generic):", K.gemm_sk_plan(prob, mode, a.tile))
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    K.gemm_sk(prob, mode, ws, a.tile)
+    K.gemm_sk(prob, mode, ws, a.tile, bf16=a.bf16)
     torch.cuda.synchronize()
     s.record()
     for _ in range(a.reps):
-        K.gemm_sk(prob, mode, ws, a.tile)
+        K.gemm_sk(prob, mode, ws, a.tile, bf16=a.bf16)
     e.record()
     torch.cuda.synchronize()
     us = s.elapsed_time(e) * 1e3 / a.reps
