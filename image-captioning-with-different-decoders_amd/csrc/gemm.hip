@@ -14,6 +14,8 @@
 // rely on split-K for parallelism; split partial slabs are summed by the consumer.
 // Global->LDS staging is register-double-buffered: tile t+1 is loaded into registers
 // while tile t is multiplied out of LDS, one barrier per K-tile.
+#include <cstdlib>
+
 #include "common.h"
 
 #include "gemm_args.h"
@@ -529,6 +531,14 @@ extern "C" long long capmi_gemm_workspace_bytes(void) {
 }
 
 namespace {
+// XCD-grouped stream-K (gemm_nt.hip); CAPMI_SK_GROUPS=1 turns it off (A/B measurement)
+bool sk_xcd_groups() {
+  static const bool on = [] {
+    const char* e = getenv("CAPMI_SK_GROUPS");
+    return !(e && e[0] == '1' && e[1] == 0);
+  }();
+  return on;
+}
 // the launch capmi_gemm_sk makes for a problem (shared by the launcher and the plan query)
 int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, GemmPlan& g, bool& sk) {
   CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
@@ -588,6 +598,7 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   a.sk_nkt = (prob->K + 31) / 32;
   a.sk_units = g.total * a.sk_nkt;
   a.sk_workers = (int)std::min<long long>(slots, a.sk_units);
+  a.sk_groups = sk_xcd_groups() && a.sk_workers % 8 == 0 && g.total >= 64 ? 8 : 1;
   a.sk_flags = static_cast<int*>(workspace);
   a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
   return gemm_nt_launch(a, amode, bmode, g.bm, g.bn, a.sk_workers, s, bf16);

@@ -15,6 +15,7 @@ struct GemmArgs {
   int sk_workers;
   int sk_nkt;            // k-tiles per output tile
   long long sk_units;    // tiles * sk_nkt
+  int sk_groups;         // 1, or 8: tiles and workers split into blockIdx%8 groups (XCD-local)
   float* sk_part;        // [workers][BM*BN] parked k-prefix partials
   int* sk_flags;         // [workers + 1], zero between launches; [workers] = spin-timeout flag
 };

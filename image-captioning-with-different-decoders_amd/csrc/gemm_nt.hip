@@ -401,10 +401,16 @@ gemm_nt_kernel(const GemmArgs args) {
     if (DEEP) {
       load_tile(s1, 1);
       __syncthreads();
-      for (int kt = 0; kt < nkt; kt += 2) {
+      // the back edge must only ever come from the second k-step: with a conditional second
+      // step inside the loop, the header merges a path on which the first step's loads are
+      // still in flight into the registers the next ds_reads overwrite, and the compiler waits
+      // vmcnt(0) at the top of EVERY iteration (the second step's prefetch then has no time)
+      int kt = 0;
+      for (; kt + 1 < nkt; kt += 2) {
         kstep(s0, s1, kt);
-        if (kt + 1 < nkt) kstep(s1, s0, kt + 1);
+        kstep(s1, s0, kt + 1);
       }
+      if (kt < nkt) kstep(s0, s1, kt);
     } else {
       __syncthreads();
       for (int kt = 0; kt < nkt; ++kt) {
@@ -529,10 +535,18 @@ gemm_nt_kernel(const GemmArgs args) {
   // visits it LAST, adds the parked partials of the lower-numbered contributors in a fixed
   // order (deterministic) and runs the epilogue. A worker only ever waits on lower-numbered
   // workgroups, which are dispatched before it.
+  //
+  // With sk_groups = 8 the tiles are cut into 8 contiguous ranges (consecutive tiles share A
+  // rows) and the workers with blockIdx % 8 == x run stream-K over range x among themselves:
+  // under the observed round-robin placement that is one XCD, whose 4 MB L2 then holds its
+  // range's A rows instead of every XCD streaming all of them (speed only). A worker still
+  // only waits on workers with a lower blockIdx (same group, earlier in the group's order).
   const capmi_gemm_problem& P = args.p[0];
-  const long long U = args.sk_units, G = gridDim.x, w = blockIdx.x;
   const int nkt = args.sk_nkt, tiles_n = args.tiles_n[0];
-  const long long u0 = w * U / G, u1 = (w + 1) * U / G;
+  const long long ngrp = args.sk_groups, grp = blockIdx.x % ngrp;
+  const long long T = args.sk_units / nkt, G = gridDim.x / ngrp, w = blockIdx.x / ngrp;
+  const long long ub = grp * T / ngrp * nkt, U = ((grp + 1) * T / ngrp) * nkt - ub;
+  const long long u0 = ub + w * U / G, u1 = ub + (w + 1) * U / G;
   if (u0 >= u1) return;
   constexpr int PART = BM * BN;
   int* flags = args.sk_flags;
@@ -544,7 +558,7 @@ gemm_nt_kernel(const GemmArgs args) {
     if (ke < nkt) {  // k-prefix of a tile finished by a higher-numbered worker: park it
       // write-through (sc1) 16-B stores, every wave drains them, one lane raises the flag
       // with an agent-scope store: the hand-off needs no L2 write-back fence
-      const auto rs = slot_rsrc(args.sk_part, w * PART);
+      const auto rs = slot_rsrc(args.sk_part, (long long)blockIdx.x * PART);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -560,23 +574,24 @@ gemm_nt_kernel(const GemmArgs args) {
           }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == 0) __hip_atomic_store(flags + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) __hip_atomic_store(flags + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       continue;
     }
     if (ks > 0) {  // add the parked k-prefixes, nearest contributor first
       for (long long w2 = w - 1;; --w2) {
+        const long long b2 = w2 * ngrp + grp;  // blockIdx of the contributor
         if (tid == 0) {
           int spins = 0;
-          while (__hip_atomic_load(flags + w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+          while (__hip_atomic_load(flags + b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
                  ++spins < (1 << 22))
             __builtin_amdgcn_s_sleep(2);
-          if (spins >= (1 << 22)) flags[G] = 1;  // never expected: report instead of hanging
-          __hip_atomic_store(flags + w2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (spins >= (1 << 22)) flags[gridDim.x] = 1;  // never expected: report instead of hanging
+          __hip_atomic_store(flags + b2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the poll
         // every load of the parked bytes is an sc1 (L1-bypassing) load: no agent acquire needed
-        const auto rs = slot_rsrc(args.sk_part, w2 * PART);
+        const auto rs = slot_rsrc(args.sk_part, b2 * PART);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -590,7 +605,7 @@ gemm_nt_kernel(const GemmArgs args) {
               acc[i][j][4 * q + 2] += __uint_as_float(v.z);
               acc[i][j][4 * q + 3] += __uint_as_float(v.w);
             }
-        if (w2 * U / G <= tb) break;  // w2's range starts inside (or at) this tile
+        if (ub + w2 * U / G <= tb) break;  // w2's range starts inside (or at) this tile
       }
     }
     epilogue(P, tm, tn, 0);

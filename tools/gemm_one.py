@@ -25,9 +25,11 @@ def main():
     ap.add_argument("--tile", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--bf16", action="store_true")
+    ap.add_argument("--nopro", action="store_true", help="drop the BN-apply+ReLU prologue (1x1: dense A)")
     a = ap.parse_args()
     dev = "cuda"
     ci, H, W, co, k, pro = SHAPES[a.shape]
+    pro = pro and not a.nopro
     N = a.batch
     M, Kd = N * H * W, ci * k * k
     g = torch.Generator(device=dev).manual_seed(0)
