@@ -23,10 +23,11 @@ CAPMI_B_NMAJOR_W, CAPMI_B_KROWS, CAPMI_B_CONV_NHWC = 0, 1, 2
 CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO = 0, 1, 2, 3
 CAPMI_MAX_GROUP = 4
 CAPMI_COLSUM_GROUPS = 64
-ABI_VERSION = 6
+ABI_VERSION = 7
 CAPMI_BNB_RELU_Y, CAPMI_BNB_RELU_OUT = 0, 1
 CAPMI_BNB_MAX_SLABS = 256
 CAPMI_GEMM_BF16 = 1
+CAPMI_GEMM_BF16_IO = 2
 
 
 class GemmProblem(ctypes.Structure):
@@ -101,6 +102,10 @@ _SIGS = {
     "capmi_adam_clamp_f64": [c_vp, c_vp, c_vp, c_vp, c_ll, c_double, c_double, c_double, c_double,
                              c_double, c_double, c_double, c_vp, c_vp],
     "capmi_embed_scatter_add": [c_vp, c_ll, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp],
+    "capmi_bn_relu_bf16": [c_vp, c_vp, c_vp, c_ll, c_int, c_vp, c_vp],
+    "capmi_bn_add_relu_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_vp, c_vp],
+    "capmi_f32_to_bf16": [c_vp, c_ll, c_vp, c_vp],
+    "capmi_adaptive_avgpool_bf16": [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_strerror": [c_int],
     "capmi_abi_version": [],
 }

@@ -7,7 +7,7 @@ import ctypes
 
 import torch
 
-from ._lib import (CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_COLSUM_GROUPS, CAPMI_TILE_128, CAPMI_TILE_64,
+from ._lib import (CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_GEMM_BF16_IO, CAPMI_COLSUM_GROUPS, CAPMI_TILE_128, CAPMI_TILE_64,
                    CAPMI_TILE_128x64, CAPMI_TILE_AUTO, GemmProblem, call, lib)
 
 F32 = torch.float32
@@ -79,6 +79,31 @@ def gemm_sk(prob, amode, workspace, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W
     _cuda(workspace, dtype=torch.int32)
     call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, bmode, tile, 1 if bf16 else 0, ptr(workspace),
          workspace.numel() * 4, stream())
+
+
+def problem_bf16(M, N, K, A, lda, B, ldb, C, ldc, *, stats=None, conv=None):
+    """capmi_gemm_problem over bf16 A / B / C (CAPMI_GEMM_BF16_IO): plain conv or dense GEMM,
+    fp32 BN statistics of the stored (bf16) output."""
+    _cuda(A, B, C, dtype=torch.bfloat16)
+    _cuda(stats)
+    p = GemmProblem()
+    p.M, p.N, p.K, p.ksplit = int(M), int(N), int(K), 1
+    p.A, p.lda, p.B, p.ldb = ptr(A), int(lda), ptr(B), int(ldb)
+    p.C, p.ldc = ptr(C), int(ldc)
+    p.alpha, p.beta = 1.0, 0.0
+    p.stats = ptr(stats)
+    if conv is not None:
+        p.cN, p.cH, p.cW, p.cCin = conv["N"], conv["H"], conv["W"], conv["Cin"]
+        p.cKH, p.cKW, p.cStride, p.cPad = conv["KH"], conv["KW"], conv["stride"], conv["pad"]
+        p.cHo, p.cWo = conv["Ho"], conv["Wo"]
+    return p
+
+
+def gemm_bf16(prob, amode, workspace, tile=CAPMI_TILE_AUTO):
+    """bf16-in / bf16-out GEMM or implicit-GEMM conv (CAPMI_GEMM_BF16_IO)."""
+    _cuda(workspace, dtype=torch.int32)
+    call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, tile, CAPMI_GEMM_BF16_IO,
+         ptr(workspace), workspace.numel() * 4, stream())
 
 
 def gemm_sk_plan(prob, amode, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W):
@@ -168,6 +193,32 @@ def bn_add_relu(y, s, b, res, out, rows, C, res_scale=None, res_shift=None):
 def bn_relu_maxpool(y, s, b, out, N, H, W, C, Ho, Wo):
     _cuda(y, s, b, out)
     call("capmi_bn_relu_maxpool", ptr(y), ptr(s), ptr(b), ptr(out), N, H, W, C, Ho, Wo, stream())
+
+
+def bn_relu_bf16(y, s, b, rows, C, x):
+    _cuda(y, x, dtype=torch.bfloat16)
+    _cuda(s, b)
+    call("capmi_bn_relu_bf16", ptr(y), ptr(s), ptr(b), rows, C, ptr(x), stream())
+
+
+def bn_add_relu_bf16(y, s, b, res, out, rows, C, res_scale=None, res_shift=None):
+    _cuda(y, res, out, dtype=torch.bfloat16)
+    _cuda(s, b, res_scale, res_shift)
+    call("capmi_bn_add_relu_bf16", ptr(y), ptr(s), ptr(b), ptr(res), ptr(res_scale), ptr(res_shift),
+         rows, C, ptr(out), stream())
+
+
+def f32_to_bf16(x, out):
+    _cuda(x)
+    _cuda(out, dtype=torch.bfloat16)
+    assert x.is_contiguous() and out.numel() >= x.numel()
+    call("capmi_f32_to_bf16", ptr(x), x.numel(), ptr(out), stream())
+
+
+def adaptive_avgpool_bf16(inp, N, H, W, C, OH, OW, out):
+    _cuda(inp, dtype=torch.bfloat16)
+    _cuda(out)
+    call("capmi_adaptive_avgpool_bf16", ptr(inp), N, H, W, C, OH, OW, ptr(out), stream())
 
 
 def adaptive_avgpool_nhwc(inp, N, H, W, C, OH, OW, out):

@@ -126,8 +126,8 @@ class EncoderRunner:
         self._ws = None
         self._ws_key = None
         self.conv_hook = None  # optional callable(tag, flops, launch_fn, kernel_key) (bench timing)
-        # bf16 MFMA for the forward convs (operands rounded to bf16 in LDS, fp32 accumulation and
-        # fp32 activations/BN): the bf16 config (BASELINE config 5); fp32 is the reference's precision
+        # bf16 forward (the bf16 config, BASELINE config 5): bf16 NHWC activations and weights, bf16
+        # MFMA with fp32 accumulation, fp32 BN statistics (_forward_bf16); fp32 is the reference's
         self.bf16 = False
 
     def _workspace(self, N, H, W, device):
@@ -210,6 +210,96 @@ class EncoderRunner:
         del stats
         return Ho, Wo, rows
 
+    # ---- bf16 activations (BASELINE config 5) -------------------------------------------------
+    def _packed_bf16(self, conv):
+        """bf16 copy of the packed [Cout][KH][KW][Cin] weight, refreshed when the weight changes."""
+        w = conv.weight
+        key = ("bf16", id(conv))
+        ent = self.packed.cache.get(key)
+        if ent is None or ent[0] != w._version or ent[1] != w.data_ptr():
+            src = self.packed.get(conv).contiguous()
+            dst = torch.empty(src.shape, device=w.device, dtype=torch.bfloat16)
+            K.f32_to_bf16(src, dst)
+            ent = (w._version, w.data_ptr(), dst)
+            self.packed.cache[key] = ent
+        return ent[2]
+
+    def _conv_bf16(self, tag, x, conv, out, N, H, W, train):
+        """bf16 NHWC x -> bf16 NHWC out (CAPMI_GEMM_BF16_IO), BN statistics into ws['stats']."""
+        co, ci, kh, kw = conv.weight.shape
+        st, pd = conv.stride[0], conv.padding[0]
+        Ho, Wo = (H + 2 * pd - kh) // st + 1, (W + 2 * pd - kw) // st + 1
+        rows = N * Ho * Wo
+        Kd = ci * kh * kw
+        w = self._packed_bf16(conv)
+        stats = self._ws["stats"] if train else None
+        if kh == 1 and st == 1:
+            prob, mode = K.problem_bf16(rows, co, Kd, x, ci, w, Kd, out, co, stats=stats), AK
+        else:
+            geo = dict(N=N, H=H, W=W, Cin=ci, KH=kh, KW=kw, stride=st, pad=pd, Ho=Ho, Wo=Wo)
+            prob, mode = K.problem_bf16(rows, co, Kd, x, 0, w, Kd, out, co, stats=stats, conv=geo), AC
+        launch = lambda: K.gemm_bf16(prob, mode, self._ws["sk"], K.TILE_AUTO)  # noqa: E731
+        if self.conv_hook is not None:
+            key = f"gemm_bf16_kernel<128, {64 if co <= 64 else 128}, {mode}>"
+            self.conv_hook(tag, 2.0 * rows * co * Kd, launch, key)
+        else:
+            launch()
+        return Ho, Wo, rows
+
+    def _forward_bf16(self, net, imgs, out_hw, train, out):
+        """The conv stack on bf16 NHWC activations: every conv but conv1 on CAPMI_GEMM_BF16_IO (bf16
+        operands, fp32 accumulation, bf16 output, fp32 BN statistics of the stored values), the BN
+        apply + ReLU of each conv input materialised once in bf16 (capmi_bn_relu_bf16), bottleneck
+        tails in bf16; conv1 (Cin = 3) reads the fp32 images with bf16 operand staging; the features
+        come out fp32 (adaptive pool), as the decoder expects."""
+        N, C0, H, W = imgs.shape
+        ws = self._workspace(N, H, W, imgs.device)
+        if "bf" not in ws:
+            big = ws["x"].numel()
+            ws["bf"] = {n: torch.empty(big, device=imgs.device, dtype=torch.bfloat16)
+                        for n in ("x", "y1", "y2", "y3", "yd", "out")}
+        bf = ws["bf"]
+        H1, W1, rows = self._conv("conv1", imgs, net.conv1, ws["y1"], N, H, W, train, nchw=True)
+        s, b = self._bn(ws, net.bn1, rows, train)
+        Hp, Wp = (H1 + 2 - 3) // 2 + 1, (W1 + 2 - 3) // 2 + 1
+        K.bn_relu_maxpool(ws["y1"], s, b, ws["x"], N, H1, W1, 64, Hp, Wp)
+        K.f32_to_bf16(ws["x"][: N * Hp * Wp * 64], bf["x"])
+        x, xo = bf["x"], bf["out"]
+        H, W, Cx = Hp, Wp, 64
+        bns = []
+        for li in range(1, 5):
+            for bi, blk in enumerate(getattr(net, f"layer{li}")):
+                tag = f"layer{li}.{bi}"
+                _, _, r1 = self._conv_bf16(tag + ".conv1", x, blk.conv1, bf["y1"], N, H, W, train)
+                s1, b1 = self._bn(ws, blk.bn1, r1, train)
+                K.bn_relu_bf16(bf["y1"], s1, b1, r1, blk.conv1.out_channels, bf["y1"])
+                H2, W2, r2 = self._conv_bf16(tag + ".conv2", bf["y1"], blk.conv2, bf["y2"], N, H, W, train)
+                s2, b2 = self._bn(ws, blk.bn2, r2, train)
+                K.bn_relu_bf16(bf["y2"], s2, b2, r2, blk.conv2.out_channels, bf["y2"])
+                _, _, r3 = self._conv_bf16(tag + ".conv3", bf["y2"], blk.conv3, bf["y3"], N, H2, W2, train)
+                s3, b3 = self._bn(ws, blk.bn3, r3, train)
+                Cout = blk.conv3.out_channels
+                if blk.downsample is not None:
+                    self._conv_bf16(tag + ".downsample", x, blk.downsample[0], bf["yd"], N, H, W, train)
+                    sd, bd = self._bn(ws, blk.downsample[1], r3, train)
+                    K.bn_add_relu_bf16(bf["y3"], s3, b3, bf["yd"], xo, r3, Cout, res_scale=sd, res_shift=bd)
+                    bns.append(blk.downsample[1])
+                else:
+                    K.bn_add_relu_bf16(bf["y3"], s3, b3, x, xo, r3, Cout)
+                bns += [blk.bn1, blk.bn2, blk.bn3]
+                x, xo = xo, x
+                H, W, Cx = H2, W2, Cout
+        if train:
+            bns.append(net.bn1)
+            nbt = [m.num_batches_tracked for m in bns if m.num_batches_tracked is not None]
+            if nbt:
+                torch._foreach_add_(nbt, 1)
+        OH, OW = out_hw
+        if out is None:
+            out = torch.empty(N, OH, OW, Cx, device=imgs.device, dtype=torch.float32)
+        K.adaptive_avgpool_bf16(x, N, H, W, Cx, OH, OW, out)
+        return out
+
     @torch.no_grad()
     def forward(self, net, imgs, out_hw=(14, 14), train=True, out=None):
         """imgs (N,3,H,W) fp32 contiguous on the device -> (N, OH, OW, 2048) NHWC (= the
@@ -217,6 +307,8 @@ class EncoderRunner:
         if imgs.dtype != torch.float32 or not imgs.is_contiguous():
             raise TypeError("encoder input must be contiguous float32 (N,3,H,W)")
         N, C0, H, W = imgs.shape
+        if self.bf16:
+            return self._forward_bf16(net, imgs, out_hw, train, out)
         ws = self._workspace(N, H, W, imgs.device)
         # conv1 7x7/2 -> bn1 -> relu -> maxpool (children 0-3)
         H1, W1, rows = self._conv("conv1", imgs, net.conv1, ws["y1"], N, H, W, train, nchw=True)

@@ -575,10 +575,59 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
   return 0;
 }
 
+namespace {
+// CAPMI_GEMM_BF16_IO: bf16 A / B / C (gemm_bf16.hip), plain conv / dense GEMM with BN statistics
+int gemm_bf16_io(const capmi_gemm_problem* prob, int amode, int bmode, int tile, void* workspace,
+                 long long ws_bytes, hipStream_t s) {
+  CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
+  const capmi_gemm_problem& p = *prob;
+  CAPMI_REQUIRE(bmode == CAPMI_B_NMAJOR_W && (amode == CAPMI_A_KMAJOR || amode == CAPMI_A_CONV_NHWC), CAPMI_EINVAL);
+  CAPMI_REQUIRE(p.A && p.B && p.C && p.M >= 0 && p.N > 0 && p.K > 0 && p.K % 64 == 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE(p.ksplit == 1 && !p.in_scale && !p.in_shift && !p.bias && !p.bias2 && !p.alpha_ptr &&
+                    p.alpha == 1.f && p.beta == 0.f && !p.relu && p.a_r1 <= 0 && p.c_r1 <= 0,
+                CAPMI_EINVAL);
+  CAPMI_REQUIRE(aligned16(p.A) && aligned16(p.B) && p.ldb % 8 == 0 && p.ldb >= p.K && p.ldc >= p.N, CAPMI_EALIGN);
+  CAPMI_REQUIRE((long long)p.N * p.ldb * 2 < (1LL << 31), CAPMI_ERANGE);
+  if (amode == CAPMI_A_CONV_NHWC) {
+    CAPMI_REQUIRE(p.cCin % 64 == 0 && p.K == p.cKH * p.cKW * p.cCin && p.M == p.cN * p.cHo * p.cWo, CAPMI_EINVAL);
+    CAPMI_REQUIRE((long long)p.cN * p.cH * p.cW * p.cCin * 2 < (1LL << 31), CAPMI_ERANGE);
+  } else {
+    CAPMI_REQUIRE(p.lda % 8 == 0 && p.lda >= p.K, CAPMI_EALIGN);
+    CAPMI_REQUIRE((long long)p.M * p.lda * 2 < (1LL << 31), CAPMI_ERANGE);
+  }
+  if (p.M == 0) return 0;
+  const int bm = 128, bn = (tile == CAPMI_TILE_128x64 || tile == CAPMI_TILE_64 || (tile == CAPMI_TILE_AUTO && p.N <= 64)) ? 64 : 128;
+  GemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.nprob = 1;
+  a.p[0] = p;
+  a.tiles_m[0] = (int)cdiv(p.M, bm);
+  a.tiles_n[0] = (int)cdiv(p.N, bn);
+  const long long total = (long long)a.tiles_m[0] * a.tiles_n[0];
+  a.tiles_begin[1] = (int)total;
+  const int cus = cu_count();
+  const long long slots = (long long)cus * 2;
+  const int nkt = p.K / 64;
+  const long long rounds = (total + slots - 1) / slots;
+  const bool sk = workspace != nullptr && nkt >= 4 && (double)total / (double)(rounds * slots) < 0.9;
+  if (!sk) return gemm_bf16_launch(a, amode, bm, bn, (int)total, s);
+  CAPMI_REQUIRE(aligned16(workspace), CAPMI_EINVAL);
+  CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
+  a.sk_nkt = nkt;
+  a.sk_units = total * nkt;
+  a.sk_workers = (int)std::min<long long>(slots, a.sk_units);
+  a.sk_groups = sk_xcd_groups() && a.sk_workers % 8 == 0 && total >= 64 ? 8 : 1;
+  a.sk_flags = static_cast<int*>(workspace);
+  a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
+  return gemm_bf16_launch(a, amode, bm, bn, a.sk_workers, s);
+}
+}  // namespace
+
 extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int bmode, int tile, int flags,
                                 void* workspace, long long ws_bytes, void* stream) {
   GemmPlan g;
   bool sk = false;
+  if (flags == CAPMI_GEMM_BF16_IO) return gemm_bf16_io(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
   CAPMI_REQUIRE((flags & ~CAPMI_GEMM_BF16) == 0, CAPMI_EINVAL);
   const bool bf16 = (flags & CAPMI_GEMM_BF16) != 0;
   const int rc = sk_decide(prob, amode, bmode, tile, g, sk);

@@ -28,5 +28,7 @@ __device__ __forceinline__ long long remap(long long r, long long r1, long long 
 // BM x BN in {128x128, 128x64, 64x64}
 int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int blocks, hipStream_t s,
                    bool bf16 = false);
+// bf16-in/bf16-out conv GEMM (gemm_bf16.hip): BM = 128, BN in {128, 64}, amode 0 (dense) / 2 (conv)
+int gemm_bf16_launch(const GemmArgs& a, int amode, int bm, int bn, int blocks, hipStream_t s);
 // resident workgroups per CU of the NT kernel for a tile shape (LDS / register bound)
 inline int gemm_nt_wg_per_cu(int bm, int bn) { return bm == 64 && bn == 64 ? 4 : 2; }

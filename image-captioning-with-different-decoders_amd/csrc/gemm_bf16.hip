@@ -1,0 +1,471 @@
+// bf16-in / bf16-out implicit-GEMM convolution for the bf16 configuration (BASELINE config 5):
+// activations and packed conv weights are bf16 in HBM, products on v_mfma_f32_32x32x16_bf16 with
+// fp32 accumulation, the output rounded to bf16 (RNE) once, train-mode BN statistics in fp32 from
+// the stored (rounded) values. Replaces the Conv2d calls of torchvision's ResNet-101
+// (models/encoder.py:88-91,107) when the encoder runs in bf16.
+//
+// vs the fp32 kernel (gemm_nt.hip), whose structure (2x2 waves, two register prefetch stages,
+// LDS double buffer, stream-K hand-off, XCD groups, slice statistics) it keeps:
+//   * BK = 64 (K % 64 == 0: every ResNet conv but conv1, Cin % 64 == 0, so a k-tile never
+//     straddles a (kh, kw) tap); one 16-B load = 8 consecutive k of one row;
+//   * loads are raw buffer loads over the whole operand: a masked slot (padding tap, row >= M)
+//     gets an offset past the buffer's end and reads zeros, so there is no select, no 64-bit
+//     address arithmetic and no prologue VALU between the loads and the LDS stores (the BN
+//     apply + ReLU of the conv input is materialised once per tensor: capmi_bn_relu_bf16);
+//   * LDS rows of 72 bf16 (144 B): the 16-lane groups of ds_read_b128 / 8-lane groups of
+//     ds_write_b128 hit 64 distinct banks; lane (r, h) reads k 16g+8h..+7 of row r, the operand
+//     layout of the 32x32x16 bf16 MFMA;
+//   * tiles 128x128 (wave 64x64: 4 MFMAs per 4 ds_read_b128) or 128x64.
+#include "gemm_args.h"
+
+namespace {
+
+constexpr int BKH = 64;      // k per tile (bf16 elements)
+constexpr int SBH = BKH + 8;  // LDS row stride (elements)
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+constexpr unsigned kOOB = 0x80000000u;  // buffer offset past every operand: the load returns 0
+constexpr int kSc1h = 16;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ unsigned short bf16_bits(float x) {
+  return __builtin_bit_cast(unsigned short, (__bf16)x);  // RNE
+}
+__device__ __forceinline__ float bf16_val(unsigned short b) {
+  return __uint_as_float((unsigned)b << 16);
+}
+
+template <int BM, int BN, int AMODE, bool SK>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+gemm_bf16_kernel(const GemmArgs args) {
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
+  constexpr int NA = BM * BKH / 8 / 256, NB = BN * BKH / 8 / 256;
+  static_assert(NA >= 1 && NB >= 1 && WM == 64, "tile");
+  __shared__ __attribute__((aligned(16))) __bf16 As[2][BM * SBH];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BN * SBH];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int kc = (tid & 7) * 8;  // k offset of this thread's 16-B chunk inside a k-tile
+
+  f32x16 acc[TM][TN];
+
+  auto mainloop = [&](const capmi_gemm_problem& P, int m0, int n0, int k_lo, int k_hi) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int nkt = (k_hi - k_lo) / BKH;
+    if (nkt <= 0) return;
+    const int M = P.M, N = P.N;
+    const int cH = P.cH, cW = P.cW, cCin = P.cCin, cKW = P.cKW;
+    const unsigned a_bytes = AMODE == 2 ? (unsigned)((long long)P.cN * cH * cW * cCin * 2)
+                                        : (unsigned)((long long)M * P.lda * 2);
+    const auto ra = rsrc_of(P.A, a_bytes);
+    const auto rb = rsrc_of(P.B, (unsigned)((long long)N * P.ldb * 2));
+    // per-slot row state
+    unsigned a_off[NA];  // dense: byte offset of (row, kc); conv: element offset of the image
+    int a_ih0[NA], a_iw0[NA];
+    bool a_ok[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int row = m0 + ((tid + i * 256) >> 3);
+      a_ok[i] = row < M;
+      if (AMODE == 0) {
+        a_off[i] = a_ok[i] ? (unsigned)(((long long)row * P.lda + kc) * 2) : kOOB;
+        a_ih0[i] = a_iw0[i] = 0;
+      } else {
+        const int hw = P.cHo * P.cWo;
+        const int rr = a_ok[i] ? row : 0;
+        const int n = rr / hw, rem = rr - n * hw;
+        const int oh = rem / P.cWo, ow = rem - oh * P.cWo;
+        a_ih0[i] = oh * P.cStride - P.cPad;
+        a_iw0[i] = ow * P.cStride - P.cPad;
+        a_off[i] = (unsigned)(n * cH * cW);  // pixel index of the image's (0, 0)
+      }
+    }
+    unsigned b_off[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int n = n0 + ((tid + i * 256) >> 3);
+      b_off[i] = n < N ? (unsigned)(((long long)n * P.ldb + kc) * 2) : kOOB;
+    }
+    int c_ci = 0, c_kh = 0, c_kw = 0;  // conv k walk, advanced BKH per k-tile
+    if (AMODE == 2) {
+      const int kpos = k_lo / cCin;
+      c_ci = k_lo - kpos * cCin;
+      c_kh = kpos / cKW;
+      c_kw = kpos - c_kh * cKW;
+    }
+
+    struct Stage {
+      u32x4_t ra[NA], rb[NB];
+    };
+    auto load_tile = [&](Stage& st, int kt) {
+      const int k = k_lo + kt * BKH;
+      const bool kok = k < k_hi;
+      if (AMODE == 0) {
+#pragma unroll
+        for (int i = 0; i < NA; ++i)
+          st.ra[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, kok ? a_off[i] + (unsigned)k * 2 : kOOB, 0, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+          const int ih = a_ih0[i] + c_kh, iw = a_iw0[i] + c_kw;
+          const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
+          const unsigned off = ((a_off[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + kc)) * 2u;
+          st.ra[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off : kOOB, 0, 0);
+        }
+        c_ci += BKH;
+        if (c_ci >= cCin) {
+          c_ci = 0;
+          if (++c_kw == cKW) {
+            c_kw = 0;
+            ++c_kh;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        st.rb[i] = __builtin_amdgcn_raw_buffer_load_b128(rb, kok ? b_off[i] + (unsigned)k * 2 : kOOB, 0, 0);
+    };
+    auto store_tile = [&](const Stage& st, int buf) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i)
+        *reinterpret_cast<u32x4_t*>(&As[buf][((tid + i * 256) >> 3) * SBH + kc]) = st.ra[i];
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        *reinterpret_cast<u32x4_t*>(&Bs[buf][((tid + i * 256) >> 3) * SBH + kc]) = st.rb[i];
+    };
+    auto compute = [&](int buf) {
+      const __bf16* Ah = &As[buf][(wm0 + lr) * SBH + 8 * lh];
+      const __bf16* Bh = &Bs[buf][(wn0 + lr) * SBH + 8 * lh];
+#pragma unroll
+      for (int g = 0; g < BKH / 16; ++g) {
+        bf16x8_t a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const bf16x8_t*>(Ah + 32 * i * SBH + 16 * g);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const bf16x8_t*>(Bh + 32 * j * SBH + 16 * g);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+    };
+    auto kstep = [&](Stage& ld, const Stage& sv, int kt) {
+      load_tile(ld, kt + 2);
+      compute(kt & 1);
+      store_tile(sv, (kt + 1) & 1);
+      __syncthreads();
+    };
+    Stage s0, s1;
+    load_tile(s0, 0);
+    store_tile(s0, 0);
+    load_tile(s1, 1);
+    __syncthreads();
+    // back edge only from the second k-step (see gemm_nt.hip: keeps the prefetch two deep)
+    int kt = 0;
+    for (; kt + 1 < nkt; kt += 2) {
+      kstep(s0, s1, kt);
+      kstep(s1, s0, kt + 1);
+    }
+    if (kt < nkt) kstep(s0, s1, kt);
+  };
+
+  // epilogue: round to bf16, store, per-channel (sum, sumsq) of the stored values per 64-row slice
+  auto epilogue = [&](const capmi_gemm_problem& P, int tm, int tn) {
+    const int M = P.M, N = P.N;
+    const int m0 = tm * BM, n0 = tn * BN;
+    unsigned short* C = reinterpret_cast<unsigned short*>(P.C);
+    const long long ldc = P.ldc;
+    float csum[TN], csq[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      csum[j] = 0.f;
+      csq[j] = 0.f;
+      const int col = n0 + wn0 + 32 * j + lr;
+      const bool cok = col < N;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (cok && row < M) {
+            const unsigned short h = bf16_bits(acc[i][j][r]);
+            C[(long long)row * ldc + col] = h;
+            const float v = bf16_val(h);
+            csum[j] += v;
+            csq[j] = fmaf(v, v, csq[j]);
+          }
+        }
+      }
+    }
+    float* __restrict__ stats = P.stats;
+    if (stats != nullptr) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        csum[j] += __shfl_xor(csum[j], 32, 64);
+        csq[j] += __shfl_xor(csq[j], 32, 64);
+      }
+      if (lh == 0) {  // WM == 64: each wave row owns one 64-row slice
+        const long long sl = (m0 + wm0) >> 6;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = n0 + wn0 + 32 * j + lr;
+          if (col < N && m0 + wm0 < M) {
+            stats[(sl * N + col) * 2 + 0] = csum[j];
+            stats[(sl * N + col) * 2 + 1] = csq[j];
+          }
+        }
+      }
+    }
+  };
+
+  if (!SK) {
+    int bid = blockIdx.x;
+    {  // XCD-aware remap (bijective for any grid size): consecutive tiles on one XCD
+      const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = bid & 7;
+      bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+    }
+    const capmi_gemm_problem& P = args.p[0];
+    const int tiles_n = args.tiles_n[0];
+    const int tn = bid % tiles_n, tm = bid / tiles_n;
+    mainloop(P, tm * BM, tn * BN, 0, P.K);
+    epilogue(P, tm, tn);
+    return;
+  }
+
+  // stream-K over (tile, k-tile) units, XCD groups: as gemm_nt.hip (the same hand-off protocol)
+  const capmi_gemm_problem& P = args.p[0];
+  const int nkt = args.sk_nkt, tiles_n = args.tiles_n[0];
+  const long long ngrp = args.sk_groups, grp = blockIdx.x % ngrp;
+  const long long T = args.sk_units / nkt, G = gridDim.x / ngrp, w = blockIdx.x / ngrp;
+  const long long ub = grp * T / ngrp * nkt, U = ((grp + 1) * T / ngrp) * nkt - ub;
+  const long long u0 = ub + w * U / G, u1 = ub + (w + 1) * U / G;
+  if (u0 >= u1) return;
+  constexpr int PART = BM * BN;
+  int* flags = args.sk_flags;
+  for (long long t = (u1 - 1) / nkt; t >= u0 / nkt; --t) {
+    const long long tb = t * nkt;
+    const int ks = (int)(max(u0, tb) - tb), ke = (int)(min(u1, tb + nkt) - tb);
+    const int tm = (int)(t / tiles_n), tn = (int)(t % tiles_n);
+    mainloop(P, tm * BM, tn * BN, ks * BKH, ke * BKH);
+    if (ke < nkt) {
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + (long long)blockIdx.x * PART, 0,
+                                                        PART * 4, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            u32x4_t v;
+            v.x = __float_as_uint(acc[i][j][4 * q + 0]);
+            v.y = __float_as_uint(acc[i][j][4 * q + 1]);
+            v.z = __float_as_uint(acc[i][j][4 * q + 2]);
+            v.w = __float_as_uint(acc[i][j][4 * q + 3]);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (((i * TN + j) * 4 + q) * 256 + tid) * 16, 0, kSc1h);
+          }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(flags + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      continue;
+    }
+    if (ks > 0) {
+      for (long long w2 = w - 1;; --w2) {
+        const long long b2 = w2 * ngrp + grp;
+        if (tid == 0) {
+          int spins = 0;
+          while (__hip_atomic_load(flags + b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+                 ++spins < (1 << 22))
+            __builtin_amdgcn_s_sleep(2);
+          if (spins >= (1 << 22)) flags[gridDim.x] = 1;  // never expected: report instead of hanging
+          __hip_atomic_store(flags + b2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + b2 * PART, 0, PART * 4, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs, (((i * TN + j) * 4 + q) * 256 + tid) * 16, 0, kSc1h);
+              acc[i][j][4 * q + 0] += __uint_as_float(v.x);
+              acc[i][j][4 * q + 1] += __uint_as_float(v.y);
+              acc[i][j][4 * q + 2] += __uint_as_float(v.z);
+              acc[i][j][4 * q + 3] += __uint_as_float(v.w);
+            }
+        if (ub + w2 * U / G <= tb) break;
+      }
+    }
+    epilogue(P, tm, tn);
+  }
+}
+
+template <int BM, int BN>
+void launch_bf16(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
+  const dim3 g(blocks), b(256);
+  const bool sk = a.sk_workers > 0;
+  if (amode == 2) {
+    if (sk)
+      hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, 2, true>), g, b, 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, 2, false>), g, b, 0, s, a);
+  } else {
+    if (sk)
+      hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, 0, true>), g, b, 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, 0, false>), g, b, 0, s, a);
+  }
+}
+
+// ---- elementwise: the bf16 activations around the convs ---------------------------------------
+
+// x = relu(y * scale[c] + shift[c]) (bf16 -> bf16): the materialised conv input
+__global__ void bn_relu_bf16_kernel(const uint4* __restrict__ y, const float* __restrict__ sc,
+                                    const float* __restrict__ sh, long long n8, int C, uint4* __restrict__ x) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const uint4 v = y[i];
+    const int c0 = (int)((i * 8) % C);
+    const unsigned in[4] = {v.x, v.y, v.z, v.w};
+    unsigned o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float lo = fmaxf(fmaf(__uint_as_float(in[q] << 16), sc[c0 + 2 * q], sh[c0 + 2 * q]), 0.f);
+      const float hi = fmaxf(fmaf(__uint_as_float(in[q] & 0xffff0000u), sc[c0 + 2 * q + 1], sh[c0 + 2 * q + 1]), 0.f);
+      o[q] = (unsigned)bf16_bits(lo) | ((unsigned)bf16_bits(hi) << 16);
+    }
+    x[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// out = relu(y*s + b + res'), res' = res or res*rs + rb (downsample BN): the bottleneck tail
+__global__ void bn_add_relu_bf16_kernel(const uint4* __restrict__ y, const float* __restrict__ s,
+                                        const float* __restrict__ b, const uint4* __restrict__ res,
+                                        const float* __restrict__ rs, const float* __restrict__ rb,
+                                        long long n8, int C, uint4* __restrict__ out) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const uint4 v = y[i], r = res[i];
+    const int c0 = (int)((i * 8) % C);
+    const unsigned yv[4] = {v.x, v.y, v.z, v.w}, rv[4] = {r.x, r.y, r.z, r.w};
+    unsigned o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float e[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = c0 + 2 * q + h;
+        const float yy = __uint_as_float(h ? (yv[q] & 0xffff0000u) : (yv[q] << 16));
+        float rr = __uint_as_float(h ? (rv[q] & 0xffff0000u) : (rv[q] << 16));
+        if (rs != nullptr) rr = fmaf(rr, rs[c], rb[c]);
+        e[h] = fmaxf(fmaf(yy, s[c], b[c]) + rr, 0.f);
+      }
+      o[q] = (unsigned)bf16_bits(e[0]) | ((unsigned)bf16_bits(e[1]) << 16);
+    }
+    out[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// fp32 -> bf16 (RNE), n % 8 == 0
+__global__ void f32_to_bf16_kernel(const float4* __restrict__ in, long long n8, uint4* __restrict__ out) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const float4 a = in[2 * i], c = in[2 * i + 1];
+    out[i] = make_uint4((unsigned)bf16_bits(a.x) | ((unsigned)bf16_bits(a.y) << 16),
+                        (unsigned)bf16_bits(a.z) | ((unsigned)bf16_bits(a.w) << 16),
+                        (unsigned)bf16_bits(c.x) | ((unsigned)bf16_bits(c.y) << 16),
+                        (unsigned)bf16_bits(c.z) | ((unsigned)bf16_bits(c.w) << 16));
+  }
+}
+
+// AdaptiveAvgPool2d(OH, OW) of a bf16 NHWC map -> fp32 NHWC (the encoder output)
+__global__ void adaptive_avgpool_bf16_kernel(const unsigned short* __restrict__ x, int N, int H, int W, int C,
+                                             int OH, int OW, float* __restrict__ out) {
+  const long long total = (long long)N * OH * OW * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    long long r = i / C;
+    const int ow = (int)(r % OW);
+    r /= OW;
+    const int oh = (int)(r % OH);
+    const int n = (int)(r / OH);
+    const int h0 = oh * H / OH, h1 = ((oh + 1) * H + OH - 1) / OH;
+    const int w0 = ow * W / OW, w1 = ((ow + 1) * W + OW - 1) / OW;
+    float acc = 0.f;
+    for (int h = h0; h < h1; ++h)
+      for (int w = w0; w < w1; ++w) acc += bf16_val(x[(((long long)n * H + h) * W + w) * C + c]);
+    out[i] = acc / (float)((h1 - h0) * (w1 - w0));
+  }
+}
+
+unsigned grid_for(long long n) { return (unsigned)std::min<long long>(std::max<long long>(cdiv(n, 256), 1), 8192); }
+
+}  // namespace
+
+int gemm_bf16_launch(const GemmArgs& a, int amode, int bm, int bn, int blocks, hipStream_t s) {
+  if (bm == 128 && bn == 128)
+    launch_bf16<128, 128>(a, amode, blocks, s);
+  else if (bm == 128 && bn == 64)
+    launch_bf16<128, 64>(a, amode, blocks, s);
+  else
+    return CAPMI_EINVAL;
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int capmi_bn_relu_bf16(const void* y, const float* scale, const float* shift, long long rows, int C,
+                                  void* x, void* stream) {
+  CAPMI_REQUIRE(y && scale && shift && x && rows >= 0 && C > 0 && C % 8 == 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE(aligned16(y) && aligned16(x), CAPMI_EALIGN);
+  const long long n8 = rows * C / 8;
+  if (n8 == 0) return 0;
+  hipLaunchKernelGGL(bn_relu_bf16_kernel, dim3(grid_for(n8)), dim3(256), 0, as_stream(stream),
+                     static_cast<const uint4*>(y), scale, shift, n8, C, static_cast<uint4*>(x));
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int capmi_bn_add_relu_bf16(const void* y, const float* scale, const float* shift, const void* res,
+                                      const float* res_scale, const float* res_shift, long long rows, int C,
+                                      void* out, void* stream) {
+  CAPMI_REQUIRE(y && scale && shift && res && out && rows >= 0 && C > 0 && C % 8 == 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE((res_scale == nullptr) == (res_shift == nullptr), CAPMI_EINVAL);
+  CAPMI_REQUIRE(aligned16(y) && aligned16(res) && aligned16(out), CAPMI_EALIGN);
+  const long long n8 = rows * C / 8;
+  if (n8 == 0) return 0;
+  hipLaunchKernelGGL(bn_add_relu_bf16_kernel, dim3(grid_for(n8)), dim3(256), 0, as_stream(stream),
+                     static_cast<const uint4*>(y), scale, shift, static_cast<const uint4*>(res), res_scale,
+                     res_shift, n8, C, static_cast<uint4*>(out));
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int capmi_f32_to_bf16(const float* in, long long n, void* out, void* stream) {
+  CAPMI_REQUIRE(in && out && n >= 0 && n % 8 == 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE(aligned16(in) && aligned16(out), CAPMI_EALIGN);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(grid_for(n / 8)), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const float4*>(in), n / 8, static_cast<uint4*>(out));
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int capmi_adaptive_avgpool_bf16(const void* x, int N, int H, int W, int C, int OH, int OW, float* out,
+                                           void* stream) {
+  CAPMI_REQUIRE(x && out && N >= 0 && H > 0 && W > 0 && C > 0 && OH > 0 && OW > 0, CAPMI_EINVAL);
+  const long long total = (long long)N * OH * OW * C;
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(adaptive_avgpool_bf16_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
+                     static_cast<const unsigned short*>(x), N, H, W, C, OH, OW, out);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}

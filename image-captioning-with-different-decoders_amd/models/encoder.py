@@ -122,8 +122,9 @@ class EncoderAttention(nn.Module):
         self._runner = EncoderRunner()
 
     def set_compute_precision(self, precision):
-        """'fp32' (the reference's) or 'bf16': bf16 MFMA for the frozen forward convs (fp32
-        accumulation, activations and BatchNorm stay fp32) -- the bf16 config (BASELINE config 5)."""
+        """'fp32' (the reference's) or 'bf16': the frozen forward on bf16 NHWC activations and
+        weights, bf16 MFMA with fp32 accumulation and fp32 BatchNorm statistics, features returned
+        fp32 -- the bf16 config (BASELINE config 5)."""
         if precision not in ("fp32", "bf16"):
             raise ValueError(precision)
         self._runner.bf16 = precision == "bf16"

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 6
+#define CAPMI_ABI_VERSION 7
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -99,6 +99,13 @@ int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int t
  * (CAPMI_A_KMAJOR / CAPMI_A_CONV_NHWC / CAPMI_A_CONV_NHWC4) x B = W[N][K] (CAPMI_B_NMAJOR_W) only.
  * Inputs, outputs, statistics and the prologue stay fp32. */
 #define CAPMI_GEMM_BF16 1
+/* CAPMI_GEMM_BF16_IO (alone): A, B and C are bf16 buffers (the float* fields carry bf16 pointers;
+ * leading dimensions in elements), v_mfma_f32_32x32x16_bf16 with fp32 accumulation, C rounded to bf16
+ * (RNE) once, `stats` fp32 from the stored values. A = CAPMI_A_KMAJOR (lda % 8 == 0) or
+ * CAPMI_A_CONV_NHWC (Cin % 64 == 0) x B = W[N][K] (CAPMI_B_NMAJOR_W, ldb % 8 == 0); K % 64 == 0;
+ * alpha 1, beta 0, no bias / relu / prologue / ksplit (the bf16 encoder materialises the conv
+ * input with capmi_bn_relu_bf16). Tile 128x128, or 128x64 for CAPMI_TILE_128x64 / N <= 64. */
+#define CAPMI_GEMM_BF16_IO 2
 int capmi_gemm_sk_ex(const capmi_gemm_problem* problem, int amode, int bmode, int tile, int flags, void* workspace,
                      long long ws_bytes, void* stream);
 /* the launch capmi_gemm_sk would make (no GPU work): tile bm x bn, stream_k 0/1, generic = 1
@@ -142,6 +149,20 @@ int capmi_bn_finalize(const float* stats, int tiles, int C, long long count, con
 int capmi_bn_eval_params(const float* gamma, const float* beta, const float* running_mean,
                          const float* running_var, int C, float eps, float* scale, float* shift,
                          void* stream);
+/* bf16 activations (the bf16 encoder of BASELINE config 5, capmi_gemm_sk_ex + CAPMI_GEMM_BF16_IO):
+ * x = relu(y*scale[c] + shift[c]) on a bf16 NHWC tensor of rows x C (C % 8 == 0): the BN-apply+ReLU
+ * of a conv input, materialised once (models/encoder.py:88-91 via torchvision's Bottleneck) */
+int capmi_bn_relu_bf16(const void* y, const float* scale, const float* shift, long long rows, int C, void* x,
+                       void* stream);
+/* bf16 bottleneck tail: out = relu(y*s + b + (res_scale ? res*rs + rb : res)) */
+int capmi_bn_add_relu_bf16(const void* y, const float* scale, const float* shift, const void* res,
+                           const float* res_scale, const float* res_shift, long long rows, int C, void* out,
+                           void* stream);
+/* fp32 -> bf16 (RNE), n % 8 == 0 (layer1 input, packed conv weights) */
+int capmi_f32_to_bf16(const float* in, long long n, void* out, void* stream);
+/* AdaptiveAvgPool2d((OH, OW)) of a bf16 NHWC map -> fp32 NHWC (models/encoder.py:92,108-109) */
+int capmi_adaptive_avgpool_bf16(const void* x, int N, int H, int W, int C, int OH, int OW, float* out,
+                                void* stream);
 /* Bottleneck tail: out = relu(y*s + b + (res_scale ? res*rs + rb : res)), NHWC, C % 4 == 0 */
 int capmi_bn_add_relu(const float* y, const float* s, const float* b, const float* res,
                       const float* res_scale, const float* res_shift, float* out, long long rows,

@@ -43,10 +43,13 @@ def test_bf16_conv_gemm_exact_on_rounded_operands(N, H, Cin, Cout, k, s, pro, ti
     ref = F.conv2d(_bf(a), _bf(w).permute(0, 3, 1, 2), stride=s, padding=pad).permute(0, 2, 3, 1)
     out = torch.empty(N, Ho, Ho, Cout, device=DEV)
     geo = dict(N=N, H=H, W=H, Cin=Cin, KH=k, KW=k, stride=s, pad=pad, Ho=Ho, Wo=Ho)
-    prob = K.problem(N * Ho * Ho, Cout, k * k * Cin, x.float().to(DEV), 0, w.float().to(DEV).contiguous(),
-                     k * k * Cin, out, Cout, conv=geo, in_scale=sc.float().to(DEV) if pro else None,
-                     in_shift=sh.float().to(DEV) if pro else None)
-    K.gemm_sk(prob, CAPMI_A_CONV_NHWC, K.gemm_workspace(DEV), tile, bf16=True)
+    # device operands bound to names: the problem holds raw pointers, and the workspace allocation
+    # below would otherwise be free to reuse a temporary's memory before the launch
+    xd, wd, ws = x.float().to(DEV), w.float().to(DEV).contiguous(), K.gemm_workspace(DEV)
+    scd, shd = (sc.float().to(DEV), sh.float().to(DEV)) if pro else (None, None)
+    prob = K.problem(N * Ho * Ho, Cout, k * k * Cin, xd, 0, wd, k * k * Cin, out, Cout, conv=geo, in_scale=scd,
+                     in_shift=shd)
+    K.gemm_sk(prob, CAPMI_A_CONV_NHWC, ws, tile, bf16=True)
     torch.cuda.synchronize()
     assert rel_err(out, ref) < 1e-5, rel_err(out, ref)
 
@@ -79,8 +82,9 @@ def test_bf16_dense_and_conv1_modes():
 
 
 def test_bf16_encoder_vs_oracle():
-    """Whole frozen ResNet-101 forward with bf16 convs vs the fp64 oracle. Each conv rounds its
-    operands to 8 significant bits (rel. 2^-9); over 104 convs the features stay at the 1e-2
+    """Whole frozen ResNet-101 forward in bf16 (bf16 NHWC activations and weights: every conv
+    input, conv output and block output is rounded to 8 significant bits, rel. 2^-9, about 5
+    roundings per bottleneck) vs the fp64 oracle; over 104 convs the features stay at the 1e-2
     level when the network is well conditioned: eval-mode BN, and train-mode BN with the residual
     branches' last BN scaled down (bn3.weight x 0.1, the regime of trained ResNets and of
     torchvision's zero_init_residual). With gamma ~ U(0.5, 1.5) everywhere, train-mode BN at
@@ -97,7 +101,7 @@ def test_bf16_encoder_vs_oracle():
     enc = _encoder(params)
     enc.set_compute_precision("bf16")
     x = gen.images(71, 2)
-    for mode, bound in (("eval", 1e-2), ("train", 3e-2)):
+    for mode, bound in (("eval", 2e-2), ("train", 6e-2)):
         r64 = build_resnet101(params).double()
         enc.train(mode == "train")
         r64.train(mode == "train")

@@ -15,7 +15,8 @@ from capmi._lib import CAPMI_A_CONV_NHWC, CAPMI_A_KMAJOR  # noqa: E402
 SHAPES = {  # name: (Cin, H, W, Cout, k, prologue)
     "l3c2": (256, 14, 14, 256, 3, True), "l3c3": (256, 14, 14, 1024, 1, True),
     "l3c1": (1024, 14, 14, 256, 1, False), "l1c2": (64, 56, 56, 64, 3, True),
-    "l1c3": (64, 56, 56, 256, 1, True)}
+    "l1c3": (64, 56, 56, 256, 1, True), "l4c2": (512, 7, 7, 512, 3, True), "l2c2": (128, 28, 28, 128, 3, True),
+    "l1c2s": (64, 56, 56, 64, 3, True)}
 
 
 def main():
@@ -25,6 +26,7 @@ def main():
     ap.add_argument("--tile", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--bf16", action="store_true")
+    ap.add_argument("--bf16io", action="store_true", help="bf16 activations/weights/output (CAPMI_GEMM_BF16_IO)")
     ap.add_argument("--nopro", action="store_true", help="drop the BN-apply+ReLU prologue (1x1: dense A)")
     a = ap.parse_args()
     dev = "cuda"
@@ -47,13 +49,24 @@ def main():
                          in_scale=sc if pro else None, in_shift=sh if pro else None)
         mode = CAPMI_A_CONV_NHWC
     ws = K.gemm_workspace(dev)
-    print("plan (bm, bn, stream_k, generic):", K.gemm_sk_plan(prob, mode, a.tile))
+    if a.bf16io:
+        xb, wb = x.to(torch.bfloat16), w.to(torch.bfloat16)
+        yb = torch.empty(M, co, device=dev, dtype=torch.bfloat16)
+        if k == 1:
+            prob, mode = K.problem_bf16(M, co, Kd, xb, ci, wb, Kd, yb, co, stats=stats), CAPMI_A_KMAJOR
+        else:
+            prob = K.problem_bf16(M, co, Kd, xb, 0, wb, Kd, yb, co, stats=stats, conv=geo)
+            mode = CAPMI_A_CONV_NHWC
+        run = lambda: K.gemm_bf16(prob, mode, ws, a.tile)  # noqa: E731
+    else:
+        print("plan (bm, bn, stream_k, generic):", K.gemm_sk_plan(prob, mode, a.tile))
+        run = lambda: K.gemm_sk(prob, mode, ws, a.tile, bf16=a.bf16)  # noqa: E731
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    K.gemm_sk(prob, mode, ws, a.tile, bf16=a.bf16)
+    run()
     torch.cuda.synchronize()
     s.record()
     for _ in range(a.reps):
-        K.gemm_sk(prob, mode, ws, a.tile, bf16=a.bf16)
+        run()
     e.record()
     torch.cuda.synchronize()
     us = s.elapsed_time(e) * 1e3 / a.reps
