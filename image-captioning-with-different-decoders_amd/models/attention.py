@@ -169,8 +169,11 @@ def train(device, args):
         decoder.fine_tune_embeddings(args.fine_tune_embedding)
         start_epoch, metrics, opt_state = 0, {}, None
     else:
-        chkpt = load_checkpoint(device, args)
+        chkpt = load_checkpoint(device, args, weights_only=not getattr(args, 'trusted_checkpoint', False))
         start_epoch, enc_sd, dec_sd, enc_opt_state, opt_state, metrics = unpack_checkpoint(chkpt)
+        # whole-module checkpoints (save_checkpoint(..., whole_modules=True), the reference's format)
+        enc_sd, dec_sd, enc_opt_state, opt_state = (
+            v.state_dict() if hasattr(v, 'state_dict') else v for v in (enc_sd, dec_sd, enc_opt_state, opt_state))
         start_epoch += 1
         encoder = EncoderAttention()
         encoder.load_state_dict(enc_sd)

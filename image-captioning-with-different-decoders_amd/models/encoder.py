@@ -74,6 +74,24 @@ class EncoderFineTuneFn(torch.autograd.Function):
         return (None, None) + tuple(grads.get(id(p)) for p in plist)
 
 
+
+def _runner_free_state(module):
+    """Pickle state of an encoder module without its launch caches (workspaces, packed
+    weights): torch.save(encoder) writes only what the reference's whole-module checkpoints
+    hold (checkpoint.py:39-62); the runner is rebuilt, with its precision, on load."""
+    st = module.__dict__.copy()
+    runner = st.pop("_runner", None)
+    st.pop("_ft_runner", None)
+    st["_capmi_bf16"] = bool(runner is not None and runner.bf16)
+    return st
+
+
+def _runner_restore(module, st):
+    bf16 = st.pop("_capmi_bf16", False)
+    nn.Module.__setstate__(module, st)
+    module._runner = EncoderRunner()
+    module._runner.bf16 = bf16
+
 class Encoder(nn.Module):
     """CNN encoder of the baseline model (reference :22-69)."""
 
@@ -86,6 +104,12 @@ class Encoder(nn.Module):
         for param in self.resnet.parameters():
             param.requires_grad = False
         self._runner = EncoderRunner()
+
+    def __getstate__(self):
+        return _runner_free_state(self)
+
+    def __setstate__(self, st):
+        _runner_restore(self, st)
 
     def forward(self, imgs):
         if not imgs.is_cuda:
@@ -120,6 +144,12 @@ class EncoderAttention(nn.Module):
         for param in self.resnet.parameters():
             param.requires_grad = False
         self._runner = EncoderRunner()
+
+    def __getstate__(self):
+        return _runner_free_state(self)
+
+    def __setstate__(self, st):
+        _runner_restore(self, st)
 
     def set_compute_precision(self, precision):
         """'fp32' (the reference's) or 'bf16': the frozen forward on bf16 NHWC activations and

@@ -46,6 +46,8 @@ def parse_args(argv=None):
                         help='only use captions with caption length <= 50 when training.')
     parser.add_argument('--use_bert', type=bool, default=False, help='whether to use BERT embeddigns for attention model.')
     # capmi additions
+    parser.add_argument('--trusted_checkpoint', type=bool, default=False,
+                        help='--checkpoint is a whole-module pickle you wrote yourself (load with weights_only=False).')
     parser.add_argument('--synthetic', type=bool, default=False, help='COCO-shaped synthetic data.')
     parser.add_argument('--synthetic_size', type=int, default=0, help='samples in the synthetic dataset.')
     parser.add_argument('--vocab_size', type=int, default=8100, help='synthetic vocabulary size.')
