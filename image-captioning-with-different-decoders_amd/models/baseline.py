@@ -1,9 +1,12 @@
 """Baseline LSTM captioner with the reference surface (models/baseline.py:19-374).
 
 BASELINE.json config 1 ("'baseline' LSTM decoder, batch_size 4 ... on CPU;
-plumbing, no GPU"): the decoder is plain nn modules (nn.LSTM / Linear), as in
-the reference; its ResNet-101 encoder (models.encoder.Encoder) runs the capmi
-kernels when given HIP tensors. A GPU baseline decoder is SURVEY.md §8f rank 4.
+plumbing, no GPU"): on CPU tensors the decoder is the plain nn modules (nn.LSTM /
+Linear), as in the reference. On HIP tensors forward()
+is capmi.baseline_fn.BaselineDecoderFn: the same parameters, hoisted input and
+vocabulary GEMMs, the fused LSTM cell per step and a BPTT backward on the capmi
+kernels. The ResNet-101 encoder (models.encoder.Encoder) runs the capmi kernels
+when given HIP tensors.
 """
 import time
 
@@ -42,9 +45,26 @@ class BaselineDecoder(nn.Module):
         for param in self.embedding.parameters():
             param.requires_grad = on
 
+    def _capmi_ws(self, device):
+        """stream-K workspace of the decoder's GEMMs (runtime state: not pickled)."""
+        ws = self.__dict__.get("_capmi_sk")
+        if ws is None or ws.device != torch.device(device):
+            from capmi import kernels as K
+            ws = K.gemm_workspace(device)
+            self.__dict__["_capmi_sk"] = ws
+        return ws
+
+    def __getstate__(self):
+        st = self.__dict__.copy()
+        st.pop("_capmi_sk", None)
+        return st
+
     def forward(self, img_features, captions):
         """(B,M) image features, (B,L) captions -> (B,L,V) scores: the image feature is
         step 0, the caption without <end> follows (reference :81-111)."""
+        if img_features.is_cuda:
+            from capmi.baseline_fn import baseline_forward
+            return baseline_forward(self, img_features, captions)
         captions = captions[:, :-1]
         embeddings = self.embedding(captions)
         embeddings = torch.cat((img_features.unsqueeze(1).float(), embeddings.float()), dim=1)
