@@ -331,50 +331,77 @@ void launch_bf16(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
 
 // ---- elementwise: the bf16 activations around the convs ---------------------------------------
 
+// The two BN kernels below stream 16-B chunks (8 channels) of a [rows][C] bf16 tensor. The grid
+// size in threads is a multiple of C/8 (host: C/8 divides 256), so a thread keeps ONE channel
+// group for its whole grid-stride loop and holds its 8 scales / shifts in registers: per chunk one
+// 16-B load per operand and one 16-B store, no index arithmetic beyond the stride.
+__device__ __forceinline__ void load8(const float* __restrict__ p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ float lo_bf(unsigned w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi_bf(unsigned w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ unsigned pack_bf(float lo, float hi) {
+  return (unsigned)bf16_bits(lo) | ((unsigned)bf16_bits(hi) << 16);
+}
+
 // x = relu(y * scale[c] + shift[c]) (bf16 -> bf16): the materialised conv input
-__global__ void bn_relu_bf16_kernel(const uint4* __restrict__ y, const float* __restrict__ sc,
-                                    const float* __restrict__ sh, long long n8, int C, uint4* __restrict__ x) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+__global__ void __launch_bounds__(256) bn_relu_bf16_kernel(const uint4* __restrict__ y, const float* __restrict__ sc,
+                                                           const float* __restrict__ sh, int n8, int C8,
+                                                           uint4* __restrict__ x) {
+  const int gt = blockIdx.x * 256 + threadIdx.x, stride = gridDim.x * 256;
+  const int c0 = (gt % C8) * 8;
+  float s[8], b[8];
+  load8(sc + c0, s);
+  load8(sh + c0, b);
+  for (int i = gt; i < n8; i += stride) {
     const uint4 v = y[i];
-    const int c0 = (int)((i * 8) % C);
     const unsigned in[4] = {v.x, v.y, v.z, v.w};
     unsigned o[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float lo = fmaxf(fmaf(__uint_as_float(in[q] << 16), sc[c0 + 2 * q], sh[c0 + 2 * q]), 0.f);
-      const float hi = fmaxf(fmaf(__uint_as_float(in[q] & 0xffff0000u), sc[c0 + 2 * q + 1], sh[c0 + 2 * q + 1]), 0.f);
-      o[q] = (unsigned)bf16_bits(lo) | ((unsigned)bf16_bits(hi) << 16);
-    }
+    for (int q = 0; q < 4; ++q)
+      o[q] = pack_bf(fmaxf(fmaf(lo_bf(in[q]), s[2 * q], b[2 * q]), 0.f),
+                     fmaxf(fmaf(hi_bf(in[q]), s[2 * q + 1], b[2 * q + 1]), 0.f));
     x[i] = make_uint4(o[0], o[1], o[2], o[3]);
   }
 }
 
 // out = relu(y*s + b + res'), res' = res or res*rs + rb (downsample BN): the bottleneck tail
-__global__ void bn_add_relu_bf16_kernel(const uint4* __restrict__ y, const float* __restrict__ s,
-                                        const float* __restrict__ b, const uint4* __restrict__ res,
-                                        const float* __restrict__ rs, const float* __restrict__ rb,
-                                        long long n8, int C, uint4* __restrict__ out) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+template <bool RBN>
+__global__ void __launch_bounds__(256) bn_add_relu_bf16_kernel(const uint4* __restrict__ y, const float* __restrict__ s_,
+                                                               const float* __restrict__ b_, const uint4* __restrict__ res,
+                                                               const float* __restrict__ rs_, const float* __restrict__ rb_,
+                                                               int n8, int C8, uint4* __restrict__ out) {
+  const int gt = blockIdx.x * 256 + threadIdx.x, stride = gridDim.x * 256;
+  const int c0 = (gt % C8) * 8;
+  float s[8], b[8], rs[8], rb[8];
+  load8(s_ + c0, s);
+  load8(b_ + c0, b);
+  if (RBN) {
+    load8(rs_ + c0, rs);
+    load8(rb_ + c0, rb);
+  }
+  for (int i = gt; i < n8; i += stride) {
     const uint4 v = y[i], r = res[i];
-    const int c0 = (int)((i * 8) % C);
     const unsigned yv[4] = {v.x, v.y, v.z, v.w}, rv[4] = {r.x, r.y, r.z, r.w};
     unsigned o[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      float e[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int c = c0 + 2 * q + h;
-        const float yy = __uint_as_float(h ? (yv[q] & 0xffff0000u) : (yv[q] << 16));
-        float rr = __uint_as_float(h ? (rv[q] & 0xffff0000u) : (rv[q] << 16));
-        if (rs != nullptr) rr = fmaf(rr, rs[c], rb[c]);
-        e[h] = fmaxf(fmaf(yy, s[c], b[c]) + rr, 0.f);
+      float r0 = lo_bf(rv[q]), r1 = hi_bf(rv[q]);
+      if (RBN) {
+        r0 = fmaf(r0, rs[2 * q], rb[2 * q]);
+        r1 = fmaf(r1, rs[2 * q + 1], rb[2 * q + 1]);
       }
-      o[q] = (unsigned)bf16_bits(e[0]) | ((unsigned)bf16_bits(e[1]) << 16);
+      o[q] = pack_bf(fmaxf(fmaf(lo_bf(yv[q]), s[2 * q], b[2 * q]) + r0, 0.f),
+                     fmaxf(fmaf(hi_bf(yv[q]), s[2 * q + 1], b[2 * q + 1]) + r1, 0.f));
     }
     out[i] = make_uint4(o[0], o[1], o[2], o[3]);
   }
 }
+
+// grid (in 256-thread blocks) for the channel-group kernels: enough blocks for every CU several
+// times over; 256 % C8 == 0 keeps the thread count a multiple of C8
+unsigned grid_c8(long long n8) { return (unsigned)std::min<long long>(std::max<long long>(cdiv(n8, 256), 1), 4096); }
 
 // fp32 -> bf16 (RNE), n % 8 == 0
 __global__ void f32_to_bf16_kernel(const float4* __restrict__ in, long long n8, uint4* __restrict__ out) {
@@ -424,12 +451,13 @@ int gemm_bf16_launch(const GemmArgs& a, int amode, int bm, int bn, int blocks, h
 
 extern "C" int capmi_bn_relu_bf16(const void* y, const float* scale, const float* shift, long long rows, int C,
                                   void* x, void* stream) {
-  CAPMI_REQUIRE(y && scale && shift && x && rows >= 0 && C > 0 && C % 8 == 0, CAPMI_EINVAL);
-  CAPMI_REQUIRE(aligned16(y) && aligned16(x), CAPMI_EALIGN);
+  CAPMI_REQUIRE(y && scale && shift && x && rows >= 0 && C > 0 && C % 8 == 0 && 256 % (C / 8) == 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE(aligned16(y) && aligned16(x) && aligned16(scale) && aligned16(shift), CAPMI_EALIGN);
   const long long n8 = rows * C / 8;
+  CAPMI_REQUIRE(n8 < (1LL << 31), CAPMI_ERANGE);
   if (n8 == 0) return 0;
-  hipLaunchKernelGGL(bn_relu_bf16_kernel, dim3(grid_for(n8)), dim3(256), 0, as_stream(stream),
-                     static_cast<const uint4*>(y), scale, shift, n8, C, static_cast<uint4*>(x));
+  hipLaunchKernelGGL(bn_relu_bf16_kernel, dim3(grid_c8(n8)), dim3(256), 0, as_stream(stream),
+                     static_cast<const uint4*>(y), scale, shift, (int)n8, C / 8, static_cast<uint4*>(x));
   CAPMI_LAUNCH_CHECK();
   return 0;
 }
@@ -437,14 +465,23 @@ extern "C" int capmi_bn_relu_bf16(const void* y, const float* scale, const float
 extern "C" int capmi_bn_add_relu_bf16(const void* y, const float* scale, const float* shift, const void* res,
                                       const float* res_scale, const float* res_shift, long long rows, int C,
                                       void* out, void* stream) {
-  CAPMI_REQUIRE(y && scale && shift && res && out && rows >= 0 && C > 0 && C % 8 == 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE(y && scale && shift && res && out && rows >= 0 && C > 0 && C % 8 == 0 && 256 % (C / 8) == 0,
+                CAPMI_EINVAL);
   CAPMI_REQUIRE((res_scale == nullptr) == (res_shift == nullptr), CAPMI_EINVAL);
-  CAPMI_REQUIRE(aligned16(y) && aligned16(res) && aligned16(out), CAPMI_EALIGN);
+  CAPMI_REQUIRE(aligned16(y) && aligned16(res) && aligned16(out) && aligned16(scale) && aligned16(shift) &&
+                    (res_scale == nullptr || (aligned16(res_scale) && aligned16(res_shift))),
+                CAPMI_EALIGN);
   const long long n8 = rows * C / 8;
+  CAPMI_REQUIRE(n8 < (1LL << 31), CAPMI_ERANGE);
   if (n8 == 0) return 0;
-  hipLaunchKernelGGL(bn_add_relu_bf16_kernel, dim3(grid_for(n8)), dim3(256), 0, as_stream(stream),
-                     static_cast<const uint4*>(y), scale, shift, static_cast<const uint4*>(res), res_scale,
-                     res_shift, n8, C, static_cast<uint4*>(out));
+  if (res_scale)
+    hipLaunchKernelGGL(bn_add_relu_bf16_kernel<true>, dim3(grid_c8(n8)), dim3(256), 0, as_stream(stream),
+                       static_cast<const uint4*>(y), scale, shift, static_cast<const uint4*>(res), res_scale,
+                       res_shift, (int)n8, C / 8, static_cast<uint4*>(out));
+  else
+    hipLaunchKernelGGL(bn_add_relu_bf16_kernel<false>, dim3(grid_c8(n8)), dim3(256), 0, as_stream(stream),
+                       static_cast<const uint4*>(y), scale, shift, static_cast<const uint4*>(res), res_scale,
+                       res_shift, (int)n8, C / 8, static_cast<uint4*>(out));
   CAPMI_LAUNCH_CHECK();
   return 0;
 }
