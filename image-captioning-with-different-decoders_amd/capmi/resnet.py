@@ -202,8 +202,7 @@ class EncoderRunner:
             bm, bn, sk, generic = K.gemm_sk_plan(prob, mode, K.TILE_AUTO)
             b = lambda v: "true" if v else "false"  # noqa: E731
             key = "gemm_kernel (generic)" if generic else \
-                f"gemm_nt_kernel<{bm}, {bn}, {mode}, 0, {b(in_ss is not None and not nchw)}, {b(sk)}" + \
-                (", true>" if bf else ">")
+                f"gemm_nt_kernel<{bm}, {bn}, {mode}, 0, {b(in_ss is not None and not nchw)}, {b(sk)}, {b(bf)}>"
             self.conv_hook(tag, 2.0 * rows * co * Kd, launch, key)
         else:
             launch()
@@ -240,7 +239,13 @@ class EncoderRunner:
             prob, mode = K.problem_bf16(rows, co, Kd, x, 0, w, Kd, out, co, stats=stats, conv=geo), AC
         launch = lambda: K.gemm_bf16(prob, mode, self._ws["sk"], K.TILE_AUTO)  # noqa: E731
         if self.conv_hook is not None:
-            key = f"gemm_bf16_kernel<128, {64 if co <= 64 else 128}, {mode}>"
+            # the launch capmi_gemm_sk_ex makes for CAPMI_GEMM_BF16_IO (gemm.hip: gemm_bf16_io)
+            bn_ = 64 if co <= 64 else 128
+            tiles = -(-rows // 128) * -(-co // bn_)
+            slots = 2 * torch.cuda.get_device_properties(x.device).multi_processor_count
+            rounds = -(-tiles // slots)
+            sk = Kd // 64 >= 4 and tiles / (rounds * slots) < 0.9
+            key = f"gemm_bf16_kernel<128, {bn_}, {mode}, {'true' if sk else 'false'}>"
             self.conv_hook(tag, 2.0 * rows * co * Kd, launch, key)
         else:
             launch()
@@ -533,7 +538,7 @@ class FineTuneRunner:
                 bm, bn, sk, gen = K.gemm_sk_plan(prob, amode, K.TILE_AUTO, bmode)
                 hook(tag, flops, lambda: self._gemm(prob, amode, bmode),
                      f"gemm_nt_kernel<{bm}, {bn}, {amode}, {bmode}, {'true' if prob.in_scale else 'false'}, "
-                     f"{'true' if sk else 'false'}>")
+                     f"{'true' if sk else 'false'}, false>")
 
         K.adaptive_avgpool_bwd_nhwc(dfeat.contiguous(), N, stt["H"], stt["W"], stt["C"], stt["OH"], stt["OW"],
                                     dA[0])
