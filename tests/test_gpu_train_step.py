@@ -123,3 +123,30 @@ def test_pipelined_equals_eager(dropout):
         assert torch.equal(pe[n], pp[n]), n
     for k in re_:
         assert torch.equal(re_[k], rp[k]), k
+
+
+def test_pipelined_graphs_equal_eager():
+    """Pipelined step with both streams replaying captured HIP graphs (the bench default) gives
+    bit-identical losses and decoder parameters to the eager sequential step (dropout 0: the
+    graph warm-up advances the dropout seed counter; it also runs extra BN forwards, so running
+    statistics are not compared, as for the one-graph mode)."""
+    B, L, V = 4, 7, 50
+    batches = [(t(gen.images(40 + i, B, 64, 64), DEV), t(gen.captions(40 + i, B, L, V), DEV)) for i in range(4)]
+    res = {}
+    for mode in ("eager", "pipe_graph"):
+        enc, dec, opt, Step = _setup(0.0)
+        step = Step(enc, dec, opt, alpha_c=1.0, graph=(mode != "eager"), seed=9, pipeline=(mode != "eager"))
+        out = []
+        for im, cp in batches:
+            x = step(im, cp, [L] * B)
+            out.append(x.clone() if mode == "eager" else x)
+        last = step.flush()
+        torch.cuda.synchronize()
+        losses = [float(x) for x in out if x is not None] + ([float(last)] if last is not None else [])
+        res[mode] = (losses, {n: q.detach().clone() for n, q in dec.named_parameters()})
+    le, pe = res["eager"]
+    lp, pp = res["pipe_graph"]
+    assert len(le) == len(lp) == 4
+    np.testing.assert_array_equal(np.array(lp), np.array(le))
+    for n in pe:
+        assert torch.equal(pe[n], pp[n]), n
