@@ -78,25 +78,28 @@ constexpr int BNF_MAXG = 32;
 // counter; the block whose add returns G-1 is the last one and finalizes those 64 channels,
 // summing the G partials in group order (deterministic) behind one agent-scope acquire, then
 // re-arms the counter to 0. The counters live in the caller's work buffer, zeroed once.
-__global__ void bn_finalize_kernel(const float* __restrict__ stats, int tiles, int C, int per_g,
-                                   unsigned long long* part, int* counters, long long count,
-                                   const float* __restrict__ gamma, const float* __restrict__ beta,
-                                   float* running_mean, float* running_var, float momentum, float eps,
-                                   float* __restrict__ scale, float* __restrict__ shift, float* save_mean,
-                                   float* save_var) {
-  __shared__ double rs[4][64], rq[4][64];
+__global__ void __launch_bounds__(1024)
+bn_finalize_kernel(const float* __restrict__ stats, int tiles, int C, int per_g,
+                   unsigned long long* part, int* counters, long long count,
+                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                   float* running_mean, float* running_var, float momentum, float eps,
+                   float* __restrict__ scale, float* __restrict__ shift, float* save_mean,
+                   float* save_var) {
+  // 1024 threads = 16 slice rows x 64 channels: 8 loads in flight per lane, so a group's slices
+  // take one or two memory round trips
+  __shared__ double rs[16][64], rq[16][64];
+  __shared__ int last;
   const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   const int G = gridDim.y;
   const int t0 = blockIdx.y * per_g, t1 = min(tiles, t0 + per_g);
   double s = 0.0, q = 0.0;
   if (c < C) {
-    // 8 slice loads in flight per lane (a latency-bound loop otherwise), summed in slice order
-    for (int t = t0 + tl; t < t1; t += 32) {
+    for (int t = t0 + tl; t < t1; t += 128) {
       float2 v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int tt = t + 4 * u;
+        const int tt = t + 16 * u;
         v[u] = tt < t1 ? *reinterpret_cast<const float2*>(stats + ((long long)tt * C + c) * 2)
                        : make_float2(0.f, 0.f);
       }
@@ -110,32 +113,55 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int tiles, i
   rs[tl][cl] = s;
   rq[tl][cl] = q;
   __syncthreads();
-  if (tl != 0) return;  // wave 0 publishes, and finalizes if it arrives last
-  if (c < C) {
-    s = rs[0][cl] + rs[1][cl] + rs[2][cl] + rs[3][cl];
-    q = rq[0][cl] + rq[1][cl] + rq[2][cl] + rq[3][cl];
-    unsigned long long* p = part + ((long long)blockIdx.y * C + c) * 2;
-    __hip_atomic_store(p, (unsigned long long)__double_as_longlong(s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(p + 1, (unsigned long long)__double_as_longlong(q), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+  if (tl == 0) {  // wave 0 publishes the group's partial and takes the arrival ticket
+    if (c < C) {
+      s = 0.0;
+      q = 0.0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s += rs[r][cl];
+        q += rq[r][cl];
+      }
+      unsigned long long* p = part + ((long long)blockIdx.y * C + c) * 2;
+      __hip_atomic_store(p, (unsigned long long)__double_as_longlong(s), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p + 1, (unsigned long long)__double_as_longlong(q), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int prev = 0;
+    if (cl == 0) prev = __hip_atomic_fetch_add(counters + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    prev = __shfl(prev, 0, 64);
+    if (cl == 0) last = prev == G - 1;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  int prev = 0;
-  if (cl == 0) prev = __hip_atomic_fetch_add(counters + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  prev = __shfl(prev, 0, 64);
-  if (prev != G - 1) return;
-  // one agent-scope acquire (drops this CU's L1), then plain loads that can all be in flight
-  // at once (sc1 atomic loads of the G partials would be issued one after the other)
+  __syncthreads();
+  if (!last) return;
+  // the last group: one agent-scope acquire per wave, then every wave sums its share of the G
+  // partials (fixed order: group g = tl + 16i, then wave order)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  s = 0.0;
+  q = 0.0;
   if (c < C) {
     const double2* pd = reinterpret_cast<const double2*>(part);
-    s = 0.0;
-    q = 0.0;
-    for (int g = 0; g < G; ++g) {
+    for (int g = tl; g < G; g += 16) {
       const double2 v = pd[(long long)g * C + c];
       s += v.x;
       q += v.y;
+    }
+  }
+  __syncthreads();  // rs / rq reused
+  rs[tl][cl] = s;
+  rq[tl][cl] = q;
+  __syncthreads();
+  if (tl != 0) return;
+  if (c < C) {
+    s = 0.0;
+    q = 0.0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s += rs[r][cl];
+      q += rq[r][cl];
     }
     const double n = (double)count;
     const double mean = s / n;
@@ -156,6 +182,64 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int tiles, i
   if (cl == 0) __hip_atomic_store(counters + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Small statistics buffers (tiles <= BNF_DIRECT: layer3/layer4 at batch 64): one 1024-thread block
+// per 64 channels reads every slice itself (16 slice rows x 8 loads in flight per lane = at most
+// two memory round trips) and finalizes -- no partials, no arrival counter, one launch latency.
+constexpr int BNF_DIRECT = 256;
+
+__global__ void __launch_bounds__(1024)
+bn_finalize_direct_kernel(const float* __restrict__ stats, int tiles, int C, long long count,
+                          const float* __restrict__ gamma, const float* __restrict__ beta, float* running_mean,
+                          float* running_var, float momentum, float eps, float* __restrict__ scale,
+                          float* __restrict__ shift, float* save_mean, float* save_var) {
+  __shared__ double rs[16][64], rq[16][64];
+  const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+    for (int t = tl; t < tiles; t += 128) {
+      float2 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int tt = t + 16 * u;
+        v[u] = tt < tiles ? *reinterpret_cast<const float2*>(stats + ((long long)tt * C + c) * 2)
+                          : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s += v[u].x;
+        q += v[u].y;
+      }
+    }
+  }
+  rs[tl][cl] = s;
+  rq[tl][cl] = q;
+  __syncthreads();
+  if (tl != 0 || c >= C) return;
+  s = 0.0;
+  q = 0.0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    s += rs[r][cl];
+    q += rq[r][cl];
+  }
+  const double n = (double)count;
+  const double mean = s / n;
+  double var = q / n - mean * mean;
+  if (var < 0) var = 0;
+  const double inv = 1.0 / sqrt(var + (double)eps);
+  const float sc = (float)((double)gamma[c] * inv);
+  scale[c] = sc;
+  shift[c] = (float)((double)beta[c] - mean * (double)sc);
+  if (save_mean) save_mean[c] = (float)mean;
+  if (save_var) save_var[c] = (float)var;
+  if (running_mean) {
+    const double unb = count > 1 ? var * n / (n - 1.0) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+  }
+}
+
 extern "C" int capmi_bn_finalize(const float* stats, int tiles, int C, long long count,
                                  const float* gamma, const float* beta, float* running_mean,
                                  float* running_var, float momentum, float eps, float* scale,
@@ -165,14 +249,21 @@ extern "C" int capmi_bn_finalize(const float* stats, int tiles, int C, long long
                 CAPMI_EINVAL);
   CAPMI_REQUIRE((running_mean == nullptr) == (running_var == nullptr), CAPMI_EINVAL);
   CAPMI_REQUIRE(((uintptr_t)stats & 7) == 0 && ((uintptr_t)work & 15) == 0, CAPMI_EALIGN);
-  const int G = std::min(BNF_MAXG, std::max(1, (tiles + 31) / 32));
-  const int per_g = (tiles + G - 1) / G;
   CAPMI_REQUIRE(C <= 8192, CAPMI_ERANGE);
+  if (tiles <= BNF_DIRECT) {
+    hipLaunchKernelGGL(bn_finalize_direct_kernel, dim3(cdiv(C, 64)), dim3(1024), 0, as_stream(stream), stats,
+                       tiles, C, count, gamma, beta, running_mean, running_var, momentum, eps, scale, shift,
+                       save_mean, save_var);
+    CAPMI_LAUNCH_CHECK();
+    return 0;
+  }
+  const int G = std::min(BNF_MAXG, std::max(1, (tiles + 127) / 128));
+  const int per_g = (tiles + G - 1) / G;
   // [0, 64 doubles): the arrival counters (one int per 64-channel block, fixed place whatever
   // C is, so BN layers of different widths can share one zeroed work buffer); then partials
   int* counters = static_cast<int*>(work);
   unsigned long long* part = static_cast<unsigned long long*>(work) + 64;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64), G), dim3(256), 0, as_stream(stream), stats,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64), G), dim3(1024), 0, as_stream(stream), stats,
                      tiles, C, per_g, part, counters, count, gamma, beta, running_mean, running_var,
                      momentum, eps, scale, shift, save_mean, save_var);
   CAPMI_LAUNCH_CHECK();

@@ -240,7 +240,7 @@ def test_bn_finalize_shared_work():
     zeroed work buffer, counters re-armed to zero after every call."""
     K = _K()
     work = torch.zeros(K.bn_work_doubles(2048), device=DEV, dtype=torch.float64)
-    for it, (C, tiles) in enumerate([(64, 3136), (2048, 49), (256, 196), (64, 3136), (1024, 7)]):
+    for it, (C, tiles) in enumerate([(64, 3136), (2048, 49), (256, 196), (64, 3136), (1024, 7), (512, 256), (128, 257)]):
         g = torch.Generator().manual_seed(40 + it)
         x = torch.randn(tiles * 64, C, generator=g, dtype=torch.float64) * 3 + 1
         rows = x.shape[0]
