@@ -2,7 +2,8 @@
 training steps run end to end (RCCL refuses two ranks on one GPU, and the 8-GPU node is the
 driver's), i.e. capmi.train_step's DP logic with real HIP kernels:
 
-  * frozen encoder (config 3), pipelined two-stream step: after the step the gradient buffer of
+  * frozen encoder (config 3), pipelined two-stream step, eager and on HIP graphs (the bench
+    default; the all-reduce + update run after the decoder graph's replay): after the step the gradient buffer of
     every rank equals the mean of the per-shard gradients, computed in the same process by the
     non-DP fused path on each shard; parameters are identical on both ranks;
   * encoder fine-tune (config 4): the same for the decoder AND the encoder gradient buffers
@@ -54,7 +55,7 @@ def _setup(fine_tune, seed=3):
     return enc, dec, dopt, eopt
 
 
-def _worker(rank, world, port, fine_tune, q):
+def _worker(rank, world, port, fine_tune, q, graph=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.join(os.path.dirname(here), "image-captioning-with-different-decoders_amd"),
@@ -93,7 +94,8 @@ def _worker(rank, world, port, fine_tune, q):
         torch.cuda.synchronize()
         # the DP step on this rank's shard (fresh model: BN running stats / weights as above)
         enc, dec, dopt, eopt = _setup(fine_tune)
-        step = AttentionTrainStep(enc, dec, dopt, ctx, seed=9, pipeline=not fine_tune, encoder_optimizer=eopt)
+        step = AttentionTrainStep(enc, dec, dopt, ctx, seed=9, pipeline=not fine_tune, encoder_optimizer=eopt,
+                                  graph=graph)
         sl = slice(rank * B, (rank + 1) * B)
         step(imgs[sl], caps[sl], [L] * B)
         step.flush()
@@ -118,12 +120,12 @@ def _worker(rank, world, port, fine_tune, q):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fine_tune", [False, True])
-def test_dp_two_ranks_one_gpu(fine_tune):
+@pytest.mark.parametrize("fine_tune,graph", [(False, False), (False, True), (True, False)])
+def test_dp_two_ranks_one_gpu(fine_tune, graph):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, fine_tune, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, fine_tune, q, graph)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
