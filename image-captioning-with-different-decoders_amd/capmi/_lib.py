@@ -106,6 +106,9 @@ _SIGS = {
     "capmi_bn_add_relu_bf16": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_vp, c_vp],
     "capmi_f32_to_bf16": [c_vp, c_ll, c_vp, c_vp],
     "capmi_adaptive_avgpool_bf16": [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp],
+    "capmi_resize_normalize_u8": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,
+                                  c_vp, c_vp],
+    "capmi_resize_taps_max": [c_int, c_int],
     "capmi_strerror": [c_int],
     "capmi_abi_version": [],
 }

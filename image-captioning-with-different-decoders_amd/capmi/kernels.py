@@ -221,6 +221,22 @@ def adaptive_avgpool_bf16(inp, N, H, W, C, OH, OW, out):
     call("capmi_adaptive_avgpool_bf16", ptr(inp), N, H, W, C, OH, OW, ptr(out), stream())
 
 
+def resize_normalize_u8(src, offsets, heights, widths, max_h, max_w, OH, OW, mean, std, tmp, out):
+    """Batch of packed uint8 RGB HWC images -> (B, 3, OH, OW) fp32: PIL-exact bilinear Resize,
+    ToTensor, Normalize (capmi_resize_normalize_u8). offsets int64 / heights, widths int32 [B] on
+    the device; tmp uint8 >= B * max_h * OW * 3."""
+    B = heights.numel()
+    _cuda(src, tmp, dtype=torch.uint8)
+    _cuda(offsets, dtype=torch.int64)
+    _cuda(heights, widths, dtype=torch.int32)
+    _cuda(out)
+    assert tmp.numel() >= B * max_h * OW * 3 and out.numel() >= B * 3 * OH * OW
+    m = (ctypes.c_float * 3)(*mean)
+    s = (ctypes.c_float * 3)(*std)
+    call("capmi_resize_normalize_u8", ptr(src), ptr(offsets), ptr(heights), ptr(widths), B, max_h, max_w, OH, OW,
+         m, s, ptr(tmp), ptr(out), stream())
+
+
 def adaptive_avgpool_nhwc(inp, N, H, W, C, OH, OW, out):
     _cuda(inp, out)
     call("capmi_adaptive_avgpool_nhwc", ptr(inp), N, H, W, C, OH, OW, ptr(out), stream())

@@ -139,7 +139,11 @@ def train(device, args):
     def collate_fn(data):
         from torch.nn.utils.rnn import pad_sequence
         imgs, captions = zip(*data)
-        imgs = torch.stack(imgs, dim=0)
+        if isinstance(imgs[0], torch.Tensor):
+            imgs = torch.stack(imgs, dim=0)
+        else:  # decoded uint8 images (COCODataset without a transform): resized on the GPU
+            from capmi.imagepipe import PackedImages
+            imgs = PackedImages(list(imgs), pin=False)
         captions = pad_sequence(captions, batch_first=True, padding_value=pad_idx)
         caption_lengths = [len(caption) for caption in captions]  # after padding (Q1)
         return imgs, captions, caption_lengths
@@ -214,6 +218,7 @@ def train(device, args):
     encoder.train()
     num_batches = len(train_loader)
     epoch_losses = metrics.get('epoch_losses', [])
+    gpu_tf = None
     for epoch in range(start_epoch, args.epochs):
         if sampler is not None:
             sampler.set_epoch(epoch)
@@ -223,7 +228,13 @@ def train(device, args):
         start = time.time()
         pending = []
         for batch_idx, (imgs, captions, caption_lengths) in enumerate(train_loader):
-            imgs = imgs.to(device, non_blocking=True)
+            if isinstance(imgs, torch.Tensor):
+                imgs = imgs.to(device, non_blocking=True)
+            else:  # PackedImages: Resize + ToTensor + Normalize on the GPU (capmi.imagepipe)
+                if gpu_tf is None:
+                    from capmi.imagepipe import GpuImageTransform
+                    gpu_tf = GpuImageTransform(device)
+                imgs = gpu_tf(imgs)
             captions = captions.to(device, non_blocking=True)
             clip_gradient(decoder_optimizer, args.grad_clip)
             if encoder_optimizer is not None:

@@ -163,6 +163,17 @@ int capmi_f32_to_bf16(const float* in, long long n, void* out, void* stream);
 /* AdaptiveAvgPool2d((OH, OW)) of a bf16 NHWC map -> fp32 NHWC (models/encoder.py:92,108-109) */
 int capmi_adaptive_avgpool_bf16(const void* x, int N, int H, int W, int C, int OH, int OW, float* out,
                                 void* stream);
+/* Image preprocessing: Resize((OH, OW)) -> ToTensor -> Normalize(mean, std) of the
+ * reference's transform (models/attention.py:296-301, dataset.py:55-59) for a batch of decoded RGB
+ * uint8 HWC images of any sizes, bit-identical to torchvision's PIL path (Pillow's antialiased
+ * bilinear resample, 22-bit fixed point, uint8 rounding after each pass). src: packed images,
+ * image b at src + offsets[b] with heights[b] x widths[b] (device arrays); max_h/max_w bound them;
+ * mean/std: 3 HOST floats each; tmp: B * max_h * OW * 3 bytes of scratch; out: (B, 3, OH, OW) fp32. */
+int capmi_resize_normalize_u8(const unsigned char* src, const long long* offsets, const int* heights,
+                              const int* widths, int B, int max_h, int max_w, int OH, int OW, const float* mean,
+                              const float* std, void* tmp, float* out, void* stream);
+/* taps per output index of that resample (2*ceil(max(1, in/out)) + 1); host-only helper */
+int capmi_resize_taps_max(int in_size, int out_size);
 /* Bottleneck tail: out = relu(y*s + b + (res_scale ? res*rs + rb : res)), NHWC, C % 4 == 0 */
 int capmi_bn_add_relu(const float* y, const float* s, const float* b, const float* res,
                       const float* res_scale, const float* res_shift, float* out, long long rows,
