@@ -106,11 +106,24 @@ def gemm_bf16(prob, amode, workspace, tile=CAPMI_TILE_AUTO):
          ptr(workspace), workspace.numel() * 4, stream())
 
 
-def gemm_sk_plan(prob, amode, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W):
-    """(bm, bn, stream_k, generic) of the launch gemm_sk would make for ``prob``."""
-    v = [ctypes.c_int(0) for _ in range(4)]
-    call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, bmode, tile, *[ctypes.byref(x) for x in v])
-    return tuple(x.value for x in v)
+def gemm_sk_plan(prob, amode, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W, bf16=False, threads=False):
+    """(bm, bn, stream_k, generic[, threads]) of the launch gemm_sk would make for ``prob``."""
+    v = [ctypes.c_int(0) for _ in range(5)]
+    call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, bmode, tile, 1 if bf16 else 0,
+         *[ctypes.byref(x) for x in v])
+    return tuple(x.value for x in v[:5 if threads else 4])
+
+
+def gemm_sk_kernel_name(prob, amode, bmode=CAPMI_B_NMAJOR_W, bf16=False):
+    """The kernel symbol (as rocprofv3 prints it) of the launch gemm_sk(..., TILE_AUTO) makes."""
+    bm, bn, sk, generic, nt = gemm_sk_plan(prob, amode, CAPMI_TILE_AUTO, bmode, bf16, threads=True)
+    b = lambda v: "true" if v else "false"  # noqa: E731
+    pro = b(bool(prob.in_scale))
+    if generic:
+        return "gemm_kernel (generic)"
+    if nt == 512:
+        return f"gemm_nt8_kernel<{amode}, {pro}, {b(sk)}>"
+    return f"gemm_nt_kernel<{bm}, {bn}, {amode}, {bmode}, {pro}, {b(sk)}, {b(bf16)}>"
 
 
 def stat_tiles(M, tile=CAPMI_TILE_128):

@@ -199,10 +199,7 @@ class EncoderRunner:
         bf = self.bf16
         launch = lambda: K.gemm_sk(prob, mode, self._ws["sk"], K.TILE_AUTO, bf16=bf)  # noqa: E731
         if self.conv_hook is not None:
-            bm, bn, sk, generic = K.gemm_sk_plan(prob, mode, K.TILE_AUTO)
-            b = lambda v: "true" if v else "false"  # noqa: E731
-            key = "gemm_kernel (generic)" if generic else \
-                f"gemm_nt_kernel<{bm}, {bn}, {mode}, 0, {b(in_ss is not None and not nchw)}, {b(sk)}, {b(bf)}>"
+            key = K.gemm_sk_kernel_name(prob, mode, bf16=bf)
             self.conv_hook(tag, 2.0 * rows * co * Kd, launch, key)
         else:
             launch()
@@ -535,10 +532,7 @@ class FineTuneRunner:
             if hook is None:
                 self._gemm(prob, amode, bmode)
             else:
-                bm, bn, sk, gen = K.gemm_sk_plan(prob, amode, K.TILE_AUTO, bmode)
-                hook(tag, flops, lambda: self._gemm(prob, amode, bmode),
-                     f"gemm_nt_kernel<{bm}, {bn}, {amode}, {bmode}, {'true' if prob.in_scale else 'false'}, "
-                     f"{'true' if sk else 'false'}, false>")
+                hook(tag, flops, lambda: self._gemm(prob, amode, bmode), K.gemm_sk_kernel_name(prob, amode, bmode))
 
         K.adaptive_avgpool_bwd_nhwc(dfeat.contiguous(), N, stt["H"], stt["W"], stt["C"], stt["OH"], stt["OW"],
                                     dA[0])

@@ -387,6 +387,7 @@ namespace {
 struct GemmPlan {
   GemmArgs a;
   int bm, bn;
+  int nt = 256;  // threads per workgroup of the v2 kernel (512: CAPMI_TILE_128_W8)
   bool nt_ok, vec;
   long long total;  // workgroups of the data-parallel launch
 };
@@ -395,7 +396,7 @@ int gemm_plan(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, 
   CAPMI_REQUIRE(probs != nullptr && nprob >= 1 && nprob <= CAPMI_MAX_GROUP, CAPMI_EINVAL);
   CAPMI_REQUIRE(amode >= 0 && amode <= 4 && bmode >= 0 && bmode <= 2, CAPMI_EINVAL);
   CAPMI_REQUIRE(bmode != 2 || amode == 1, CAPMI_EINVAL);
-  CAPMI_REQUIRE(tile >= CAPMI_TILE_128 && tile <= CAPMI_TILE_AUTO, CAPMI_EINVAL);
+  CAPMI_REQUIRE(tile >= CAPMI_TILE_128 && tile <= CAPMI_TILE_128_W8, CAPMI_EINVAL);
   CAPMI_REQUIRE(amode != 4 || bmode == 0, CAPMI_EINVAL);
   GemmArgs& a = g.a;
   memset(&a, 0, sizeof(a));
@@ -455,6 +456,12 @@ int gemm_plan(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, 
   nt_ok = nt_ok && (vec || ((amode == 2 || amode == 4) && bmode == 0));
   CAPMI_REQUIRE(bmode != 2 || nt_ok, CAPMI_EALIGN);  // no generic-kernel form of the im2col B
   int bm = 128, bn = 128;
+  g.nt = 256;
+  if (tile == CAPMI_TILE_128_W8) {  // 512-thread 128x128 form: forward modes of the v2 kernel only
+    CAPMI_REQUIRE(nt_ok && bmode == 0 && (amode == 0 || amode == 2 || amode == 4), CAPMI_EINVAL);
+    g.nt = 512;
+    tile = CAPMI_TILE_128;
+  }
   if (tile == CAPMI_TILE_64) {
     bm = bn = 64;
   } else if (tile == CAPMI_TILE_128x64) {
@@ -493,7 +500,7 @@ int gemm_plan(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, 
 
 int gemm_launch_dp(const GemmPlan& g, int amode, int bmode, hipStream_t s) {
   if (g.total == 0) return 0;
-  if (g.nt_ok) return gemm_nt_launch(g.a, amode, bmode, g.bm, g.bn, (int)g.total, s);
+  if (g.nt_ok) return gemm_nt_launch(g.a, amode, bmode, g.bm, g.bn, (int)g.total, s, false, g.nt);
   if (g.bm == 128) return launch_mode<128, 128, 64, 64>(g.a, amode, bmode, g.vec, (int)g.total, s);
   return launch_mode<64, 64, 32, 32>(g.a, amode, bmode, g.vec, (int)g.total, s);
 }
@@ -540,7 +547,7 @@ bool sk_xcd_groups() {
   return on;
 }
 // the launch capmi_gemm_sk makes for a problem (shared by the launcher and the plan query)
-int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, GemmPlan& g, bool& sk) {
+int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, bool bf16, GemmPlan& g, bool& sk) {
   CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
   const int nkt = (prob->K + 31) / 32;
   const bool automatic = tile == CAPMI_TILE_AUTO;
@@ -548,9 +555,18 @@ int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Ge
   // output tile, stream-K over 128x64 tiles is the fastest form; below that the per-segment
   // pipeline fill outweighs the balance gain and 64x64 data-parallel wins
   if (automatic) tile = nkt >= 16 ? CAPMI_TILE_128x64 : CAPMI_TILE_64;
-  const int rc = gemm_plan(prob, 1, amode, bmode, tile, g);
+  int rc = gemm_plan(prob, 1, amode, bmode, tile, g);
   if (rc) return rc;
-  const long long slots = (long long)cu_count() * gemm_nt_wg_per_cu(g.bm, g.bn);
+  // the 512-thread 128x128 form (tools/w8_ab.sh over all 19 encoder conv shapes, batch 64):
+  // 2-12% faster wherever N >= 128 and either the k-loop is long (>= 16 k-tiles) or N <= 256;
+  // slower for N = 64 (half the tile idle) and for N >= 512 with a short k-loop (64x64 keeps
+  // 4 workgroups per CU to hide the epilogue)
+  if (automatic && g.nt_ok && !bf16 && bmode == 0 && (amode == 0 || amode == 2 || amode == 4) &&
+      prob->ksplit == 1 && prob->M >= 2048 && prob->N >= 128 && (nkt >= 16 || prob->N <= 256)) {
+    rc = gemm_plan(prob, 1, amode, bmode, CAPMI_TILE_128_W8, g);
+    if (rc) return rc;
+  }
+  const long long slots = (long long)cu_count() * (g.nt == 512 ? 1 : gemm_nt_wg_per_cu(g.bm, g.bn));
   const long long tiles = g.total;
   sk = g.nt_ok && prob->ksplit == 1 && tiles > 0 && (!automatic || nkt >= 16);
   if (sk) {
@@ -562,12 +578,14 @@ int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Ge
 }
 }  // namespace
 
-extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, int* bm,
-                                  int* bn, int* stream_k, int* generic) {
+extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, int flags,
+                                  int* bm, int* bn, int* stream_k, int* generic, int* threads) {
   GemmPlan g;
   bool sk = false;
-  const int rc = sk_decide(prob, amode, bmode, tile, g, sk);
+  CAPMI_REQUIRE((flags & ~CAPMI_GEMM_BF16) == 0, CAPMI_EINVAL);
+  const int rc = sk_decide(prob, amode, bmode, tile, (flags & CAPMI_GEMM_BF16) != 0, g, sk);
   if (rc) return rc;
+  if (threads) *threads = g.nt_ok ? g.nt : 256;
   if (bm) *bm = g.bm;
   if (bn) *bn = g.bn;
   if (stream_k) *stream_k = sk ? 1 : 0;
@@ -630,9 +648,10 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   if (flags == CAPMI_GEMM_BF16_IO) return gemm_bf16_io(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
   CAPMI_REQUIRE((flags & ~CAPMI_GEMM_BF16) == 0, CAPMI_EINVAL);
   const bool bf16 = (flags & CAPMI_GEMM_BF16) != 0;
-  const int rc = sk_decide(prob, amode, bmode, tile, g, sk);
+  const int rc = sk_decide(prob, amode, bmode, tile, bf16, g, sk);
   if (rc) return rc;
-  CAPMI_REQUIRE(!bf16 || (g.nt_ok && bmode == 0 && (amode == 0 || amode == 2 || amode == 4)), CAPMI_EINVAL);
+  CAPMI_REQUIRE(!bf16 || (g.nt_ok && g.nt == 256 && bmode == 0 && (amode == 0 || amode == 2 || amode == 4)),
+                CAPMI_EINVAL);
   hipStream_t s = as_stream(stream);
   if (!sk) {
     if (g.total == 0) return 0;
@@ -642,7 +661,7 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   CAPMI_REQUIRE(workspace != nullptr && aligned16(workspace), CAPMI_EINVAL);
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
   const int cus = cu_count();
-  const long long slots = (long long)cus * gemm_nt_wg_per_cu(g.bm, g.bn);
+  const long long slots = (long long)cus * (g.nt == 512 ? 1 : gemm_nt_wg_per_cu(g.bm, g.bn));
   GemmArgs& a = g.a;
   a.sk_nkt = (prob->K + 31) / 32;
   a.sk_units = g.total * a.sk_nkt;
@@ -650,7 +669,7 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   a.sk_groups = sk_xcd_groups() && a.sk_workers % 8 == 0 && g.total >= 64 ? 8 : 1;
   a.sk_flags = static_cast<int*>(workspace);
   a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
-  return gemm_nt_launch(a, amode, bmode, g.bm, g.bn, a.sk_workers, s, bf16);
+  return gemm_nt_launch(a, amode, bmode, g.bm, g.bn, a.sk_workers, s, bf16, g.nt);
 }
 
 extern "C" int capmi_gemm_sk(const capmi_gemm_problem* prob, int amode, int bmode, int tile,

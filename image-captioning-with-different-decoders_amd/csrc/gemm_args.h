@@ -27,7 +27,7 @@ __device__ __forceinline__ long long remap(long long r, long long r1, long long 
 // v2 kernel: A K-major dense / NHWC conv / NHWC4 conv1 / M-major (k rows), B = W[N][K] or k rows;
 // BM x BN in {128x128, 128x64, 64x64}
 int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int blocks, hipStream_t s,
-                   bool bf16 = false);
+                   bool bf16 = false, int nt = 256);
 // bf16-in/bf16-out conv GEMM (gemm_bf16.hip): BM = 128, BN in {128, 64}, amode 0 (dense) / 2 (conv)
 int gemm_bf16_launch(const GemmArgs& a, int amode, int bm, int bn, int blocks, hipStream_t s);
 // resident workgroups per CU of the NT kernel for a tile shape (LDS / register bound)

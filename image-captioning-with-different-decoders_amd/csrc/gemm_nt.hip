@@ -82,12 +82,16 @@ __device__ __forceinline__ bf16x4 to_bf16x4(float4 v) {
   return r;
 }
 
-template <int BM, int BN, int AMODE, int BMODE, bool PRO, bool SK, bool BF = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWavesPerEu<BM, BN>)))
-gemm_nt_kernel(const GemmArgs args) {
+// NT threads = NT/64 waves as (NT/128) rows x 2 columns: 256 (the 2x2 form, every mode) or 512
+// (128x128 tiles only, 4x2 waves of 32x64: one workgroup per CU moves a third fewer bytes per
+// k-tile through L2 and LDS than two 128x64 workgroups; forward modes only)
+template <int BM, int BN, int AMODE, int BMODE, bool PRO, bool SK, bool BF, int NT>
+__device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
   static_assert(!BF || (BMODE == 0 && AMODE != 1), "bf16 staging: row-major A (dense / conv) x W[N][K] only");
-  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
-  constexpr int NA = BM * BK2 / 4 / 256, NB = BN * BK2 / 4 / 256;
+  static_assert(NT == 256 || (NT == 512 && BMODE == 0 && AMODE != 1 && !BF), "512-thread form: forward modes");
+  constexpr int WR = NT / 128;  // wave rows
+  constexpr int WM = BM / WR, WN = BN / 2, TM = WM / 32, TN = WN / 32;
+  constexpr int NA = BM * BK2 / 4 / NT, NB = BN * BK2 / 4 / NT;
   static_assert(NA >= 1 && NB >= 1, "tile");
   __shared__ __attribute__((aligned(16))) float As[2][BM * S2];
   __shared__ __attribute__((aligned(16))) float Bs[2][BN * S2];
@@ -131,7 +135,7 @@ gemm_nt_kernel(const GemmArgs args) {
     bool a_ok[NA];
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int f = tid + i * 256;
+      const int f = tid + i * NT;
       if (AMODE == 1) {
         const int jq = (tid & 15) + 16 * (i % AQ16);
         const int m = m0 + jq * 4;
@@ -165,7 +169,7 @@ gemm_nt_kernel(const GemmArgs args) {
     const float inv_hw = 1.f / (float)cHW, inv_wo = 1.f / (float)cWo;
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int f = tid + i * 256;
+      const int f = tid + i * NT;
       b_kh[i] = b_kw[i] = 0;
       b_sc[i] = f4(1.f);
       b_sh[i] = f4(0.f);
@@ -302,14 +306,14 @@ gemm_nt_kernel(const GemmArgs args) {
           float4 v = st.ra[i];
           if (PRO && AMODE == 2) v = relu4(fma4(v, st.sc, st.sh));
           if (!((st.am >> i) & 1u)) v = f4(0.f);
-          const int f = tid + i * 256;
+          const int f = tid + i * NT;
           *reinterpret_cast<bf16x4*>(Ah + (f >> 3) * SB + kq) = to_bf16x4(v);
         }
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
           float4 v = st.rb[i];
           if (!((st.bm >> i) & 1u)) v = f4(0.f);
-          const int f = tid + i * 256;
+          const int f = tid + i * NT;
           *reinterpret_cast<bf16x4*>(Bh + (f >> 3) * SB + kq) = to_bf16x4(v);
         }
         return;
@@ -319,7 +323,7 @@ gemm_nt_kernel(const GemmArgs args) {
         float4 v = st.ra[i];
         if (PRO && AMODE == 2) v = relu4(fma4(v, st.sc, st.sh));
         if (!((st.am >> i) & 1u)) v = f4(0.f);
-        const int f = tid + i * 256;
+        const int f = tid + i * NT;
         if (AMODE == 1) {
           store_t4(&As[buf][(i % AQ16 * 16 + (tid & 15)) * 4 * S2 + (tid >> 4) + 16 * (i / AQ16)], v, tid);
         } else {
@@ -331,7 +335,7 @@ gemm_nt_kernel(const GemmArgs args) {
         float4 v = st.rb[i];
         if (PRO && BMODE == 2) v = relu4(fma4(v, b_sc[i], b_sh[i]));
         if (!((st.bm >> i) & 1u)) v = f4(0.f);
-        const int f = tid + i * 256;
+        const int f = tid + i * NT;
         if (BMODE >= 1) {
           store_t4(&Bs[buf][(i % BQ16 * 16 + (tid & 15)) * 4 * S2 + (tid >> 4) + 16 * (i / BQ16)], v, tid);
         } else {
@@ -392,7 +396,7 @@ gemm_nt_kernel(const GemmArgs args) {
 
     // 128x128 with the BN prologue cannot afford the second register stage (it would drop to
     // one wave per SIMD): it prefetches one tile ahead.
-    constexpr bool DEEP = !(BM == 128 && BN == 128 && PRO);
+    constexpr bool DEEP = !(BM == 128 && BN == 128 && PRO && NT == 256);
     Stage s0, s1;
     s0.sc = s1.sc = f4(1.f);
     s0.sh = s1.sh = f4(0.f);
@@ -482,7 +486,7 @@ gemm_nt_kernel(const GemmArgs args) {
             }
           }
         }
-      } else {  // BM == 64: both wave rows share slice tm
+      } else {  // WM == 32: wave rows 2s and 2s+1 share the tile's 64-row slice s
         float* red = As[0];  // the K loop ended with a barrier: LDS is free
         if (lh == 0) {
 #pragma unroll
@@ -492,14 +496,17 @@ gemm_nt_kernel(const GemmArgs args) {
           }
         }
         __syncthreads();
-        for (int c = tid; c < BN; c += 256) {
-          const int wn = c / WN, cc = c % WN;
-          const float s = red[((0 * 2 + wn) * 2 + 0) * WN + cc] + red[((1 * 2 + wn) * 2 + 0) * WN + cc];
-          const float q = red[((0 * 2 + wn) * 2 + 1) * WN + cc] + red[((1 * 2 + wn) * 2 + 1) * WN + cc];
-          const int col = n0 + c;
-          if (col < N) {
-            stats[((long long)tm * N + col) * 2 + 0] = s;
-            stats[((long long)tm * N + col) * 2 + 1] = q;
+        constexpr int NS = BM / 64;  // 64-row slices per tile
+        for (int c = tid; c < NS * BN; c += NT) {
+          const int sl = c / BN, cn = c % BN, wn = cn / WN, cc = cn % WN;
+          const int w0 = (2 * sl) * 2 + wn, w1 = (2 * sl + 1) * 2 + wn;  // wid = 2 * row + column
+          const float s = red[(w0 * 2 + 0) * WN + cc] + red[(w1 * 2 + 0) * WN + cc];
+          const float q = red[(w0 * 2 + 1) * WN + cc] + red[(w1 * 2 + 1) * WN + cc];
+          const int col = n0 + cn;
+          if (col < N && m0 + 64 * sl < M) {
+            const long long slice = (m0 >> 6) + sl;
+            stats[(slice * N + col) * 2 + 0] = s;
+            stats[(slice * N + col) * 2 + 1] = q;
           }
         }
         __syncthreads();  // LDS reused by the next tile (stream-K)
@@ -570,7 +577,7 @@ gemm_nt_kernel(const GemmArgs args) {
             v.y = __float_as_uint(acc[i][j][4 * q + 1]);
             v.z = __float_as_uint(acc[i][j][4 * q + 2]);
             v.w = __float_as_uint(acc[i][j][4 * q + 3]);
-            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (((i * TN + j) * 4 + q) * 256 + tid) * 16, 0, kSc1);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (((i * TN + j) * 4 + q) * NT + tid) * 16, 0, kSc1);
           }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -599,7 +606,7 @@ gemm_nt_kernel(const GemmArgs args) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
-                  rs, (((i * TN + j) * 4 + q) * 256 + tid) * 16, 0, kSc1);
+                  rs, (((i * TN + j) * 4 + q) * NT + tid) * 16, 0, kSc1);
               acc[i][j][4 * q + 0] += __uint_as_float(v.x);
               acc[i][j][4 * q + 1] += __uint_as_float(v.y);
               acc[i][j][4 * q + 2] += __uint_as_float(v.z);
@@ -610,6 +617,31 @@ gemm_nt_kernel(const GemmArgs args) {
     }
     epilogue(P, tm, tn, 0);
   }
+}
+
+template <int BM, int BN, int AMODE, int BMODE, bool PRO, bool SK, bool BF = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWavesPerEu<BM, BN>)))
+gemm_nt_kernel(const GemmArgs args) {
+  gemm_nt_body<BM, BN, AMODE, BMODE, PRO, SK, BF, 256>(args);
+}
+
+template <int AMODE, bool PRO, bool SK>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+gemm_nt8_kernel(const GemmArgs args) {
+  gemm_nt_body<128, 128, AMODE, 0, PRO, SK, false, 512>(args);
+}
+
+template <bool SK>
+void launch_nt8(const GemmArgs& a, int amode, bool pro, int blocks, hipStream_t s) {
+  const dim3 g(blocks), b(512);
+  if (amode == 4)
+    hipLaunchKernelGGL((gemm_nt8_kernel<4, false, SK>), g, b, 0, s, a);
+  else if (amode == 0)
+    hipLaunchKernelGGL((gemm_nt8_kernel<0, false, SK>), g, b, 0, s, a);
+  else if (pro)
+    hipLaunchKernelGGL((gemm_nt8_kernel<2, true, SK>), g, b, 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_nt8_kernel<2, false, SK>), g, b, 0, s, a);
 }
 
 template <int BM, int BN, bool SK>
@@ -669,7 +701,7 @@ int launch_bmbn(const GemmArgs& a, int amode, int bmode, bool pro, bool bf16, in
 }  // namespace
 
 int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int blocks, hipStream_t s,
-                   bool bf16) {
+                   bool bf16, int nt) {
   bool pro = false;
   for (int i = 0; i < a.nprob; ++i) pro = pro || a.p[i].in_scale != nullptr;
   for (int i = 0; i < a.nprob; ++i)
@@ -677,6 +709,15 @@ int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int 
   if (pro && !((amode == 2 && bmode == 0) || (amode == 1 && bmode == 2))) return CAPMI_EINVAL;
   if (bmode == 2 && amode != 1) return CAPMI_EINVAL;
   if (bf16 && !(bmode == 0 && (amode == 0 || amode == 2 || amode == 4))) return CAPMI_EINVAL;
+  if (nt == 512) {
+    if (bm != 128 || bn != 128 || bf16 || bmode != 0 || !(amode == 0 || amode == 2 || amode == 4)) return CAPMI_EINVAL;
+    if (a.sk_workers > 0)
+      launch_nt8<true>(a, amode, pro, blocks, s);
+    else
+      launch_nt8<false>(a, amode, pro, blocks, s);
+    CAPMI_LAUNCH_CHECK();
+    return 0;
+  }
   if (bm == 128 && bn == 128) return launch_bmbn<128, 128>(a, amode, bmode, pro, bf16, blocks, s);
   if (bm == 128 && bn == 64) return launch_bmbn<128, 64>(a, amode, bmode, pro, bf16, blocks, s);
   if (bm == 64 && bn == 64) return launch_bmbn<64, 64>(a, amode, bmode, pro, bf16, blocks, s);

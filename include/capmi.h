@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 7
+#define CAPMI_ABI_VERSION 8
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -56,8 +56,11 @@ enum capmi_bmode {
                            (dY stored as [pixel][Cout]); C = dW[Cout][KH][KW][Cin]; in_scale/in_shift, when
                            set, are the BN-apply+ReLU prologue of the conv's input (Cin % 4 == 0) */
 };
-/* tile: 128x128, 64x64, 128x64, or AUTO (chosen from the grid size; what the encoder uses) */
-enum capmi_tile { CAPMI_TILE_128 = 0, CAPMI_TILE_64 = 1, CAPMI_TILE_128x64 = 2, CAPMI_TILE_AUTO = 3 };
+/* tile: 128x128, 64x64, 128x64, or AUTO (chosen from the grid size; what the encoder uses);
+ * CAPMI_TILE_128_W8: 128x128 with 512-thread workgroups (8 waves, one workgroup per CU), forward
+ * modes (A row-major / conv x W[N][K]) of capmi_gemm_sk only */
+enum capmi_tile { CAPMI_TILE_128 = 0, CAPMI_TILE_64 = 1, CAPMI_TILE_128x64 = 2, CAPMI_TILE_AUTO = 3,
+                  CAPMI_TILE_128_W8 = 4 };
 
 typedef struct capmi_gemm_problem {
   int M, N, K;
@@ -108,10 +111,12 @@ int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int t
 #define CAPMI_GEMM_BF16_IO 2
 int capmi_gemm_sk_ex(const capmi_gemm_problem* problem, int amode, int bmode, int tile, int flags, void* workspace,
                      long long ws_bytes, void* stream);
-/* the launch capmi_gemm_sk would make (no GPU work): tile bm x bn, stream_k 0/1, generic = 1
- * when the problem falls back to the generic kernel. Used by the benchmark to attribute time. */
-int capmi_gemm_sk_plan(const capmi_gemm_problem* problem, int amode, int bmode, int tile, int* bm, int* bn,
-                       int* stream_k, int* generic);
+/* the launch capmi_gemm_sk_ex(..., flags, ...) would make (no GPU work): tile bm x bn, stream_k 0/1,
+ * generic = 1 when the problem falls back to the generic kernel, threads = workgroup size (256, or
+ * 512 for the CAPMI_TILE_128_W8 form AUTO picks for wide convs). Used by the benchmark to attribute
+ * time. Any out pointer may be NULL. */
+int capmi_gemm_sk_plan(const capmi_gemm_problem* problem, int amode, int bmode, int tile, int flags, int* bm,
+                       int* bn, int* stream_k, int* generic, int* threads);
 
 /* sum of S partial slabs: out[r][c] = sum_s in[s*slab + r*ld_in + c] (+ bias[c]); rows x cols */
 int capmi_splitk_reduce(const float* in, int S, long long slab, int rows, int cols, long long ld_in,

@@ -207,7 +207,7 @@ def test_gemm_sk_linear(tile, M, N, Kd):
 
 
 @pytest.mark.parametrize("k,stride,cin,cout,hw", [(3, 1, 64, 128, 14), (3, 2, 128, 64, 15), (1, 1, 256, 64, 7)])
-def test_conv_sk_prologue(k, stride, cin, cout, hw):
+def test_conv_sk_prologue(k, stride, cin, cout, hw, tile=3):
     K = _K()
     N = 4
     x = rnd(N, cin, hw, hw, seed=34)
@@ -227,9 +227,9 @@ def test_conv_sk_prologue(k, stride, cin, cout, hw):
     geo = dict(N=N, H=hw, W=hw, Cin=cin, KH=k, KW=k, stride=stride, pad=pad, Ho=Ho, Wo=Ho)
     ws = K.gemm_workspace(DEV)
     K.gemm_sk(K.problem(M, cout, k * k * cin, x_nhwc, 0, wp, k * k * cin, out, cout, conv=geo, stats=stats,
-                        in_scale=sc.float().to(DEV), in_shift=sh.float().to(DEV)), 2, ws)
+                        in_scale=sc.float().to(DEV), in_shift=sh.float().to(DEV)), 2, ws, tile)
     got = out.view(N, Ho, Ho, cout).permute(0, 3, 1, 2)
-    check(got, ref, ref_abs, f"stream-K conv{k}x{k}/s{stride}")
+    check(got, ref, ref_abs, f"stream-K conv{k}x{k}/s{stride} tile {tile}")
     s = stats.double().cpu().sum(0)
     Cd = out.double().cpu()
     torch.testing.assert_close(s[:, 0], Cd.sum(0), rtol=1e-5, atol=1e-3)
@@ -279,3 +279,51 @@ def test_gemm_sk_transposed(tile, M, N, Kd):
     K.gemm_sk(K.problem(Kd, N, M, dYd, M, Wd, N, out, N), 0, ws, tile, bmode=1)
     torch.cuda.synchronize()
     check(out, dY @ W, dY.abs() @ W.abs(), "stream-K KMAJOR x KROWS")
+
+
+@pytest.mark.parametrize("k,stride,cin,cout,hw", [(3, 1, 256, 256, 14), (1, 1, 256, 1024, 14), (3, 2, 128, 128, 28),
+                                                  (3, 1, 64, 192, 9)])
+def test_conv_512_thread_tile(k, stride, cin, cout, hw):
+    """CAPMI_TILE_128_W8 (128x128, 8 waves as 4x2, one workgroup per CU): the same conv contract,
+    prologue and per-64-row-slice statistics (two wave rows per slice) as the 256-thread forms."""
+    test_conv_sk_prologue(k, stride, cin, cout, hw, tile=4)
+
+
+def test_dense_512_thread_tile():
+    K = _K()
+    M, N, Kd = 3000, 320, 640
+    a, b = rnd(M, Kd, seed=61), rnd(N, Kd, seed=62)
+    ad, bd = a.float().to(DEV), b.float().to(DEV)
+    c = torch.empty(M, N, device=DEV)
+    stats = torch.empty(K.stat_tiles(M), N, 2, device=DEV)
+    ws = K.gemm_workspace(DEV)
+    K.gemm_sk(K.problem(M, N, Kd, ad, Kd, bd, Kd, c, N, stats=stats), 0, ws, 4)
+    torch.cuda.synchronize()
+    check(c, a @ b.T, a.abs() @ b.abs().T, "512-thread dense")
+    s = stats.double().cpu()
+    Cd = c.double().cpu()
+    for sl in range(K.stat_tiles(M)):
+        rows = Cd[64 * sl: 64 * (sl + 1)]
+        torch.testing.assert_close(s[sl, :, 0], rows.sum(0), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("cin,hw,cout,k,stride,want_nt", [(256, 14, 256, 3, 1, 512), (64, 56, 64, 3, 1, 256),
+                                                          (128, 28, 512, 1, 1, 256), (512, 7, 2048, 1, 1, 512),
+                                                          (64, 56, 256, 1, 1, 512)])
+def test_auto_tile_picks_512_thread_form(cin, hw, cout, k, stride, want_nt):
+    """TILE_AUTO's choice of workgroup form on encoder conv shapes (batch 64), as measured by
+    tools/w8_ab.sh; with the bf16-operand flag the 256-thread kernel is always used."""
+    K = _K()
+    N = 64
+    Ho = (hw + 2 * (k // 2) - k) // stride + 1
+    M, Kd = N * Ho * Ho, k * k * cin
+    x = torch.empty(N, hw, hw, cin, device=DEV)
+    w = torch.empty(cout, Kd, device=DEV)
+    y = torch.empty(M, cout, device=DEV)
+    geo = dict(N=N, H=hw, W=hw, Cin=cin, KH=k, KW=k, stride=stride, pad=k // 2, Ho=Ho, Wo=Ho)
+    sc = torch.empty(cin, device=DEV)
+    prob = K.problem(M, cout, Kd, x, 0, w, Kd, y, cout, conv=geo, in_scale=sc, in_shift=sc)
+    assert K.gemm_sk_plan(prob, 2, threads=True)[4] == want_nt
+    assert K.gemm_sk_plan(prob, 2, bf16=True, threads=True)[4] == 256
+    name = K.gemm_sk_kernel_name(prob, 2)
+    assert name.startswith("gemm_nt8_kernel<2, true," if want_nt == 512 else "gemm_nt_kernel<")

@@ -12,11 +12,17 @@ import torch  # noqa: E402
 from capmi import kernels as K  # noqa: E402
 from capmi._lib import CAPMI_A_CONV_NHWC, CAPMI_A_KMAJOR  # noqa: E402
 
-SHAPES = {  # name: (Cin, H, W, Cout, k, prologue)
+SHAPES = {  # name: (Cin, H, W, Cout, k, prologue[, stride]) -- ResNet-101 encoder convs at 224x224
     "l3c2": (256, 14, 14, 256, 3, True), "l3c3": (256, 14, 14, 1024, 1, True),
     "l3c1": (1024, 14, 14, 256, 1, False), "l1c2": (64, 56, 56, 64, 3, True),
     "l1c3": (64, 56, 56, 256, 1, True), "l4c2": (512, 7, 7, 512, 3, True), "l2c2": (128, 28, 28, 128, 3, True),
-    "l1c2s": (64, 56, 56, 64, 3, True)}
+    "l1c2s": (64, 56, 56, 64, 3, True),
+    "l1c1": (256, 56, 56, 64, 1, False), "l2c1": (512, 28, 28, 128, 1, False), "l2c3": (128, 28, 28, 512, 1, True),
+    "l4c1": (2048, 7, 7, 512, 1, False), "l4c3": (512, 7, 7, 2048, 1, True),
+    "l2c2s": (128, 56, 56, 128, 3, True, 2), "l3c2s": (256, 28, 28, 256, 3, True, 2),
+    "l4c2s": (512, 14, 14, 512, 3, True, 2), "ds1": (64, 56, 56, 256, 1, False, 1),
+    "ds2": (256, 56, 56, 512, 1, False, 2), "ds3": (512, 28, 28, 1024, 1, False, 2),
+    "ds4": (1024, 14, 14, 2048, 1, False, 2)}
 
 
 def main():
@@ -30,10 +36,12 @@ def main():
     ap.add_argument("--nopro", action="store_true", help="drop the BN-apply+ReLU prologue (1x1: dense A)")
     a = ap.parse_args()
     dev = "cuda"
-    ci, H, W, co, k, pro = SHAPES[a.shape]
+    ci, H, W, co, k, pro, *st = SHAPES[a.shape]
+    stride = st[0] if st else 1
     pro = pro and not a.nopro
     N = a.batch
-    M, Kd = N * H * W, ci * k * k
+    Ho, Wo = (H + 2 * (k // 2) - k) // stride + 1, (W + 2 * (k // 2) - k) // stride + 1
+    M, Kd = N * Ho * Wo, ci * k * k
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.rand(N, H, W, ci, device=dev, generator=g) - 0.5
     w = torch.rand(co, Kd, device=dev, generator=g) - 0.5
@@ -41,8 +49,8 @@ def main():
     stats = torch.empty(K.stat_tiles(M, 1) * co * 2 + 64, device=dev)
     sc = torch.rand(ci, device=dev, generator=g) + 0.5
     sh = torch.rand(ci, device=dev, generator=g) - 0.5
-    geo = dict(N=N, H=H, W=W, Cin=ci, KH=k, KW=k, stride=1, pad=k // 2, Ho=H, Wo=W)
-    if k == 1 and not pro:
+    geo = dict(N=N, H=H, W=W, Cin=ci, KH=k, KW=k, stride=stride, pad=k // 2, Ho=Ho, Wo=Wo)
+    if k == 1 and not pro and stride == 1:
         prob, mode = K.problem(M, co, Kd, x, ci, w, Kd, y, co, stats=stats), CAPMI_A_KMAJOR
     else:
         prob = K.problem(M, co, Kd, x, 0, w, Kd, y, co, conv=geo, stats=stats,
@@ -52,14 +60,14 @@ def main():
     if a.bf16io:
         xb, wb = x.to(torch.bfloat16), w.to(torch.bfloat16)
         yb = torch.empty(M, co, device=dev, dtype=torch.bfloat16)
-        if k == 1:
+        if k == 1 and stride == 1:
             prob, mode = K.problem_bf16(M, co, Kd, xb, ci, wb, Kd, yb, co, stats=stats), CAPMI_A_KMAJOR
         else:
             prob = K.problem_bf16(M, co, Kd, xb, 0, wb, Kd, yb, co, stats=stats, conv=geo)
             mode = CAPMI_A_CONV_NHWC
         run = lambda: K.gemm_bf16(prob, mode, ws, a.tile)  # noqa: E731
     else:
-        print("plan (bm, bn, stream_k, generic):", K.gemm_sk_plan(prob, mode, a.tile))
+        print("plan (bm, bn, stream_k, generic, threads):", K.gemm_sk_plan(prob, mode, a.tile, bf16=a.bf16, threads=True))
         run = lambda: K.gemm_sk(prob, mode, ws, a.tile, bf16=a.bf16)  # noqa: E731
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     run()
