@@ -27,6 +27,8 @@ its clamp+Adam update is applied at the start of step k+1's decoder, after step 
 encoder forward has been launched: the encoder does not read the decoder's weights, so the
 collective overlaps the ResNet forward. ``flush()`` completes the last pending update.
 """
+import os
+
 import torch
 
 from . import decoder_fn as DF
@@ -72,8 +74,9 @@ class AttentionTrainStep:
             self._pg = None
             self._pg_key = None
             lo, hi = torch.cuda.Stream.priority_range()
-            self.s_enc = torch.cuda.Stream(device=dev, priority=lo)
-            self.s_dec = torch.cuda.Stream(device=dev, priority=hi)
+            pe, pd = {"swap": (hi, lo), "equal": (lo, lo)}.get(os.environ.get("CAPMI_PIPE_PRIO", ""), (lo, hi))
+            self.s_enc = torch.cuda.Stream(device=dev, priority=pe)
+            self.s_dec = torch.cuda.Stream(device=dev, priority=pd)
             self._feats = [None, None]
             self._slot = 0
             self._pend = None
