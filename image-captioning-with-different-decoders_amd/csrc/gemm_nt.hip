@@ -387,8 +387,15 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
     // The loads and stores are unconditional (tiles past the end load masked dummies and park
     // zeros in the unused buffer): a branch around them makes the compiler's vmcnt merge at the
     // join wait for the loads just issued, i.e. it silently drops the second prefetch stage.
+    // 512-thread form: a scheduling fence after the loads keeps them at the top of the k-step.
+    // Without it the scheduler sinks them below most of the step's MFMAs (and then consumes
+    // the A loads with the BN prologue right after issuing them, vmcnt(1) in the ISA), so the
+    // "two k-steps ahead" prefetch had well under one step of MFMA work to land behind
+    // (tools/fence_ab.sh: headline +1.5 %, dominant conv 88-90 -> 92-93 TF/s; the 256-thread
+    // 128x64 form measured 2 % slower with it, so it is not fenced).
     auto kstep = [&](Stage& ld, const Stage& sv, int kt) {
       load_tile(ld, kt + 2);
+      if (NT == 512) __builtin_amdgcn_sched_barrier(0);
       compute(kt & 1);
       store_tile(sv, (kt + 1) & 1);
       __syncthreads();

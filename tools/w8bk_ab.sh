@@ -1,4 +1,5 @@
 # A/B of the k-tile depth of the 512-thread fp32 conv form (CAPMI_W8_BK=32|64): parity tests with
+# (CAPMI_W8_BK was removed after this measurement; the knob lives in git history)
 # 64, per-shape timings, then the headline bench with each
 set -e
 mkdir -p gpurun_out; : > gpurun_out/w8bk_ab.txt
