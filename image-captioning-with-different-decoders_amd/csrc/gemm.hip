@@ -546,6 +546,14 @@ bool sk_xcd_groups() {
   }();
   return on;
 }
+// hybrid data-parallel + stream-K schedule (gemm_nt.hip); CAPMI_SK_HYBRID=0 turns it off (A/B)
+bool sk_hybrid() {
+  static const bool on = [] {
+    const char* e = getenv("CAPMI_SK_HYBRID");
+    return !(e && e[0] == '0' && e[1] == 0);
+  }();
+  return on;
+}
 // the launch capmi_gemm_sk makes for a problem (shared by the launcher and the plan query)
 int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, bool bf16, GemmPlan& g, bool& sk) {
   CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
@@ -568,6 +576,8 @@ int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, bo
   }
   const long long slots = (long long)cu_count() * (g.nt == 512 ? 1 : gemm_nt_wg_per_cu(g.bm, g.bn));
   const long long tiles = g.total;
+  // short k-loops (< 16 k-tiles) stay data-parallel even in the hybrid form: splitting the last
+  // rounds' tiles there cost 6-10 % on the layer1-3 1x1 shapes (tools/hybrid_ab.sh)
   sk = g.nt_ok && prob->ksplit == 1 && tiles > 0 && (!automatic || nkt >= 16);
   if (sk) {
     // stream-K only when the data-parallel grid would leave a costly partial last round
@@ -664,7 +674,9 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   const long long slots = (long long)cus * (g.nt == 512 ? 1 : gemm_nt_wg_per_cu(g.bm, g.bn));
   GemmArgs& a = g.a;
   a.sk_nkt = (prob->K + 31) / 32;
-  a.sk_units = g.total * a.sk_nkt;
+  // hybrid: with more than two rounds of tiles, all but the last 1-2 rounds' worth run whole
+  a.sk_dp_tiles = sk_hybrid() && g.total >= 2 * slots ? (int)((g.total / slots - 1) * slots) : 0;
+  a.sk_units = (g.total - a.sk_dp_tiles) * a.sk_nkt;
   a.sk_workers = (int)std::min<long long>(slots, a.sk_units);
   a.sk_groups = sk_xcd_groups() && a.sk_workers % 8 == 0 && g.total >= 64 ? 8 : 1;
   a.sk_flags = static_cast<int*>(workspace);

@@ -14,7 +14,8 @@ struct GemmArgs {
   // stream-K (gemm_nt only, one problem, no k-split): 0 workers = data-parallel launch
   int sk_workers;
   int sk_nkt;            // k-tiles per output tile
-  long long sk_units;    // tiles * sk_nkt
+  long long sk_units;    // stream-K tiles * sk_nkt
+  int sk_dp_tiles;       // tiles after the stream-K ones, run whole by the workers first (a multiple of workers)
   int sk_groups;         // 1, or 8: tiles and workers split into blockIdx%8 groups (XCD-local)
   float* sk_part;        // [workers][BM*BN] parked k-prefix partials
   int* sk_flags;         // [workers + 1], zero between launches; [workers] = spin-timeout flag

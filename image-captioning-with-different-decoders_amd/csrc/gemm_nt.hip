@@ -555,10 +555,24 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
   // under the observed round-robin placement that is one XCD, whose 4 MB L2 then holds its
   // range's A rows instead of every XCD streaming all of them (speed only). A worker still
   // only waits on workers with a lower blockIdx (same group, earlier in the group's order).
+  //
+  // Hybrid (sk_dp_tiles > 0, grids of more than two rounds): the tiles after the first
+  // T = sk_units / nkt are run whole, round-robin over the workers (XCD-aware: each round's
+  // tiles are cut into 8 contiguous chunks, one per blockIdx % 8), before the worker's stream-K
+  // segment; only the last one-to-two rounds' worth of tiles is balanced by stream-K.
   const capmi_gemm_problem& P = args.p[0];
   const int nkt = args.sk_nkt, tiles_n = args.tiles_n[0];
   const long long ngrp = args.sk_groups, grp = blockIdx.x % ngrp;
   const long long T = args.sk_units / nkt, G = gridDim.x / ngrp, w = blockIdx.x / ngrp;
+  if (args.sk_dp_tiles > 0) {
+    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = blockIdx.x & 7;
+    const int pos = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (blockIdx.x >> 3);
+    for (long long t = T + pos; t < T + args.sk_dp_tiles; t += nwg) {
+      const int tm = (int)(t / tiles_n), tn = (int)(t % tiles_n);
+      mainloop(P, tm * BM, tn * BN, 0, P.K);
+      epilogue(P, tm, tn, 0);
+    }
+  }
   const long long ub = grp * T / ngrp * nkt, U = ((grp + 1) * T / ngrp) * nkt - ub;
   const long long u0 = ub + w * U / G, u1 = ub + (w + 1) * U / G;
   if (u0 >= u1) return;

@@ -327,3 +327,30 @@ def test_auto_tile_picks_512_thread_form(cin, hw, cout, k, stride, want_nt):
     assert K.gemm_sk_plan(prob, 2, bf16=True, threads=True)[4] == 256
     name = K.gemm_sk_kernel_name(prob, 2)
     assert name.startswith("gemm_nt8_kernel<2, true," if want_nt == 512 else "gemm_nt_kernel<")
+
+
+@pytest.mark.parametrize("tile", [1, 2, 4])
+def test_gemm_sk_hybrid_rounds(tile):
+    """Grids of more than two rounds of tiles: the hybrid schedule runs all but the last 1-2
+    rounds' worth of tiles whole (round-robin over the persistent workers) before stream-K
+    balances the rest -- same result and statistics as the fp64 product, deterministic."""
+    K = _K()
+    M, N, Kd = 140000 if tile != 4 else 70000, 64 if tile != 4 else 256, 576
+    X, W = rnd(M, Kd, seed=71), rnd(N, Kd, seed=72)
+    Xd, Wd = X.float().to(DEV), W.float().to(DEV)
+    C = torch.empty(M, N, device=DEV)
+    stats = torch.empty(K.stat_tiles(M), N, 2, device=DEV)
+    ws = K.gemm_workspace(DEV)
+    prob = K.problem(M, N, Kd, Xd, Kd, Wd, Kd, C, N, stats=stats)
+    bm, bn, sk, _ = K.gemm_sk_plan(prob, 0, tile)
+    slots = torch.cuda.get_device_properties(0).multi_processor_count * (4 if bm == bn == 64 else 2 if tile != 4 else 1)
+    assert sk == 1 and ((M + bm - 1) // bm) * ((N + bn - 1) // bn) >= 2 * slots, "not a hybrid grid"
+    K.gemm_sk(prob, 0, ws, tile)
+    first = C.clone()
+    K.gemm_sk(prob, 0, ws, tile)
+    torch.cuda.synchronize()
+    assert torch.equal(first, C)
+    check(C, X @ W.T, X.abs() @ W.abs().T, f"hybrid stream-K tile {tile}")
+    Cd = C.double().cpu()
+    s = stats.double().cpu().sum(0)
+    torch.testing.assert_close(s[:, 0], Cd.sum(0), rtol=1e-5, atol=1e-2)
