@@ -6,6 +6,8 @@
 // Reference: models/encoder.py:88-92 (resnet children()[:-2], AdaptiveAvgPool2d(14,14)),
 // :107-110 (forward + permute to NHWC); BN in train mode because of
 // models/attention.py:374 (encoder.train()).
+#include <cstdlib>
+
 #include "common.h"
 
 __global__ void conv_weight_pack_kernel(const float* __restrict__ w, int Cout, int Cin, int KH,
@@ -182,40 +184,63 @@ bn_finalize_kernel(const float* __restrict__ stats, int tiles, int C, int per_g,
   if (cl == 0) __hip_atomic_store(counters + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Small statistics buffers (tiles <= BNF_DIRECT: layer3/layer4 at batch 64): one 1024-thread block
-// per 64 channels reads every slice itself (16 slice rows x 8 loads in flight per lane = at most
-// two memory round trips) and finalizes -- no partials, no arrival counter, one launch latency.
+// Direct finalize: each 1024-thread block reads every slice of its channels itself and finalizes --
+// no partials, no arrival counter, one launch latency. Block width by slice count (batch 64):
+// <= 64 slices (layer4) 64 channels x 8 loads in flight; 65-256 (layer3) 16 channels x 4 loads;
+// more (layer1/2: 784 / 3136 slices) 4 channels x 16 loads, one round of loads up to 4096 slices
+// (it replaced the two-level group kernel below: 7-8 -> 4.4-5.3 us per call, tools/bnf_ab.sh).
 constexpr int BNF_DIRECT = 256;
+// CAPMI_BNF_NARROW=0: always the 64-channel form (A/B measurement)
+bool bnf_narrow() {
+  static const bool on = [] {
+    const char* e = getenv("CAPMI_BNF_NARROW");
+    return !(e && e[0] == '0' && e[1] == 0);
+  }();
+  return on;
+}
 
+// CW channels per workgroup: a wave reads 64 / CW slice rows of CW channels per load. CW = 16
+// spreads a layer3-sized reduction (196 slices) over 4x more CUs in one round of loads; CW = 64
+// (fewer, wider workgroups) is the faster form for layer4's 49 slices.
+template <int CW, int U>
 __global__ void __launch_bounds__(1024)
 bn_finalize_direct_kernel(const float* __restrict__ stats, int tiles, int C, long long count,
                           const float* __restrict__ gamma, const float* __restrict__ beta, float* running_mean,
                           float* running_var, float momentum, float eps, float* __restrict__ scale,
                           float* __restrict__ shift, float* save_mean, float* save_var) {
-  __shared__ double rs[16][64], rq[16][64];
-  const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  constexpr int TS = 64 / CW, ROWS = 16 * TS;
+  __shared__ double rs[16][CW], rq[16][CW];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cl = lane % CW, ts = lane / CW;
+  const int c = blockIdx.x * CW + cl;
   double s = 0.0, q = 0.0;
   if (c < C) {
-    for (int t = tl; t < tiles; t += 128) {
-      float2 v[8];
+    for (int t = w * TS + ts; t < tiles; t += ROWS * U) {
+      float2 v[U];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int tt = t + 16 * u;
+      for (int u = 0; u < U; ++u) {
+        const int tt = t + ROWS * u;
         v[u] = tt < tiles ? *reinterpret_cast<const float2*>(stats + ((long long)tt * C + c) * 2)
                           : make_float2(0.f, 0.f);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < U; ++u) {
         s += v[u].x;
         q += v[u].y;
       }
     }
   }
-  rs[tl][cl] = s;
-  rq[tl][cl] = q;
+#pragma unroll
+  for (int o = CW; o < 64; o <<= 1) {  // the TS slice lanes of a channel, fixed order
+    s += __shfl_xor(s, o);
+    q += __shfl_xor(q, o);
+  }
+  if (ts == 0) {
+    rs[w][cl] = s;
+    rq[w][cl] = q;
+  }
   __syncthreads();
-  if (tl != 0 || c >= C) return;
+  if (w != 0 || ts != 0 || c >= C) return;
   s = 0.0;
   q = 0.0;
 #pragma unroll
@@ -250,13 +275,26 @@ extern "C" int capmi_bn_finalize(const float* stats, int tiles, int C, long long
   CAPMI_REQUIRE((running_mean == nullptr) == (running_var == nullptr), CAPMI_EINVAL);
   CAPMI_REQUIRE(((uintptr_t)stats & 7) == 0 && ((uintptr_t)work & 15) == 0, CAPMI_EALIGN);
   CAPMI_REQUIRE(C <= 8192, CAPMI_ERANGE);
-  if (tiles <= BNF_DIRECT) {
-    hipLaunchKernelGGL(bn_finalize_direct_kernel, dim3(cdiv(C, 64)), dim3(1024), 0, as_stream(stream), stats,
-                       tiles, C, count, gamma, beta, running_mean, running_var, momentum, eps, scale, shift,
-                       save_mean, save_var);
+  hipStream_t st = as_stream(stream);
+#define CAPMI_BNF_DIRECT(CW, U)                                                                            \
+  hipLaunchKernelGGL((bn_finalize_direct_kernel<CW, U>), dim3(cdiv(C, CW)), dim3(1024), 0, st, stats, tiles, C, \
+                     count, gamma, beta, running_mean, running_var, momentum, eps, scale, shift, save_mean,      \
+                     save_var)
+  if (tiles <= 64 || !bnf_narrow()) {
+    if (tiles <= BNF_DIRECT) {
+      CAPMI_BNF_DIRECT(64, 8);
+      CAPMI_LAUNCH_CHECK();
+      return 0;
+    }
+  } else {
+    if (tiles <= BNF_DIRECT)
+      CAPMI_BNF_DIRECT(16, 4);
+    else
+      CAPMI_BNF_DIRECT(4, 16);  // one round of loads up to 4096 slices, no partials or counters
     CAPMI_LAUNCH_CHECK();
     return 0;
   }
+#undef CAPMI_BNF_DIRECT
   const int G = std::min(BNF_MAXG, std::max(1, (tiles + 127) / 128));
   const int per_g = (tiles + G - 1) / G;
   // [0, 64 doubles): the arrival counters (one int per 64-channel block, fixed place whatever
