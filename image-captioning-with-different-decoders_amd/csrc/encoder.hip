@@ -332,19 +332,28 @@ extern "C" int capmi_bn_eval_params(const float* gamma, const float* beta, const
 // ---------------------------------------------------------------------------------
 // out = relu(y*s + b + (res_scale ? res*rs + rb : res))
 // ---------------------------------------------------------------------------------
-__global__ void bn_add_relu_kernel(const float4* __restrict__ y, const float* __restrict__ s,
-                                   const float* __restrict__ b, const float4* __restrict__ res,
-                                   const float* __restrict__ rs, const float* __restrict__ rb,
-                                   float4* __restrict__ out, long long n4, int C4) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C4) * 4;
-    const float4 sc = *reinterpret_cast<const float4*>(s + c);
-    const float4 sh = *reinterpret_cast<const float4*>(b + c);
-    float4 r = res[i];
-    if (rs) r = fma4(r, *reinterpret_cast<const float4*>(rs + c), *reinterpret_cast<const float4*>(rb + c));
-    out[i] = relu4(fma4(y[i], sc, sh) + r);
+// Two float4 per thread, both loads of y and res in flight before any math, 32-bit indexing (the
+// grid covers n4 exactly once: no grid-stride tail round, no 64-bit modulo per element).
+template <bool RBN>
+__global__ void __launch_bounds__(256) bn_add_relu_kernel(const float4* __restrict__ y, const float* __restrict__ s,
+                                                           const float* __restrict__ b,
+                                                           const float4* __restrict__ res,
+                                                           const float* __restrict__ rs,
+                                                           const float* __restrict__ rb, float4* __restrict__ out,
+                                                           int n4, int C4) {
+  const int i0 = blockIdx.x * 512 + threadIdx.x, i1 = i0 + 256;
+  const bool ok0 = i0 < n4, ok1 = i1 < n4;
+  const float4 y0 = ok0 ? y[i0] : f4(0.f), y1 = ok1 ? y[i1] : f4(0.f);
+  float4 r0 = ok0 ? res[i0] : f4(0.f), r1 = ok1 ? res[i1] : f4(0.f);
+  const int c0 = (i0 % C4) * 4, c1 = (i1 % C4) * 4;
+  if (RBN) {
+    r0 = fma4(r0, *reinterpret_cast<const float4*>(rs + c0), *reinterpret_cast<const float4*>(rb + c0));
+    r1 = fma4(r1, *reinterpret_cast<const float4*>(rs + c1), *reinterpret_cast<const float4*>(rb + c1));
   }
+  const float4 o0 = relu4(fma4(y0, *reinterpret_cast<const float4*>(s + c0), *reinterpret_cast<const float4*>(b + c0)) + r0);
+  const float4 o1 = relu4(fma4(y1, *reinterpret_cast<const float4*>(s + c1), *reinterpret_cast<const float4*>(b + c1)) + r1);
+  if (ok0) out[i0] = o0;
+  if (ok1) out[i1] = o1;
 }
 
 extern "C" int capmi_bn_add_relu(const float* y, const float* s, const float* b, const float* res,
@@ -353,11 +362,17 @@ extern "C" int capmi_bn_add_relu(const float* y, const float* s, const float* b,
   CAPMI_REQUIRE(y && s && b && res && out && rows >= 0 && C > 0 && C % 4 == 0, CAPMI_EINVAL);
   CAPMI_REQUIRE(aligned16(y) && aligned16(res) && aligned16(out) && aligned16(s) && aligned16(b),
                 CAPMI_EALIGN);
+  CAPMI_REQUIRE((res_scale == nullptr) == (res_shift == nullptr), CAPMI_EINVAL);
   const long long n4 = rows * C / 4;
   if (n4 == 0) return 0;
-  hipLaunchKernelGGL(bn_add_relu_kernel, dim3(std::min<long long>(cdiv(n4, 256), 8192)), dim3(256),
-                     0, as_stream(stream), (const float4*)y, s, b, (const float4*)res, res_scale,
-                     res_shift, (float4*)out, n4, C / 4);
+  CAPMI_REQUIRE(n4 < (1LL << 31) - 512, CAPMI_ERANGE);
+  const dim3 g((unsigned)cdiv(n4, 512)), blk(256);
+  if (res_scale)
+    hipLaunchKernelGGL(bn_add_relu_kernel<true>, g, blk, 0, as_stream(stream), (const float4*)y, s, b,
+                       (const float4*)res, res_scale, res_shift, (float4*)out, (int)n4, C / 4);
+  else
+    hipLaunchKernelGGL(bn_add_relu_kernel<false>, g, blk, 0, as_stream(stream), (const float4*)y, s, b,
+                       (const float4*)res, res_scale, res_shift, (float4*)out, (int)n4, C / 4);
   CAPMI_LAUNCH_CHECK();
   return 0;
 }

@@ -70,3 +70,21 @@ def test_encoder_surface():
     enc.fine_tune(True)
     assert not any(p.requires_grad for p in list(enc.resnet.children())[4].parameters())
     assert all(p.requires_grad for p in list(enc.resnet.children())[5].parameters())
+
+
+@pytest.mark.parametrize("rows,C,rbn", [(12544, 1024, False), (3137, 256, True), (5, 12, False), (1, 4, True)])
+def test_bn_add_relu_elementwise(rows, C, rbn):
+    """out = relu(y*s + b + (res*rs + rb | res)) elementwise vs torch fp32 (same fma order up to
+    contraction: 1 ulp), ragged sizes (n4 not a multiple of the 512 float4 a block covers)."""
+    from capmi import kernels as K
+    g = torch.Generator().manual_seed(rows + C)
+    y, res = (torch.randn(rows, C, generator=g) for _ in range(2))
+    s, b, rs, rb = (torch.randn(C, generator=g) for _ in range(4))
+    r = res * rs + rb if rbn else res
+    want = torch.relu(y * s + b + r)
+    d = [x.to(DEV) for x in (y, s, b, res, rs, rb)]
+    out = torch.full((rows, C), float("nan"), device=DEV)
+    K.bn_add_relu(d[0], d[1], d[2], d[3], out, rows, C, res_scale=d[4] if rbn else None,
+                  res_shift=d[5] if rbn else None)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.cpu(), want, rtol=1e-6, atol=1e-6)
