@@ -55,6 +55,30 @@ def test_gemm_rejects_bad_shapes():
     assert lib.capmi_gemm(arr, 1, 7, 0, 0, None) == 1001
 
 
+def test_gemm_sk_plan_on_host():
+    """The launch plan is host logic (no GPU work): the 512-thread form for a wide conv, the
+    256-thread kernel for N = 64 or with the bf16-operand flag, unknown flags rejected."""
+    from capmi._lib import GemmProblem, lib
+    c_int = ctypes.c_int
+
+    def plan(N, flags=0, M=12544, Cin=256):
+        p = GemmProblem()
+        p.M, p.N, p.K, p.ksplit = M, N, 9 * Cin, 1
+        p.A = p.B = p.C = 256  # 16-B aligned stand-ins: the plan never dereferences them
+        p.ldb = 9 * Cin
+        p.cN, p.cH, p.cW, p.cCin, p.cKH, p.cKW = M // 196, 14, 14, Cin, 3, 3
+        p.cStride, p.cPad, p.cHo, p.cWo = 1, 1, 14, 14
+        v = [c_int(0) for _ in range(5)]
+        rc = lib.capmi_gemm_sk_plan(ctypes.byref(p), 2, 0, 3, flags, *[ctypes.byref(x) for x in v])
+        return rc, tuple(x.value for x in v)
+
+    rc, (bm, bn, sk, generic, nt) = plan(256)
+    assert rc == 0 and (bm, bn, generic, nt) == (128, 128, 0, 512)
+    assert plan(64)[1][4] == 256
+    assert plan(256, flags=1)[1][4] == 256
+    assert plan(256, flags=4)[0] == 1001
+
+
 def test_device_tensors_required():
     from capmi import kernels as K
     x = torch.zeros(4, 4)
