@@ -21,6 +21,29 @@ def check_samples(fx, prefix, x, rtol=1e-5, atol=1e-6):
     np.testing.assert_allclose(d, fx[prefix + "__digest"], rtol=max(rtol, 1e-6) * 10, atol=atol * x.size ** 0.5)
 
 
+def check_adam_post(post, want, g_want, lr=1e-4, eps=1e-8, err_msg=""):
+    """Post-Adam parameters. The first Adam step moves a weight by lr*g/(|g|+eps)
+    (oracle/decoder_ref.py adam_step): where |g| is below ~1e-5 the step's sign and size are
+    set by gradient digits the 1e-6 gradient tolerance does not fix (fp32 sum order differs
+    between CPUs), so there the post value is only pinned to the +-lr step bound; everywhere
+    else to rtol 1e-5 / atol 1e-6."""
+    sure = np.abs(g_want) > 1e-5
+    np.testing.assert_allclose(post[sure], want[sure], rtol=1e-5, atol=1e-6, err_msg=err_msg)
+    np.testing.assert_allclose(post[~sure], want[~sure], rtol=0, atol=2 * lr, err_msg=err_msg)
+
+
+def check_adam_post_samples(fx, post_key, grad_key, post, err_msg=""):
+    """check_adam_post on the sampled fixtures; the digest allows a few near-zero-gradient
+    weights stepping the other way (attention.full_att.bias has a zero true gradient: softmax
+    is shift-invariant), so it is pinned to 1e-5 of the sum of magnitudes plus one 2*lr step."""
+    x = np.asarray(post).ravel()
+    idx = fx[post_key + "__idx"]
+    assert np.array_equal(idx, fx[grad_key + "__idx"])
+    check_adam_post(x[idx], fx[post_key + "__val"], fx[grad_key + "__val"], err_msg=err_msg)
+    want = fx[post_key + "__digest"]
+    np.testing.assert_allclose(gen.digest(x), want, rtol=0, atol=1e-5 * want[1] + 2e-4, err_msg=err_msg)
+
+
 @pytest.mark.parametrize("tag", ["prod", "small"])
 def test_soft_attention(golden, tag):
     fx = golden(f"soft_attention_{tag}")
@@ -98,10 +121,10 @@ def test_train_step(golden, tag):
         g = raw[k].numpy()
         if full:
             np.testing.assert_allclose(g, fx["grad." + k], rtol=1e-3, atol=1e-6, err_msg=k)
-            np.testing.assert_allclose(new_p[k].numpy(), fx["post." + k], rtol=1e-5, atol=1e-6, err_msg=k)
+            check_adam_post(new_p[k].numpy(), fx["post." + k], fx["grad." + k], err_msg=k)
         else:
             check_samples(fx, "grad." + k, g, rtol=1e-3, atol=1e-6)
-            check_samples(fx, "post." + k, new_p[k].numpy(), rtol=1e-5, atol=1e-6)
+            check_adam_post_samples(fx, "post." + k, "grad." + k, new_p[k].numpy(), err_msg=k)
 
 
 def _resnet_child_key(k):
@@ -137,7 +160,11 @@ def test_encoder_wrapper(golden, case):
     with torch.no_grad():
         y = encoder_attention_forward(net, t(x))
     assert list(y.shape) == list(fx["shape"])
-    check_samples(fx, "features", y.numpy(), rtol=1e-4, atol=1e-5)
+    # eval mode with random-init running stats (mean 0, var 1) leaves the activations
+    # unnormalised (features up to ~2.5e5); the host's oneDNN conv kernel choice (ISA-dependent
+    # sum order) then moves them by up to ~1.5e-3 relative. Train mode is normalised: 1e-4.
+    rtol = 1e-4 if m["mode"] == "train" else 3e-3
+    check_samples(fx, "features", y.numpy(), rtol=rtol, atol=1e-5)
 
 
 @pytest.mark.parametrize("tag", ["small", "prod"])
@@ -177,7 +204,7 @@ def test_finetune_train_step(golden):
         check_samples(fx, "post_enc." + key, out["enc_new"][n].numpy(), rtol=1e-5, atol=2e-6)
     for k, g in out["dec_raw"].items():
         check_samples(fx, "grad.dec." + k, g.numpy(), rtol=1e-3, atol=1e-6)
-        check_samples(fx, "post_dec." + k, out["dec_new"][k].numpy(), rtol=1e-5, atol=1e-6)
+        check_adam_post_samples(fx, "post_dec." + k, "grad.dec." + k, out["dec_new"][k].numpy(), err_msg=k)
 
 
 @pytest.mark.parametrize("tag", ["small", "k5", "noend"])
