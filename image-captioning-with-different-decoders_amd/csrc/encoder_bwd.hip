@@ -171,19 +171,44 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(int mode, const floa
   }
 }
 
-// stage 2: one thread per channel sums the slabs in fp64 (slab order: deterministic)
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int slabs, int C, long long count,
-                                       const float* __restrict__ gamma, const float* __restrict__ mean,
-                                       const float* __restrict__ var, float eps, float* dgamma, float* dbeta,
-                                       int accumulate, float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// stage 2: block of 256 threads = BNB_FIN_CW channels x (256 / BNB_FIN_CW) slab lanes. Each lane
+// sums its strided slabs in fp64 (all of its loads independent, so they are in flight together,
+// instead of one thread walking up to 256 slabs with one dependent load each: 60 -> a few us per
+// call), then a fixed-shape LDS tree adds the lanes: the result is deterministic run to run.
+constexpr int BNB_FIN_CW = 16;
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ part, int slabs, int C,
+                                                              long long count, const float* __restrict__ gamma,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ var, float eps,
+                                                              float* dgamma, float* dbeta, int accumulate,
+                                                              float* __restrict__ coef) {
+  constexpr int SL = 256 / BNB_FIN_CW;
+  __shared__ double ls[256], lq[256];
+  const int cl = threadIdx.x % BNB_FIN_CW, lane = threadIdx.x / BNB_FIN_CW;
+  const int c = blockIdx.x * BNB_FIN_CW + cl;
   double s = 0.0, q = 0.0;
-  for (int k = 0; k < slabs; ++k) {
-    const float2 v = *reinterpret_cast<const float2*>(part + ((long long)k * C + c) * 2);
-    s += v.x;
-    q += v.y;
+  if (c < C) {
+#pragma unroll 4
+    for (int k = lane; k < slabs; k += SL) {
+      const float2 v = *reinterpret_cast<const float2*>(part + ((long long)k * C + c) * 2);
+      s += v.x;
+      q += v.y;
+    }
   }
+  ls[threadIdx.x] = s;
+  lq[threadIdx.x] = q;
+  __syncthreads();
+#pragma unroll
+  for (int st = SL / 2; st > 0; st >>= 1) {
+    if (lane < st) {
+      ls[threadIdx.x] += ls[threadIdx.x + st * BNB_FIN_CW];
+      lq[threadIdx.x] += lq[threadIdx.x + st * BNB_FIN_CW];
+    }
+    __syncthreads();
+  }
+  if (lane != 0 || c >= C) return;
+  s = ls[cl];
+  q = lq[cl];
   const double inv = 1.0 / sqrt((double)var[c] + (double)eps);
   const double dg = q * inv, db = s;
   if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)dg : (float)dg;
@@ -222,7 +247,7 @@ extern "C" int capmi_bn_bwd_reduce(int mode, const float* d, const float* y, con
   const float* sh = shift ? shift : save_mean;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(gx, (unsigned)slabs), dim3(256), 0, s, mode, d, y, mask_src, sc,
                      sh, save_mean, rows, C, CB, per, work);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, s, work, (int)slabs, C, rows,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, BNB_FIN_CW)), dim3(256), 0, s, work, (int)slabs, C, rows,
                      gamma, save_mean, save_var, eps, dgamma, dbeta, accumulate, coef);
   CAPMI_LAUNCH_CHECK();
   return 0;
