@@ -522,6 +522,12 @@ class FineTuneRunner:
         wmax = max(b["wd"] * 9 * b["wd"] for b in blocks)
         dwp = gp("dw_packed", wmax, dev)
         wdg = gp("w_dgrad", wmax, dev)
+        # 1x1 dgrads read the weight transposed (B = W^T[n][k], CAPMI_B_NMAJOR_W), packed per step
+        # by conv_weight_pack_dgrad: that opens the 512-thread 128x128 form and the row-major B
+        # path, 10-15 % faster per launch than the k-rows B form on every layer2-4 1x1 dgrad
+        # (tools/bwd_gemm_ab.py); one buffer, reused in stream order
+        w1max = max(max(b["Cout"] * b["wd"], b["wd"] * b["Cin"], b["Cout"] * b["Cin"]) for b in blocks)
+        wt = gp("w1x1_t", w1max, dev)
         coef = gp("coef", 2 * 4 * 2048, dev).view(2, 4 * 2048)
         work = gp("bnwork", K.bnb_work_floats(2048), dev)
 
@@ -567,8 +573,9 @@ class FineTuneRunner:
                     K.problem(Cout, wd, r3, dy3, Cout, b["y2"], 0, G(c3.weight), wd, conv=geo3, in_scale=s2,
                               in_shift=b2), AMM, BCONV)
             da2 = dmid[:r3 * wd]
+            K.conv_weight_pack_dgrad(c3.weight.detach(), wt[:Cout * wd])
             run(tag + ".conv3.dgrad", 2.0 * r3 * Cout * wd,
-                K.problem(r3, wd, Cout, dy3, Cout, c3.weight, wd, da2, wd), AK, BKR)
+                K.problem(r3, wd, Cout, dy3, Cout, wt, Cout, da2, wd), AK, BW)
             # ---- bn2 + relu
             bn2 = blk.bn2
             K.bn_bwd_reduce(K.BNB_RELU_Y, da2, b["y2"], None, s2, b2, bn2.weight, m2[0], m2[1], bn2.eps, r3, wd,
@@ -603,9 +610,10 @@ class FineTuneRunner:
                 run(tag + ".conv1.wgrad", 2.0 * r1 * wd * Cin,
                     K.problem(wd, Cin, r1, da1, wd, b["x"], Cin, G(c1.weight), Cin), AMM, BKR)
             if need_dx:
+                K.conv_weight_pack_dgrad(c1.weight.detach(), wt[:wd * Cin])
                 run(tag + ".conv1.dgrad", 2.0 * r1 * wd * Cin,
-                    K.problem(r1, Cin, wd, da1, wd, c1.weight, Cin, dx, Cin, beta=1.0 if ds is None else 0.0),
-                    AK, BKR)
+                    K.problem(r1, Cin, wd, da1, wd, wt, wd, dx, Cin, beta=1.0 if ds is None else 0.0),
+                    AK, BW)
             # ---- downsample (1x1, stride s) on x
             if ds is not None:
                 cd = ds[0]
@@ -616,9 +624,10 @@ class FineTuneRunner:
                 if need_dx:
                     # dX[n, s*i, s*j, :] += dYd[n, i, j, :] W_d  (rows (n, i, j) -> strided NHWC rows)
                     rm = dict(c_r1=W2, c_s2=s * W * Cin) if s > 1 else {}
+                    K.conv_weight_pack_dgrad(cd.weight.detach(), wt[:Cout * Cin])
                     run(tag + ".downsample.dgrad", 2.0 * r3 * Cout * Cin,
-                        K.problem(r3, Cin, Cout, dyd, Cout, cd.weight, Cin, dx, s * Cin, beta=1.0, **rm),
-                        AK, BKR)
+                        K.problem(r3, Cin, Cout, dyd, Cout, wt, Cout, dx, s * Cin, beta=1.0, **rm),
+                        AK, BW)
             cur ^= 1
         self.state = None
 
