@@ -78,6 +78,22 @@ def test_gemm_sk_plan_on_host():
     assert plan(256, flags=1)[1][4] == 256
     assert plan(256, flags=4)[0] == 1001
 
+    def wgrad_plan(Cout, Cin, k):
+        # dW[Cout, (kh, kw, ci)] over k = 64*14*14 output pixels (A_MMAJOR x B_CONV_NHWC)
+        p = GemmProblem()
+        p.M, p.N, p.K, p.ksplit = Cout, k * k * Cin, 12544, 1
+        p.A = p.B = p.C = 256
+        p.lda, p.ldc = Cout, k * k * Cin
+        p.cN, p.cH, p.cW, p.cCin, p.cKH, p.cKW = 64, 14, 14, Cin, k, k
+        p.cStride, p.cPad, p.cHo, p.cWo = 1, k // 2, 14, 14
+        v = [c_int(0) for _ in range(5)]
+        rc = lib.capmi_gemm_sk_plan(ctypes.byref(p), 1, 2, 3, 0, *[ctypes.byref(x) for x in v])
+        assert rc == 0
+        return tuple(x.value for x in v)
+
+    assert wgrad_plan(256, 256, 3)[:2] == (128, 128)  # wide 3x3 weight gradient
+    assert wgrad_plan(1024, 256, 1)[:2] == (64, 64)   # 1x1 weight gradient
+
 
 def test_device_tensors_required():
     from capmi import kernels as K
