@@ -114,9 +114,9 @@ def gemm_sk_plan(prob, amode, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W, bf16
     return tuple(x.value for x in v[:5 if threads else 4])
 
 
-def gemm_sk_kernel_name(prob, amode, bmode=CAPMI_B_NMAJOR_W, bf16=False):
-    """The kernel symbol (as rocprofv3 prints it) of the launch gemm_sk(..., TILE_AUTO) makes."""
-    bm, bn, sk, generic, nt = gemm_sk_plan(prob, amode, CAPMI_TILE_AUTO, bmode, bf16, threads=True)
+def gemm_sk_kernel_name(prob, amode, bmode=CAPMI_B_NMAJOR_W, bf16=False, tile=CAPMI_TILE_AUTO):
+    """The kernel symbol (as rocprofv3 prints it) of the launch gemm_sk(..., tile) makes."""
+    bm, bn, sk, generic, nt = gemm_sk_plan(prob, amode, tile, bmode, bf16, threads=True)
     b = lambda v: "true" if v else "false"  # noqa: E731
     pro = b(bool(prob.in_scale))
     if generic:

@@ -499,8 +499,8 @@ class FineTuneRunner:
         return out
 
     # ------------------------------------------------------------------ backward
-    def _gemm(self, prob, amode, bmode):
-        K.gemm_sk(prob, amode, self.r._ws["sk"], K.TILE_AUTO, bmode)
+    def _gemm(self, prob, amode, bmode, tile=K.TILE_AUTO):
+        K.gemm_sk(prob, amode, self.r._ws["sk"], tile, bmode)
 
     @torch.no_grad()
     def backward(self, dfeat, grads, hook=None):
@@ -534,11 +534,12 @@ class FineTuneRunner:
         def G(p):
             return grads.get(id(p))
 
-        def run(tag, flops, prob, amode, bmode):
+        def run(tag, flops, prob, amode, bmode, tile=K.TILE_AUTO):
             if hook is None:
-                self._gemm(prob, amode, bmode)
+                self._gemm(prob, amode, bmode, tile)
             else:
-                hook(tag, flops, lambda: self._gemm(prob, amode, bmode), K.gemm_sk_kernel_name(prob, amode, bmode))
+                hook(tag, flops, lambda: self._gemm(prob, amode, bmode, tile),
+                     K.gemm_sk_kernel_name(prob, amode, bmode, tile=tile))
 
         K.adaptive_avgpool_bwd_nhwc(dfeat.contiguous(), N, stt["H"], stt["W"], stt["C"], stt["OH"], stt["OW"],
                                     dA[0])
@@ -608,7 +609,8 @@ class FineTuneRunner:
             c1 = blk.conv1
             if G(c1.weight) is not None:
                 run(tag + ".conv1.wgrad", 2.0 * r1 * wd * Cin,
-                    K.problem(wd, Cin, r1, da1, wd, b["x"], Cin, G(c1.weight), Cin), AMM, BKR)
+                    K.problem(wd, Cin, r1, da1, wd, b["x"], Cin, G(c1.weight), Cin), AMM, BKR,
+                    K.TILE_64)  # 5-7 % faster than the auto 128x64 on layer2-4 (tools/bwd_gemm_ab.py)
             if need_dx:
                 K.conv_weight_pack_dgrad(c1.weight.detach(), wt[:wd * Cin])
                 run(tag + ".conv1.dgrad", 2.0 * r1 * wd * Cin,

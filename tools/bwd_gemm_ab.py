@@ -63,6 +63,10 @@ def main():
             plan = K.gemm_sk_plan(prob, amode, K.TILE_AUTO, CAPMI_B_KROWS, threads=True)
             f = 2.0 * M * N * Kd
             extra = ""
+            if cname.endswith("wgrad"):
+                for tn, t in (("64", K.TILE_64), ("128", K.TILE_128), ("128x64", K.TILE_128x64)):
+                    us = timeit(lambda: K.gemm_sk(prob, amode, ws, t, CAPMI_B_KROWS))
+                    extra += f" | {tn}: {us:.1f} us ({f / us / 1e6:.1f} TF/s)"
             if cname.endswith("dgrad"):
                 # B = W[n][k]: the 1x1 weight transposed by conv_weight_pack_dgrad (CAPMI_B_NMAJOR_W)
                 wsrc = w1 if cname == "conv1.dgrad" else w3
