@@ -266,6 +266,15 @@ def conv_weight_pack_dgrad(w, out):
     call("capmi_conv_weight_pack_dgrad", ptr(w), co, ci, kh, kw, ptr(out), stream())
 
 
+def conv_weight_pack_dgrad_s2(w, ph, pw, out):
+    """3x3 stride-2 conv, parity class (ph, pw): out[ci][th][tw][co] = w[co][ci][kh(th)][kw(tw)],
+    kh = 1 (ph = 0) or 2 - 2*th (ph = 1)."""
+    _cuda(w, out)
+    co, ci, kh, kw = w.shape
+    assert (kh, kw) == (3, 3) and w.is_contiguous() and out.numel() >= co * ci * (ph + 1) * (pw + 1)
+    call("capmi_conv_weight_pack_dgrad_s2", ptr(w), co, ci, int(ph), int(pw), ptr(out), stream())
+
+
 def conv_weight_unpack(packed, shape, out):
     """[Cout][KH][KW][Cin] -> out [Cout][Cin][KH][KW] (``shape`` = nn.Conv2d weight shape)"""
     _cuda(packed, out)

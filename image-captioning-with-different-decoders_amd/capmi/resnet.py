@@ -518,7 +518,6 @@ class FineTuneRunner:
         dmid = gp("dmid", big, dev)
         dy3 = gp("dy3", big, dev)
         dyd = gp("dyd", big, dev)
-        up = gp("up", big, dev)
         wmax = max(b["wd"] * 9 * b["wd"] for b in blocks)
         dwp = gp("dw_packed", wmax, dev)
         wdg = gp("w_dgrad", wmax, dev)
@@ -590,16 +589,26 @@ class FineTuneRunner:
                     K.problem(wd, 9 * wd, r3, da2, wd, b["y1"], 0, dwp, 9 * wd, conv=geo2, in_scale=s1,
                               in_shift=b1), AMM, BCONV)
                 K.conv_weight_unpack(dwp, tuple(c2.weight.shape), G(c2.weight))
-            K.conv_weight_pack_dgrad(c2.weight.detach().contiguous(), wdg[:wd * 9 * wd])
-            if s == 1:
-                src = da2
-            else:
-                src = up[:r1 * wd]
-                K.zero_upsample2_nhwc(da2, N, H2, W2, wd, H, W, src)
             da1 = dy3[:r1 * wd]  # dy3 is consumed
-            geod = dict(N=N, H=H, W=W, Cin=wd, KH=3, KW=3, stride=1, pad=1, Ho=H, Wo=W)
-            run(tag + ".conv2.dgrad", 2.0 * r3 * wd * 9 * wd,
-                K.problem(r1, wd, 9 * wd, src, 0, wdg, 9 * wd, da1, wd, conv=geod), AC, BW)
+            if s == 1:
+                K.conv_weight_pack_dgrad(c2.weight.detach().contiguous(), wdg[:wd * 9 * wd])
+                geod = dict(N=N, H=H, W=W, Cin=wd, KH=3, KW=3, stride=1, pad=1, Ho=H, Wo=W)
+                run(tag + ".conv2.dgrad", 2.0 * r3 * wd * 9 * wd,
+                    K.problem(r1, wd, 9 * wd, da2, 0, wdg, 9 * wd, da1, wd, conv=geod), AC, BW)
+            else:
+                # sub-pixel form: input pixel (2i+ph, 2j+pw) is a (ph+1)x(pw+1) stride-1 pad-0 conv of
+                # dY (9 taps over the 4 classes, vs 36 on a zero-upsampled grid); the class's rows
+                # land at stride 2 through the output remap (H = 2*H2, W = 2*W2)
+                assert H == 2 * H2 and W == 2 * W2
+                for ph in (0, 1):
+                    for pw in (0, 1):
+                        th, tw = ph + 1, pw + 1
+                        kk = th * tw * wd
+                        K.conv_weight_pack_dgrad_s2(c2.weight.detach().contiguous(), ph, pw, wdg[:wd * kk])
+                        geoc = dict(N=N, H=H2, W=W2, Cin=wd, KH=th, KW=tw, stride=1, pad=0, Ho=H2, Wo=W2)
+                        run(tag + f".conv2.dgrad.p{ph}{pw}", 2.0 * r3 * wd * kk,
+                            K.problem(r3, wd, kk, da2, 0, wdg, kk, da1[(ph * W + pw) * wd:], 2 * wd, conv=geoc,
+                                      c_r1=W2, c_s2=2 * W * wd), AC, BW)
             # ---- bn1 + relu
             bn1 = blk.bn1
             K.bn_bwd_reduce(K.BNB_RELU_Y, da1, b["y1"], None, s1, b1, bn1.weight, m1[0], m1[1], bn1.eps, r1, wd,

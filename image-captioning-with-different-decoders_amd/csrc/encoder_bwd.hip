@@ -45,6 +45,37 @@ extern "C" int capmi_conv_weight_pack_dgrad(const float* w, int Cout, int Cin, i
   return 0;
 }
 
+// Sub-pixel data gradient of a 3x3 / stride-2 / pad-1 conv: input pixel (2i+ph, 2j+pw) receives
+// dY[i+th][j+tw] * W[kh(th)][kw(tw)] with kh = 1 for ph = 0 (one tap) and kh = 2, 0 for th = 0, 1
+// when ph = 1 (two taps); same along w. out[ci][th][tw][co] = w[co][ci][kh(th)][kw(tw)], the B
+// operand of the parity class's (1|2)x(1|2) stride-1 pad-0 conv over dY.
+__global__ void conv_weight_pack_dgrad_s2_kernel(const float* __restrict__ w, int Cout, int Cin, int ph, int pw,
+                                                 float* __restrict__ out) {
+  const int TH = ph + 1, TW = pw + 1;
+  const long long n = (long long)Cout * Cin * TH * TW;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int co = (int)(i % Cout);
+    long long r = i / Cout;
+    const int tw = (int)(r % TW);
+    r /= TW;
+    const int th = (int)(r % TH);
+    const int ci = (int)(r / TH);
+    const int kh = ph ? 2 - 2 * th : 1, kw = pw ? 2 - 2 * tw : 1;
+    out[i] = w[(((long long)co * Cin + ci) * 3 + kh) * 3 + kw];
+  }
+}
+
+extern "C" int capmi_conv_weight_pack_dgrad_s2(const float* w, int Cout, int Cin, int ph, int pw, float* out,
+                                               void* stream) {
+  CAPMI_REQUIRE(w && out && Cout > 0 && Cin > 0 && (ph == 0 || ph == 1) && (pw == 0 || pw == 1), CAPMI_EINVAL);
+  const long long n = (long long)Cout * Cin * (ph + 1) * (pw + 1);
+  hipLaunchKernelGGL(conv_weight_pack_dgrad_s2_kernel, dim3(std::min<long long>(cdiv(n, 256), 8192)), dim3(256),
+                     0, as_stream(stream), w, Cout, Cin, ph, pw, out);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
 // out[co][ci][kh][kw] (= nn.Conv2d weight layout) from the GEMM layout g[co][kh][kw][ci]
 __global__ void conv_weight_unpack_kernel(const float* __restrict__ g, int Cout, int Cin, int KH, int KW,
                                           float* __restrict__ out) {

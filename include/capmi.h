@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 8
+#define CAPMI_ABI_VERSION 9
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -192,12 +192,18 @@ int capmi_adaptive_avgpool_nhwc(const float* in, int N, int H, int W, int C, int
 
 /* ------------------------------------------------------------------------
  * Encoder fine-tune backward (EncoderAttention.fine_tune, models/encoder.py:112-121: layer2-4
- * trainable; BASELINE config 4). Conv dgrad = capmi_gemm_sk over CAPMI_A_CONV_NHWC of dY (zero-
- * upsampled first for stride 2) with the weights from capmi_conv_weight_pack_dgrad; conv wgrad =
+ * trainable; BASELINE config 4). Conv dgrad = capmi_gemm_sk over CAPMI_A_CONV_NHWC of dY with the
+ * weights from capmi_conv_weight_pack_dgrad (stride 2: four parity-class GEMMs with the weights from
+ * capmi_conv_weight_pack_dgrad_s2; capmi_zero_upsample2_nhwc is the older 4x-FLOP form); conv wgrad =
  * capmi_gemm_sk(CAPMI_A_MMAJOR, CAPMI_B_CONV_NHWC).
  * ---------------------------------------------------------------------------------------- */
 /* out[ci][kh][kw][co] = w[co][ci][KH-1-kh][KW-1-kw] (B operand of the data-gradient conv) */
 int capmi_conv_weight_pack_dgrad(const float* w, int Cout, int Cin, int KH, int KW, float* out, void* stream);
+/* 3x3 / stride 2 / pad 1 conv, parity class (ph, pw) of the input grid: out[ci][th][tw][co] =
+ * w[co][ci][kh][kw], kh = 1 (ph = 0) or 2 - 2*th (ph = 1, th in {0,1}), same for kw. The class's
+ * data gradient is a (ph+1)x(pw+1) stride-1 pad-0 conv over dY written to rows (2i+ph, 2j+pw)
+ * (sub-pixel form: 9 taps in total over the 4 classes instead of 36 on the zero-upsampled grid). */
+int capmi_conv_weight_pack_dgrad_s2(const float* w, int Cout, int Cin, int ph, int pw, float* out, void* stream);
 /* [Cout][KH][KW][Cin] (GEMM layout of a weight gradient) -> [Cout][Cin][KH][KW] (nn.Conv2d layout) */
 int capmi_conv_weight_unpack(const float* packed, int Cout, int Cin, int KH, int KW, float* out, void* stream);
 /* out (N,H,W,C) = dy (N,Ho,Wo,C) at even (h, w), zero elsewhere (stride-2 conv data gradient) */
