@@ -618,8 +618,7 @@ class FineTuneRunner:
             c1 = blk.conv1
             if G(c1.weight) is not None:
                 run(tag + ".conv1.wgrad", 2.0 * r1 * wd * Cin,
-                    K.problem(wd, Cin, r1, da1, wd, b["x"], Cin, G(c1.weight), Cin), AMM, BKR,
-                    K.TILE_64)  # 5-7 % faster than the auto 128x64 on layer2-4 (tools/bwd_gemm_ab.py)
+                    K.problem(wd, Cin, r1, da1, wd, b["x"], Cin, G(c1.weight), Cin), AMM, BKR)
             if need_dx:
                 K.conv_weight_pack_dgrad(c1.weight.detach(), wt[:wd * Cin])
                 run(tag + ".conv1.dgrad", 2.0 * r1 * wd * Cin,

@@ -563,11 +563,12 @@ int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, bo
   // output tile, stream-K over 128x64 tiles is the fastest form; below that the per-segment
   // pipeline fill outweighs the balance gain and 64x64 data-parallel wins
   if (automatic) tile = nkt >= 16 ? CAPMI_TILE_128x64 : CAPMI_TILE_64;
-  // conv weight gradients (k = output pixels, always >= 16 k-tiles; tools/wgrad_tile_ab.py):
-  // 128x128 for the wide 3x3 ones (Cout >= 256, N = 9*Cin >= 2048: layer3/4, 7-12 % faster than
-  // 128x64), 64x64 for the rest (layer2 3x3 and the 1x1 ones: 1-7 %)
+  // conv weight gradients (k = output pixels, always >= 16 k-tiles; tools/wgrad_tile_ab.py, with
+  // the k-major LDS images): 128x128 for the wide 3x3 ones (Cout >= 256, N = 9*Cin >= 2048:
+  // layer3/4, 1-7 % faster than 128x64), 128x64 for the rest (layer2 3x3 and the 1x1 ones: 128x128
+  // is up to 2x slower there, 64x64 5-12 % slower)
   if (automatic && amode == CAPMI_A_MMAJOR && bmode == CAPMI_B_CONV_NHWC)
-    tile = (prob->M >= 256 && prob->N >= 2048) ? CAPMI_TILE_128 : CAPMI_TILE_64;
+    tile = (prob->M >= 256 && prob->N >= 2048) ? CAPMI_TILE_128 : CAPMI_TILE_128x64;
   int rc = gemm_plan(prob, 1, amode, bmode, tile, g);
   if (rc) return rc;
   // the 512-thread 128x128 form (tools/w8_ab.sh over all 19 encoder conv shapes, batch 64):

@@ -39,18 +39,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t slot_rsrc(float* base, long lo
   return __builtin_amdgcn_make_buffer_rsrc(p, 0, 256 * 1024, 0x00020000);
 }
 
-// transposed staging: v = 4 consecutive m (or n) at one k -> rows d, d+S2, d+2S2, d+3S2 of
-// the [m][k] LDS image; store j writes component (j + r) & 3, r = (tid & 15) >> 2
-__device__ __forceinline__ void store_t4(float* d, const float4 v, int tid) {
-  const int r = (tid & 15) >> 2;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int c = (j + r) & 3;
-    const float x = c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
-    d[c * S2] = x;
-  }
-}
-
 // q = a / b for 0 <= a < 2^24, b > 0, from a float reciprocal plus one correction step
 __device__ __forceinline__ int fdivq(int a, int b, float inv_b) {
   int q = (int)((float)a * inv_b);
@@ -95,6 +83,11 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
   static_assert(NA >= 1 && NB >= 1, "tile");
   __shared__ __attribute__((aligned(16))) float As[2][BM * S2];
   __shared__ __attribute__((aligned(16))) float Bs[2][BN * S2];
+  // row strides of the k-major images of transposed operands (AMODE 1 / BMODE >= 1): BK2 rows of
+  // BM (BN) + 8 floats fit the [m][k] image's BM * S2 for BM >= 64; the +8 puts the two half-waves'
+  // rows (4 apart) on disjoint bank halves
+  constexpr int SMA = BM + 8, SMB = BN + 8;
+  static_assert(BK2 * SMA <= BM * S2 && BK2 * SMB <= BN * S2, "k-major LDS image");
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
@@ -125,9 +118,10 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
     // staging slots. Row-major operands (k contiguous): float4 f -> (row f>>3, k 4*(f&7)).
     // Transposed operands (AMODE 1 / BMODE 1: stored as k rows, m/n contiguous): slot i of
     // thread tid holds the float4 at column group jq = tid%16 + 16*(i % (Q/16)) of k-row
-    // tid/16 + 16*(i / (Q/16)) (16 lanes read 256 contiguous bytes of a k-row), and writes it
-    // to the same [m][k] LDS image by four scalar stores whose order is rotated by
-    // (tid%16)>>2, which makes every one of them bank-conflict-free (64 distinct banks).
+    // tid/16 + 16*(i / (Q/16)) (16 lanes read 256 contiguous bytes of a k-row) and stores it
+    // whole into a k-major LDS image [k][m]; the MFMA loop reads it back as four ds_read_b32
+    // per four k. (Transposing at the store into the [m][k] image, four rotated scalar stores
+    // per float4, was 20-25 % slower on the weight gradients: tools/wgrad_tile_ab.py.)
     constexpr int AQ = BM / 4, BQ = BN / 4;  // float4s per k-row of a transposed tile
     constexpr int AQ16 = AQ / 16, BQ16 = BQ / 16;
     long long a_base[NA];  // dense: row offset; conv: image base offset; transposed: column
@@ -325,7 +319,8 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
         if (!((st.am >> i) & 1u)) v = f4(0.f);
         const int f = tid + i * NT;
         if (AMODE == 1) {
-          store_t4(&As[buf][(i % AQ16 * 16 + (tid & 15)) * 4 * S2 + (tid >> 4) + 16 * (i / AQ16)], v, tid);
+          // k-major LDS image [k][m] (row stride SMA): the float4 along m lands whole
+          *reinterpret_cast<float4*>(&As[buf][((tid >> 4) + 16 * (i / AQ16)) * SMA + (i % AQ16 * 16 + (tid & 15)) * 4]) = v;
         } else {
           *reinterpret_cast<float4*>(&As[buf][(f >> 3) * S2 + kq]) = v;
         }
@@ -337,7 +332,7 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
         if (!((st.bm >> i) & 1u)) v = f4(0.f);
         const int f = tid + i * NT;
         if (BMODE >= 1) {
-          store_t4(&Bs[buf][(i % BQ16 * 16 + (tid & 15)) * 4 * S2 + (tid >> 4) + 16 * (i / BQ16)], v, tid);
+          *reinterpret_cast<float4*>(&Bs[buf][((tid >> 4) + 16 * (i / BQ16)) * SMB + (i % BQ16 * 16 + (tid & 15)) * 4]) = v;
         } else {
           *reinterpret_cast<float4*>(&Bs[buf][(f >> 3) * S2 + kq]) = v;
         }
@@ -362,15 +357,31 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
         }
         return;
       }
-      const float* Ab = As[buf] + (wm0 + lr) * S2 + 4 * lh;
-      const float* Bb = Bs[buf] + (wn0 + lr) * S2 + 4 * lh;
+      // [m][k] images: lane (lr, lh) reads k = 8g + 4lh .. +3 of its row in one ds_read_b128;
+      // k-major images ([k][m], transposed operands): the same four k as four ds_read_b32
+      const float* Ab = AMODE == 1 ? As[buf] + 4 * lh * SMA + wm0 + lr : As[buf] + (wm0 + lr) * S2 + 4 * lh;
+      const float* Bb = BMODE >= 1 ? Bs[buf] + 4 * lh * SMB + wn0 + lr : Bs[buf] + (wn0 + lr) * S2 + 4 * lh;
 #pragma unroll
       for (int g = 0; g < BK2 / 8; ++g) {
         float4 a[TM], b[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const float4*>(Ab + 32 * i * S2 + 8 * g);
+        for (int i = 0; i < TM; ++i) {
+          if (AMODE == 1) {
+            const float* q = Ab + 8 * g * SMA + 32 * i;
+            a[i] = make_float4(q[0], q[SMA], q[2 * SMA], q[3 * SMA]);
+          } else {
+            a[i] = *reinterpret_cast<const float4*>(Ab + 32 * i * S2 + 8 * g);
+          }
+        }
 #pragma unroll
-        for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const float4*>(Bb + 32 * j * S2 + 8 * g);
+        for (int j = 0; j < TN; ++j) {
+          if (BMODE >= 1) {
+            const float* q = Bb + 8 * g * SMB + 32 * j;
+            b[j] = make_float4(q[0], q[SMB], q[2 * SMB], q[3 * SMB]);
+          } else {
+            b[j] = *reinterpret_cast<const float4*>(Bb + 32 * j * S2 + 8 * g);
+          }
+        }
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
