@@ -94,10 +94,16 @@ class ConvTimer:
         return per
 
 
-def _traffic(kernel):
-    """HBM bytes per launch of ``kernel`` from the committed PMC summary (2*FETCH_SIZE +
-    WRITE_SIZE, gfx950 correction; tools/pmc_traffic.py), or None."""
-    path = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+def _traffic_file(config):
+    """The committed PMC summary of ``config``'s own run (a kernel name can stand for different
+    shapes in different configs, so each config reads only its own passes)."""
+    return "r01_pmc_traffic.json" if config == "attention" else f"r01_pmc_traffic_{config}.json"
+
+
+def _traffic(kernel, config="attention"):
+    """HBM bytes per launch of ``kernel`` from the committed PMC summary of this config's run
+    (2*FETCH_SIZE + WRITE_SIZE, gfx950 correction; tools/pmc_traffic.py), or None."""
+    path = os.path.join(REPO, "profiles", _traffic_file(config))
     try:
         with open(path) as f:
             tab = json.load(f)
@@ -291,11 +297,11 @@ def main():
         per_img = sum(v[1] for v in per.values()) / args.steps / B
         peak = BF16_MFMA_PEAK_TF if encoder._runner.bf16 else FP32_MFMA_PEAK_TF
         roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(ach / peak, 4), "traffic": _traffic(key),
+                "frac": round(ach / peak, 4), "traffic": _traffic(key, args.config),
                 "kernel": key,
                 "launches_per_step": n // args.steps,
                 "flops_per_launch": round(flops / n), "avg_launch_us": round(ms * 1e3 / n, 2),
-                "traffic_unit": "HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, profiles/r01_pmc_traffic.json)",
+                "traffic_unit": f"HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, profiles/{_traffic_file(args.config)})",
                 "conv_family": {"achieved_tflops": round(fam_flops / (fam_ms * 1e-3) / 1e12, 3),
                                 "frac": round(fam_flops / (fam_ms * 1e-3) / 1e12 / peak, 4),
                                 "conv_ms_per_step": round(fam_ms / args.steps, 3),

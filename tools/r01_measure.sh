@@ -20,4 +20,9 @@ c) tools/gpu_steps.sh \
 d) tools/gpu_steps.sh \
   "300|pmcfb|$P --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch_bert -o pmc -- python $R/bench.py --config bert_attention --steps 2 --warmup 1 --no-cpu-baseline --no-roofline" \
   "300|pmcwb|$P --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write_bert -o pmc -- python $R/bench.py --config bert_attention --steps 2 --warmup 1 --no-cpu-baseline --no-roofline" ;;
+e) tools/gpu_steps.sh \
+  "300|pmcfb|$P --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch_bert -o pmc -- python $R/bench.py --config bert_attention --steps 2 --warmup 1 --no-cpu-baseline --no-roofline" \
+  "300|pmcwb|$P --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write_bert -o pmc -- python $R/bench.py --config bert_attention --steps 2 --warmup 1 --no-cpu-baseline --no-roofline" \
+  "300|pmcff|$P --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch_ft -o pmc -- python $R/bench.py --config glove_finetune --steps 2 --warmup 1 --no-cpu-baseline --no-roofline" \
+  "300|pmcwf|$P --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write_ft -o pmc -- python $R/bench.py --config glove_finetune --steps 2 --warmup 1 --no-cpu-baseline --no-roofline" ;;
 esac
