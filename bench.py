@@ -1,6 +1,11 @@
 """Headline benchmark: 'attention' captioner training images/sec on MI355X.
 
-python bench.py --gpus N --steps K --warmup W     (N > 1: launched by torchrun, one rank per GPU)
+python bench.py --gpus N --steps K --warmup W
+
+N > 1: one rank per GPU over RCCL. Under torchrun (WORLD_SIZE set) the ranks are the launcher's;
+without it, this process starts ``python -m torch.distributed.run --nproc-per-node N`` on itself
+as a CHILD process before anything touches the GPU, waits for it and exits with its code (it
+never exec()s). Every rank checks that the world size equals --gpus.
 
 One step = the reference's training step (models/attention.py:386-430) on a resident
 synthetic batch of 64 (image 3x224x224, 25-token caption, V = 8100) per GPU: ResNet-101
@@ -18,9 +23,16 @@ graph instead.
 Rank 0 prints ONE JSON line. ``roofline`` is for the dominant kernel: the conv implicit-GEMM
 instantiation with the most time per step (the conv family is 86% of the step's FLOPs; the
 family aggregate is reported beside it). achieved = that kernel's algorithmic conv FLOPs /
-its summed launch time, HIP events on the launch stream around every conv launch.
-``cpu_baseline`` times the CPU oracle (op-for-op restatement of the reference step) on
-the host cores, rank 0 at N = 1 only, on a small bounded sample.
+its summed launch time. The launch times come from a graph-node timing pass right after the
+timed region: the same step (same launch mode, same graphs structure) is captured again with
+timing events recorded as graph nodes (hipEventRecordWithFlags(External)) around every conv
+launch, on the launch stream, and --steps calls are replayed and read back one by one.
+``cpu_baseline`` times the CPU oracle (op-for-op restatement of the reference step) on the
+host cores, rank 0 at N = 1 only: the full batch (64 images) for at least one step.
+
+``--config baseline_cpu`` is BASELINE config 1 (the 'baseline' LSTM captioner at batch 4 on
+the CPU, the reference's plumbing config): torch CPU modules, gloo for N > 1 (the CPU tests
+drive the multi-rank launch through it).
 """
 import argparse
 import json
@@ -45,9 +57,10 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 64; baseline_cpu: 4)")
+    ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--caption-len", type=int, default=25)
     ap.add_argument("--vocab", type=int, default=8100)
     ap.add_argument("--no-roofline", action="store_true", help="skip per-conv event timing")
@@ -55,24 +68,76 @@ def parse():
                     help="no encoder/decoder pipelining: the whole step in one HIP graph (or --eager)")
     ap.add_argument("--eager", action="store_true",
                     help="with --sequential: launch every kernel from Python (no HIP graph)")
-    ap.add_argument("--config", default="attention", choices=["attention", "glove_finetune", "bert_attention"],
+    ap.add_argument("--config", default="attention",
+                    choices=["attention", "glove_finetune", "bert_attention", "baseline_cpu"],
                     help="attention = BASELINE config 2/3 (frozen encoder, the headline); glove_finetune = "
                          "config 4 (GloVe-300 fp64 embedding fine-tuned + encoder layer2-4 fine-tuned); "
-                         "bert_attention = config 5 (768-d word features instead of the table, synthetic)")
+                         "bert_attention = config 5 (768-d word features instead of the table, synthetic); "
+                         "baseline_cpu = config 1 (baseline LSTM captioner, batch 4, CPU, gloo)")
     ap.add_argument("--fp32", action="store_true", help="bert_attention: keep the encoder convs fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    return ap.parse_args()
+    ap.add_argument("--cpu-seconds", type=float, default=20.0,
+                    help="cpu_baseline: keep stepping the oracle at the full batch until this much time "
+                         "has passed (at least one step)")
+    ap.add_argument("--master-port", type=int, default=0, help="N > 1 self-launch: rendezvous port (0: free)")
+    args = ap.parse_args()
+    if args.batch is None:
+        args.batch = 4 if args.config == "baseline_cpu" else 64
+    return args
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """--gpus N > 1 outside torchrun: run torch.distributed.run on this script as a child process
+    (nothing has touched the GPU yet in this process) and return its exit code."""
+    import subprocess
+    port = args.master_port or _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL between processes)
+    return subprocess.call(cmd, env=env)
 
 
 class ConvTimer:
-    """HIP-event bracket around every conv GEMM launch (on the launch stream), per kernel."""
+    """Times every conv GEMM launch with HIP events on the launch stream, per kernel.
+
+    Eager launches (``enabled``): an event pair around the launch. Inside a graph capture:
+    the pair is recorded as graph nodes (external events), filed under the label of the graph
+    being captured (``on_capture``); after each replay ``harvest(labels)`` reads the pairs of
+    the graphs that ran (the caller synchronizes first)."""
 
     def __init__(self):
-        self.events = []  # (kernel key, flops, start event, end event)
+        self.events = []  # eager: (kernel key, flops, start event, end event)
         self.enabled = False
+        self.graph = {}   # capture label -> [(key, flops, s, e)]
+        self.label = None
+        self.acc = {}     # key -> [launches, flops, ms] (harvested graph replays)
+
+    def on_capture(self, label):
+        self.label = label
+        self.graph[label] = []
 
     def __call__(self, tag, flops, launch, key):
+        if torch.cuda.is_current_stream_capturing():
+            if self.label is None:
+                launch()
+                return
+            s = torch.cuda.Event(enable_timing=True, external=True)
+            e = torch.cuda.Event(enable_timing=True, external=True)
+            s.record()
+            launch()
+            e.record()
+            self.graph[self.label].append((key, flops, s, e))
+            return
         if not self.enabled:
             launch()
             return
@@ -83,9 +148,17 @@ class ConvTimer:
         e.record()
         self.events.append((key, flops, s, e))
 
+    def harvest(self, labels):
+        for lab in labels:
+            for key, f, s, e in self.graph.get(lab, ()):
+                ent = self.acc.setdefault(key, [0, 0.0, 0.0])
+                ent[0] += 1
+                ent[1] += f
+                ent[2] += s.elapsed_time(e)
+
     def result(self):
-        """{kernel key: [launches, flops, ms]} and the family total."""
-        per = {}
+        """{kernel key: [launches, flops, ms]}."""
+        per = {k: list(v) for k, v in self.acc.items()}
         for key, f, s, e in self.events:
             ent = per.setdefault(key, [0, 0.0, 0.0])
             ent[0] += 1
@@ -113,81 +186,194 @@ def _traffic(kernel, config="attention"):
     return None if ent is None else ent.get("hbm_bytes_per_launch")
 
 
+def _host_threads():
+    """Threads for the CPU baseline: the box's CPU share for this process (OMP_NUM_THREADS is set
+    to it on the GPU boxes), else the CPUs this process may run on."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _oracle_loop(step_fn, B, seconds, desc, threads):
+    """Full-batch oracle steps until ``seconds`` have passed (at least one; no warm-up step: a
+    batch-64 step is seconds long, its first-call overheads are noise)."""
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step_fn()
+        n += 1
+        if time.perf_counter() - t0 > seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(B * n / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "sample": f"{n} oracle train step(s) at B={B} ({desc}), torch CPU fp32, {threads} threads, {dt:.1f} s"}
+
+
 def cpu_baseline(args, seconds):
-    """Oracle (CPU restatement of the reference step) on a bounded sample: B=2, full
-    ResNet-101 encoder forward + the unhoisted 24-step decoder fwd/bwd + clamp + Adam."""
+    """Oracle (CPU restatement of the reference step) at the full batch: ResNet-101 encoder
+    forward (train-mode BN) + the unhoisted 24-step decoder fwd/bwd + clamp + Adam."""
     sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
     import gen
     from oracle import decoder_ref as R
     from oracle.resnet_ref import build_resnet101, encoder_attention_forward
-    threads = min(16, os.cpu_count() or 1)
+    threads = _host_threads()
     torch.set_num_threads(threads)
-    B, L, V = 2, args.caption_len, args.vocab
+    B, L, V = args.batch, args.caption_len, args.vocab
     bert = args.config == "bert_attention"
     M = 768 if bert else 512
     net = build_resnet101(gen.resnet101_params(5)).train()
     p = {k: torch.from_numpy(v) for k, v in gen.decoder_params(5, 512, 512, M, V).items()}
     trainable = set(k for k in p if k != "embedding.weight")
-    imgs = torch.from_numpy(gen.images(5, B))
+    imgs = torch.from_numpy(gen.images(5, B, args.image_size, args.image_size))
     caps = torch.from_numpy(gen.captions(5, B, L, V))
     emb = None
     if bert:
         from capmi.data import SyntheticBertEmbedder
         emb = SyntheticBertEmbedder(V, 768)(caps)
-    state, n, t0 = {}, 0, None
-    while True:
+    state = {}
+
+    def one():
+        nonlocal state
         with torch.no_grad():
             feats = encoder_attention_forward(net, imgs)
         out = R.train_step(p, trainable, feats, caps, [L] * B, state=state, embeddings=emb)
         p.update(out[5])
         state = out[6]
-        n += 1
-        if t0 is None:          # first step is warm-up
-            t0, n = time.perf_counter(), 0
-        elif time.perf_counter() - t0 > seconds:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(B * n / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} oracle train steps at B={B} (ResNet-101 fwd + unhoisted decoder fwd/bwd + "
-                      f"clamp/Adam, L={L}, V={V}, M={M}), torch CPU fp32, {threads} threads, {dt:.1f} s"}
+
+    return _oracle_loop(one, B, seconds, f"ResNet-101 fwd + unhoisted decoder fwd/bwd + clamp/Adam, L={L}, "
+                                         f"V={V}, M={M}", threads)
 
 
 def cpu_baseline_finetune(args, seconds):
     """Oracle fine-tune step (oracle/finetune_ref.py: ResNet-101 fwd+bwd of layer2-4, decoder
-    fwd/bwd with fp64 GloVe-300 embedding, clamp + two Adams) at B=2 on the host cores."""
+    fwd/bwd with fp64 GloVe-300 embedding, clamp + two Adams) at the full batch."""
     sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
     import gen
     from oracle.finetune_ref import finetune_train_step
-    threads = min(16, os.cpu_count() or 1)
+    threads = _host_threads()
     torch.set_num_threads(threads)
-    B, L, V = 2, args.caption_len, args.vocab
+    B, L, V = args.batch, args.caption_len, args.vocab
     rp = gen.resnet101_params(5)
     p = {k: torch.from_numpy(v) for k, v in gen.decoder_params(5, 512, 512, 300, V, emb_dtype=np.float64).items()}
-    imgs = torch.from_numpy(gen.images(5, B))
+    imgs = torch.from_numpy(gen.images(5, B, args.image_size, args.image_size))
     caps = torch.from_numpy(gen.captions(5, B, L, V))
-    n, t0 = 0, None
-    while True:
-        finetune_train_step(rp, p, set(p), imgs, caps, [L] * B)
-        n += 1
-        if t0 is None:
-            t0, n = time.perf_counter(), 0
-        elif time.perf_counter() - t0 > seconds:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(B * n / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} oracle fine-tune train steps at B={B} (ResNet-101 fwd + layer2-4 bwd, unhoisted "
-                      f"decoder fwd/bwd, fp64 GloVe-300 embedding, clamp/2x Adam, L={L}, V={V}), torch CPU fp32, "
-                      f"{threads} threads, {dt:.1f} s"}
+    return _oracle_loop(lambda: finetune_train_step(rp, p, set(p), imgs, caps, [L] * B), B, seconds,
+                        f"ResNet-101 fwd + layer2-4 bwd, unhoisted decoder fwd/bwd, fp64 GloVe-300 embedding, "
+                        f"clamp/2x Adam, L={L}, V={V}", threads)
+
+
+def run_baseline_cpu(args, ctx):
+    """BASELINE config 1: the 'baseline' captioner (models/baseline.py: ResNet-101 + Linear encoder,
+    nn.LSTM decoder) trained on the CPU at batch 4, as the reference's train loop does
+    (models/baseline.py:114-264: CE ignore_index=PAD, backward, clamp, Adam); N > 1 ranks average
+    the gradients over gloo. Returns (seconds for the timed steps, last loss)."""
+    from capmi import dist as cdist
+    from models.baseline import BaselineDecoder, BaselineDecoderParams
+    from models.encoder import Encoder
+    from train_utils import clip_gradient
+    torch.set_num_threads(max(1, _host_threads() // ctx.world))
+    torch.manual_seed(0)
+    enc = Encoder(512).train()
+    prm = BaselineDecoderParams()
+    prm.vocab_size = args.vocab
+    dec = BaselineDecoder(prm).train()
+    dec.fine_tune_embeddings(False)  # --fine_tune_embedding default (train.py:41-42)
+    cdist.broadcast_module(enc, ctx)
+    cdist.broadcast_module(dec, ctx)
+    params = [q for q in dec.parameters() if q.requires_grad]
+    opt = torch.optim.Adam(params, lr=1e-4)
+    crit = torch.nn.CrossEntropyLoss(ignore_index=0)
+    from capmi.data import synthetic_batch
+    imgs, caps, _ = synthetic_batch(args.batch, args.caption_len, args.vocab, "cpu", seed=1234 + ctx.rank,
+                                    H=args.image_size, W=args.image_size)
+
+    def one():
+        with torch.no_grad():
+            feats = enc(imgs)  # frozen ResNet (the reference's baseline trains only the decoder by default)
+        scores = dec(feats, caps)
+        loss = crit(scores.reshape(-1, scores.shape[2]), caps.reshape(-1))
+        opt.zero_grad()
+        loss.backward()
+        if ctx.distributed:
+            flat = torch.cat([q.grad.reshape(-1) for q in params])
+            cdist.allreduce_mean_([flat], ctx)
+            o = 0
+            for q in params:
+                q.grad.copy_(flat[o:o + q.numel()].view_as(q))
+                o += q.numel()
+        clip_gradient(opt, 5.0)
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        one()
+    cdist.barrier(ctx)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = one()
+    cdist.barrier(ctx)
+    return time.perf_counter() - t0, float(loss.detach())
+
+
+def graph_timing_pass(args, make_step, imgs, caps, lens, timer, encoder):
+    """Re-capture the benchmarked step with timing events as graph nodes around every conv launch
+    (ConvTimer) and replay it ``args.steps`` times, reading the events back after each call: the
+    conv kernels' durations inside graph replays of the timed step's structure. Returns a
+    description, or raises when the runtime refuses event nodes."""
+    step2 = make_step(seed_off=99)
+    step2.capture_hook = timer.on_capture
+    encoder._runner.conv_hook = timer
+    pipe = step2.pipeline
+    step2(imgs, caps, lens)          # captures (events as nodes) + first replay
+    if not pipe:
+        step2.flush()
+    torch.cuda.synchronize()
+    for _ in range(args.steps):
+        step2(imgs, caps, lens)
+        torch.cuda.synchronize()
+        timer.harvest(step2.replayed)
+    step2.flush()
+    torch.cuda.synchronize()
+    encoder._runner.conv_hook = None
+    return (f"HIP events recorded as graph nodes around each conv launch on its stream, {args.steps} replays of "
+            "a re-capture of the timed step (" + ("pipelined: the decoder graph of the previous batch replaying "
+                                                  "beside the encoder graph, as in the timed region)" if pipe else
+                                                  "one graph per step, as in the timed region)"))
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     from capmi import dist as cdist
-    ctx = cdist.init_from_env("cuda")
+    cpu_cfg = args.config == "baseline_cpu"
+    ctx = cdist.init_from_env("cpu" if cpu_cfg else "cuda", backend="gloo" if cpu_cfg else None)
+    if ctx.world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started {ctx.world} rank(s)")
+    if cpu_cfg:
+        return main_baseline_cpu(args, ctx)
+    if ctx.device.type != "cuda":
+        raise SystemExit("bench: no HIP device (the GPU configs need an MI355X; --config baseline_cpu runs on CPU)")
     dev = ctx.device
     from capmi.data import synthetic_batch
     from capmi.optim import Adam
     from capmi.train_step import AttentionTrainStep
+    from capmi import kernels as K
     from models.attention import AttentionDecoder, AttentionDecoderParams
     from models.encoder import EncoderAttention
     from vocabulary import synthetic_vocab
@@ -213,22 +399,27 @@ def main():
     decoder = decoder.to(dev).train()
     # glove_att: --fine_tune_embedding True (Makefile:13); bert: the table is unused; else Q8 default
     decoder.fine_tune_embeddings(ft)
+    cdist.broadcast_module(encoder, ctx)
     cdist.broadcast_module(decoder, ctx)
     opt = Adam(filter(lambda q: q.requires_grad, decoder.parameters()), lr=1e-4)
     opt.set_clip(5.0)
     enc_opt = None
     if ft:
         encoder.fine_tune(True)
-        cdist.broadcast_module(encoder, ctx)
         enc_opt = Adam(filter(lambda q: q.requires_grad, encoder.parameters()), lr=1e-4)
         enc_opt.set_clip(5.0)
     pipe = not args.sequential and not ft
-    step = AttentionTrainStep(encoder, decoder, opt, ctx, alpha_c=1.0, graph=not args.eager,
-                              seed=77 + ctx.rank, pipeline=pipe, encoder_optimizer=enc_opt)
+
+    def make_step(seed_off=0):
+        return AttentionTrainStep(encoder, decoder, opt, ctx, alpha_c=1.0, graph=not args.eager,
+                                  seed=77 + seed_off + ctx.rank, pipeline=pipe, encoder_optimizer=enc_opt)
+
+    step = make_step()
     timer = ConvTimer()
-    encoder._runner.conv_hook = None if args.no_roofline else timer
+    encoder._runner.conv_hook = None if args.no_roofline or not args.eager else timer
     B = args.batch
-    imgs, caps, lens = synthetic_batch(B, args.caption_len, args.vocab, dev, seed=1234 + ctx.rank)
+    imgs, caps, lens = synthetic_batch(B, args.caption_len, args.vocab, dev, seed=1234 + ctx.rank,
+                                       H=args.image_size, W=args.image_size)
 
     for _ in range(args.warmup):
         step(imgs, caps, lens)
@@ -246,48 +437,28 @@ def main():
     torch.cuda.synchronize()
     cdist.barrier(ctx)
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    dt_rank = time.perf_counter() - t0
     timer.enabled = False
-    dt = cdist.max_over_ranks(dt, ctx)
+    rank_dts = cdist.gather_floats(dt_rank, ctx)
+    dt = max(rank_dts)
     if pipe:  # K encoder and K decoder passes were timed; drain the in-flight encoder pass
         step.flush()
         torch.cuda.synchronize()
     loss_v = float(loss.item())
-    if pipe and not args.eager and not args.no_roofline:
-        # graph replays cannot bracket single kernels: time the conv launches of `steps` more
-        # pipelined steps launched eagerly (the encoder sharing the GPU with the decoder as in
-        # the timed region), right after it
-        step2 = AttentionTrainStep(encoder, decoder, opt, ctx, alpha_c=1.0, graph=False, seed=99 + ctx.rank,
-                                   pipeline=True)
-        step2(imgs, caps, lens)
-        torch.cuda.synchronize()
-        timer.enabled = True
-        for _ in range(args.steps):
-            step2(imgs, caps, lens)
-        torch.cuda.synchronize()
-        timer.enabled = False
-        step2.flush()
-        torch.cuda.synchronize()
-    elif not (args.eager or pipe) and not args.no_roofline:
-        # graph replays cannot bracket single kernels: time the same conv launches (same shapes,
-        # same inputs) in eager encoder forwards right after the timed region
-        timer.enabled = True
-        with torch.no_grad():
-            for _ in range(args.steps):
-                if ft:  # fine-tune: the forward and the layer2-4 backward GEMMs
-                    f = encoder.ft_forward(imgs)
-                    encoder.ft_backward(torch.ones_like(f) * 1e-4, {id(q): q.grad for q in enc_opt.param_groups[0]["params"]},
-                                        hook=timer)
-                else:
-                    encoder(imgs)
-        torch.cuda.synchronize()
-        timer.enabled = False
+    K.sk_check()  # stream-K hand-off invariant over the timed run (raises if a hand-off timed out)
+    timing = None
+    if not args.no_roofline:
+        if args.eager:
+            timing = "HIP events around each conv launch on its stream, inside the timed (eager) steps"
+        else:
+            timing = graph_timing_pass(args, make_step, imgs, caps, lens, timer, encoder)
+            K.sk_check()
 
     N = ctx.world
     value = N * B * args.steps / dt
     roof = None
-    if not args.no_roofline and timer.events:
-        per = timer.result()
+    per = timer.result() if not args.no_roofline else {}
+    if per:
         # the dominant kernel: the conv GEMM instantiation with the most time
         key = max(per, key=lambda k: per[k][2])
         n, flops, ms = per[key]
@@ -306,13 +477,7 @@ def main():
                                 "frac": round(fam_flops / (fam_ms * 1e-3) / 1e12 / peak, 4),
                                 "conv_ms_per_step": round(fam_ms / args.steps, 3),
                                 "conv_gflop_per_image": round(per_img / 1e9, 3)},
-                "timing": "HIP events around each conv launch on its stream, " + (
-                    "inside the timed steps (pipelined, eager: while the decoder step shares the GPU)"
-                    if pipe and args.eager else
-                    f"{args.steps} eagerly launched pipelined steps after the timed graph replays (the decoder "
-                    "step sharing the GPU as in the timed region)" if pipe else
-                    "inside the timed steps" if args.eager else
-                    f"{args.steps} eager encoder forwards after the timed graph replays")}
+                "timing": timing}
     cpu = None
     if ctx.rank == 0 and N == 1 and not args.no_cpu_baseline:
         cpu = (cpu_baseline_finetune if ft else cpu_baseline)(args, args.cpu_seconds)
@@ -332,10 +497,12 @@ def main():
                                     "forces fp32 at the LSTM input)" if encoder._runner.bf16 else "")) if bert else
                        ("'attention' decoder + frozen ResNet-101 encoder (BN train mode), "
                         "one training step per batch"),
-                       "per_gpu_batch": B, "global_batch": B * N,
+                       "per_gpu_batch": B, "global_batch": B * N, "image_size": args.image_size,
                        "caption_len": args.caption_len, "decode_steps": args.caption_len - 1,
                        "vocab": args.vocab, "attention_dim": 512, "decoder_dim": 512, "embed_size": prm.embed_size,
                        "parallelism": f"dp{N}"},
+            "dist": {"world_size": N, "backend": ctx.backend or "none",
+                     "rank_ms_per_step": [round(x / args.steps * 1e3, 3) for x in rank_dts]},
             "loss_last_step": round(loss_v, 5),
             "launch": ("pipelined_2stream_eager" if args.eager else "pipelined_2stream_hip_graphs") if pipe
             else ("eager" if args.eager else "hip_graph"),
@@ -343,6 +510,28 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+
+
+def main_baseline_cpu(args, ctx):
+    dt_rank, loss_v = run_baseline_cpu(args, ctx)
+    from capmi import dist as cdist
+    rank_dts = cdist.gather_floats(dt_rank, ctx)
+    dt = max(rank_dts)
+    N = ctx.world
+    if ctx.rank == 0:
+        print(json.dumps({
+            "metric": "training images/sec (whole node), 'baseline' decoder on CPU (BASELINE config 1)",
+            "value": round(N * args.batch * args.steps / dt, 3), "unit": "images/s", "n_gpus": 0,
+            "n_ranks": N, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic (random-init weights, torch.manual_seed(0))",
+            "config": {"workload": "'baseline' LSTM captioner (ResNet-101 + Linear encoder frozen, nn.LSTM "
+                                   "decoder), CPU, one training step per batch",
+                       "per_rank_batch": args.batch, "global_batch": args.batch * N, "image_size": args.image_size,
+                       "caption_len": args.caption_len, "vocab": args.vocab, "parallelism": f"dp{N} (gloo, CPU)"},
+            "dist": {"world_size": N, "backend": ctx.backend or "none",
+                     "rank_ms_per_step": [round(x / args.steps * 1e3, 3) for x in rank_dts]},
+            "loss_last_step": round(loss_v, 5), "roofline": None, "cpu_baseline": None}), flush=True)
 
 
 if __name__ == "__main__":

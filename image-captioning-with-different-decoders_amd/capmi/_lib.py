@@ -23,7 +23,7 @@ CAPMI_B_NMAJOR_W, CAPMI_B_KROWS, CAPMI_B_CONV_NHWC = 0, 1, 2
 CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO, CAPMI_TILE_128_W8 = 0, 1, 2, 3, 4
 CAPMI_MAX_GROUP = 4
 CAPMI_COLSUM_GROUPS = 64
-ABI_VERSION = 9
+ABI_VERSION = 10
 CAPMI_BNB_RELU_Y, CAPMI_BNB_RELU_OUT = 0, 1
 CAPMI_BNB_MAX_SLABS = 256
 CAPMI_GEMM_BF16 = 1
@@ -51,6 +51,7 @@ _SIGS = {
     "capmi_gemm": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_int, c_vp],
     "capmi_gemm_stat_tiles": [c_int, c_int],
     "capmi_gemm_workspace_bytes": [],
+    "capmi_gemm_workspace_flag_bytes": [],
     "capmi_gemm_sk": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_vp, c_ll, c_vp],
     "capmi_gemm_sk_ex": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_int, c_vp, c_ll, c_vp],
     "capmi_gemm_sk_plan": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp],
@@ -113,7 +114,8 @@ _SIGS = {
     "capmi_strerror": [c_int],
     "capmi_abi_version": [],
 }
-_RESTYPES = {"capmi_strerror": ctypes.c_char_p, "capmi_gemm_workspace_bytes": c_ll}
+_RESTYPES = {"capmi_strerror": ctypes.c_char_p, "capmi_gemm_workspace_bytes": c_ll,
+             "capmi_gemm_workspace_flag_bytes": c_ll}
 EXPORTS = tuple(_SIGS)
 
 

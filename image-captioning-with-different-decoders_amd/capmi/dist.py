@@ -88,6 +88,17 @@ def max_over_ranks(x, ctx):
     return float(t.item())
 
 
+def gather_floats(x, ctx):
+    """[x of rank 0, x of rank 1, ...] on every rank (bench: per-rank step times)."""
+    if not ctx.distributed:
+        return [float(x)]
+    dev = ctx.device if ctx.backend == "nccl" else "cpu"
+    t = torch.zeros(ctx.world, dtype=torch.float64, device=dev)
+    t[ctx.rank] = x
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(v) for v in t.tolist()]
+
+
 def barrier(ctx):
     if ctx.distributed:
         if ctx.backend == "nccl":

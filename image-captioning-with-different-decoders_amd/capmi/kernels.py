@@ -4,6 +4,7 @@ Shape/dtype/device validation happens here, before the call (include/capmi.h
 contract); every launch goes on ``torch.cuda.current_stream()``.
 """
 import ctypes
+import weakref
 
 import torch
 
@@ -68,10 +69,33 @@ def gemm_workspace_bytes():
     return int(lib.capmi_gemm_workspace_bytes())
 
 
+_WORKSPACES = weakref.WeakSet()
+
+
 def gemm_workspace(device):
     """Zeroed stream-K workspace for capmi_gemm_sk (one per stream that runs it)."""
     n = (gemm_workspace_bytes() + 3) // 4
-    return torch.zeros(n, device=device, dtype=torch.int32)
+    ws = torch.zeros(n, device=device, dtype=torch.int32)
+    _WORKSPACES.add(ws)
+    return ws
+
+
+def sk_check(workspaces=None):
+    """Host-side check of the stream-K hand-off invariant at a sync point: every flag word of a
+    workspace is zero between launches (include/capmi.h, capmi_gemm_workspace_flag_bytes). A
+    nonzero word means a hand-off timed out and a result is invalid: the flags are re-zeroed (so
+    later launches start clean) and RuntimeError is raised. Reads every live workspace by default
+    (one small device->host copy each); call it only where the host synchronises anyway."""
+    nflag = int(lib.capmi_gemm_workspace_flag_bytes()) // 4
+    bad = []
+    for ws in list(_WORKSPACES) if workspaces is None else workspaces:
+        f = ws[:nflag]
+        if bool(f.any()):
+            bad.append(int(f.count_nonzero()))
+            f.zero_()
+    if bad:
+        raise RuntimeError(f"capmi stream-K: hand-off timed out ({bad} nonzero flag words); results of the "
+                           "launches since the last check are invalid (flags re-zeroed)")
 
 
 def gemm_sk(prob, amode, workspace, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W, bf16=False):

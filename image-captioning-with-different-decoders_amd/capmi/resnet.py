@@ -511,6 +511,8 @@ class FineTuneRunner:
         if stt is None:
             raise RuntimeError("FineTuneRunner.backward without a saved forward")
         N, dev = stt["N"], stt["device"]
+        if hook is None:
+            hook = self.r.conv_hook  # bench timing of the backward GEMMs (None: plain launches)
         gp = self.grad.get
         blocks = stt["blocks"]
         big = max(b["H"] * b["W"] * max(b["Cin"], b["Cout"], b["wd"]) for b in blocks) * N

@@ -62,6 +62,10 @@ class AttentionTrainStep:
         self.seed_dev = torch.full((1,), s, dtype=torch.int64, device=dev)
         self._graph = None
         self._static = None
+        # optional callable(label) run before each graph capture (bench: graph-node timing), and
+        # the labels of the graphs the last call replayed ("enc0"/"dec1"..., or "step")
+        self.capture_hook = None
+        self.replayed = []
         # pipelined mode: the frozen encoder of batch k runs on its own stream while the decoder
         # step of batch k-1 runs (the encoder reads no decoder state); see _pipe_call
         self.pipeline = pipeline
@@ -84,6 +88,20 @@ class AttentionTrainStep:
 
     def _grads(self):
         return {n: self.params[n].grad for n in self.need}
+
+    def _snapshot(self):
+        """Device state a capture warm-up must not change: the encoder's BatchNorm buffers
+        (running mean/var, num_batches_tracked: train-mode forwards update them) and the dropout
+        seed counter. Restored after the warm-ups, so a graph replay sequence equals the eager one."""
+        return [(b, b.detach().clone()) for b in self.encoder.buffers()] + [(self.seed_dev, self.seed_dev.clone())]
+
+    @staticmethod
+    def _restore(snap):
+        torch.cuda.synchronize()
+        with torch.no_grad():
+            for b, v in snap:
+                b.copy_(v)
+        torch.cuda.synchronize()
 
     def _grad_buffers(self):
         bufs = list(self.opt.grad_buffers())
@@ -157,6 +175,7 @@ class AttentionTrainStep:
         Returns the loss of batch k-1 (None on the first call); flush() runs the last decoder.
         The returned loss lives on s_dec: synchronize before reading it."""
         cur = torch.cuda.current_stream()
+        self.replayed = []
         slot = self._slot
         self._slot ^= 1
         N, _, H, W = imgs.shape
@@ -170,8 +189,12 @@ class AttentionTrainStep:
             self.encoder.forward_into(imgs, self._feats[slot])
             ev_enc = torch.cuda.Event()
             ev_enc.record(self.s_enc)
+        # the caller's tensors are read on the side streams: keep their blocks from being handed
+        # to a later allocation on the caller's stream until those reads are done
+        imgs.record_stream(self.s_enc)
+        captions.record_stream(self.s_dec)
         loss = self._pipe_decoder()
-        self._pend = (slot, captions, caption_lengths, ev_enc)
+        self._pend = ("eager", slot, captions, caption_lengths, ev_enc)
         return loss
 
     # ------------------------------------------------------- pipelined graphs
@@ -183,6 +206,7 @@ class AttentionTrainStep:
         dev = imgs.device
         N = imgs.shape[0]
         upd = not self.ctx.distributed
+        snap = self._snapshot()
         self._feats = [torch.empty(N, 14, 14, 2048, device=dev, dtype=torch.float32) for _ in range(2)]
         pg = []
         for slot in range(2):
@@ -196,14 +220,19 @@ class AttentionTrainStep:
                 self.encoder.forward_into(pg[0]["imgs"], self._feats[0])
                 self._dec_body(self._feats[0], pg[0]["caps"], pg[0]["lens"], with_update=False)
         torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
+        self._restore(snap)
         for slot in range(2):
             st = pg[slot]
             g = torch.cuda.CUDAGraph()
+            if self.capture_hook is not None:
+                self.capture_hook(f"enc{slot}")
             with torch.cuda.graph(g):
                 self.encoder.forward_into(st["imgs"], self._feats[slot])
             st["g_enc"] = g
+            st["feats"] = self._feats[slot]  # the graphs hold raw pointers: keep the buffer alive
             g = torch.cuda.CUDAGraph()
+            if self.capture_hook is not None:
+                self.capture_hook(f"dec{slot}")
             with torch.cuda.graph(g):
                 st["loss"] = self._dec_body(self._feats[slot], st["caps"], st["lens"], with_update=upd)
             st["g_dec"] = g
@@ -227,26 +256,32 @@ class AttentionTrainStep:
         with torch.cuda.stream(self.s_enc):
             if imgs.data_ptr() != st["imgs"].data_ptr():
                 st["imgs"].copy_(imgs, non_blocking=True)
+                imgs.record_stream(self.s_enc)  # read on s_enc: see _pipe_call
             if captions.data_ptr() != st["caps"].data_ptr():
                 st["caps"].copy_(captions, non_blocking=True)
+                captions.record_stream(self.s_enc)
             st["g_enc"].replay()
             ev_enc = torch.cuda.Event()
             ev_enc.record(self.s_enc)
+        self.replayed = [f"enc{slot}"]
         loss = self._pipe_decoder()
-        self._pend = (slot, captions, caption_lengths, ev_enc)
+        self._pend = ("graph", slot, captions, caption_lengths, ev_enc)
         return loss
 
     def _pipe_decoder(self):
         if self._pend is None:
             return None
-        if self.pipe_graph:
-            pslot, _, _, ev = self._pend
+        # dispatch on how the pending batch's encoder was launched (a ragged batch runs eagerly
+        # between graph-replayed ones)
+        if self._pend[0] == "graph":
+            _, pslot, _, _, ev = self._pend
             self._pend = None
             self.s_dec.wait_event(ev)
             self.s_dec.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self.s_dec):
                 st = self._pg[pslot]
                 st["g_dec"].replay()
+                self.replayed.append(f"dec{pslot}")
                 if self.ctx.distributed:
                     cdist.allreduce_mean_(self.opt.grad_buffers(), self.ctx)
                     self.opt.step()
@@ -254,7 +289,7 @@ class AttentionTrainStep:
                 self._ev_dec = torch.cuda.Event()
                 self._ev_dec.record(self.s_dec)
             return loss
-        pslot, caps, lens, ev = self._pend
+        _, pslot, caps, lens, ev = self._pend
         self._pend = None
         self.s_dec.wait_event(ev)
         self.s_dec.wait_stream(torch.cuda.current_stream())
@@ -316,6 +351,7 @@ class AttentionTrainStep:
         if captions.data_ptr() != st["caps"].data_ptr():
             st["caps"].copy_(captions, non_blocking=True)
         self._graph.replay()
+        self.replayed = ["step"]
         if self.ctx.distributed:
             cdist.allreduce_mean_(self._grad_buffers(), self.ctx)
             self._step_all()
@@ -327,14 +363,19 @@ class AttentionTrainStep:
               "lens": list(caption_lengths)}
         # warm-up on a side stream: allocates every workspace outside the graph's pool. No
         # parameter update here (gradients are overwritten by the next step), so the first
-        # call still applies exactly one update; BN running stats do see the extra forwards.
+        # call still applies exactly one update; the BN running statistics and the dropout seed
+        # counter the warm-up forwards advance are restored afterwards (graph == eager).
+        snap = self._snapshot()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self._body(st["imgs"], st["caps"], st["lens"], with_update=False)
         torch.cuda.current_stream().wait_stream(s)
+        self._restore(snap)
         g = torch.cuda.CUDAGraph()
+        if self.capture_hook is not None:
+            self.capture_hook("step")
         with torch.cuda.graph(g):
             st["loss"] = self._body(st["imgs"], st["caps"], st["lens"], with_update=upd)
         self._graph, self._static = g, st

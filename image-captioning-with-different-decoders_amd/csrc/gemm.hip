@@ -530,6 +530,8 @@ extern "C" int capmi_gemm(const capmi_gemm_problem* probs, int nprob, int amode,
   return gemm_launch_dp(g, amode, bmode, as_stream(stream));
 }
 
+extern "C" long long capmi_gemm_workspace_flag_bytes(void) { return sk_flag_bytes(cu_count()); }
+
 extern "C" long long capmi_gemm_workspace_bytes(void) {
   const int cus = cu_count();
   // parked partials: (WGs per CU) * BM * BN floats per CU is 64 KB for 4 x 64x64 and for

@@ -287,8 +287,13 @@ gemm_bf16_kernel(const GemmArgs args) {
           while (__hip_atomic_load(flags + b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
                  ++spins < (1 << 22))
             __builtin_amdgcn_s_sleep(2);
-          if (spins >= (1 << 22)) flags[gridDim.x] = 1;  // never expected: report instead of hanging
-          __hip_atomic_store(flags + b2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // never expected: report instead of hanging. The flag of b2 is left as it is and the
+          // error word raised, so the host's check (capmi.kernels.sk_check: every flag word must
+          // be zero between launches) raises and re-zeroes the workspace instead of carrying on
+          if (spins >= (1 << 22))
+            __hip_atomic_store(flags + gridDim.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else
+            __hip_atomic_store(flags + b2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -13,6 +13,7 @@ import torch
 import torch.nn as nn
 
 from capmi import decoder_fn as DF
+from capmi import kernels as K
 from capmi.optim import Adam as FusedAdam
 from checkpoint import load_checkpoint, save_checkpoint, unpack_checkpoint
 from metric import AccumulatingMetric
@@ -120,6 +121,55 @@ def _train_dataset(args):
     return COCODataset(mode='train', caption_max_len=args.max_caption_length)
 
 
+def _build_models(args, vocab, device):
+    """Encoder + decoder of train() (reference :329-364): fresh from the args, or resumed from
+    ``args.checkpoint`` (state_dict or whole-module format). Returns (encoder, decoder,
+    start_epoch, metrics, decoder optimizer state, encoder optimizer state)."""
+    enc_opt_state = None
+    if args.checkpoint is None:
+        encoder = EncoderAttention()
+        if args.fine_tune_encoder:
+            # the reference builds Adam over an all-frozen encoder here and crashes (Q9);
+            # fine-tuning means fine_tune(True): layer2-4 trainable (models/encoder.py:112-121)
+            encoder.fine_tune(True)
+        decoder_params = AttentionDecoderParams()
+        decoder_params.attention_dim = args.attention_dim
+        decoder_params.decoder_dim = args.decoder_dim
+        decoder_params.embed_size = args.embed_size
+        decoder_params.dropout = args.decoder_dropout
+        decoder_params.vocab = vocab
+        decoder_params.use_bert = args.use_bert
+        decoder = AttentionDecoder(device, decoder_params)
+        if args.use_glove:
+            from embed import load_glove_vectors
+            decoder.load_pretrained_embeddins(load_glove_vectors())
+        decoder.fine_tune_embeddings(args.fine_tune_embedding)
+        start_epoch, metrics, opt_state = 0, {}, None
+    else:
+        chkpt = load_checkpoint(device, args, weights_only=not getattr(args, 'trusted_checkpoint', False))
+        start_epoch, enc_sd, dec_sd, enc_opt_state, opt_state, metrics = unpack_checkpoint(chkpt)
+        # whole-module checkpoints (save_checkpoint(..., whole_modules=True), the reference's format)
+        enc_sd, dec_sd, enc_opt_state, opt_state = (
+            v.state_dict() if hasattr(v, 'state_dict') else v for v in (enc_sd, dec_sd, enc_opt_state, opt_state))
+        start_epoch += 1
+        encoder = EncoderAttention()
+        encoder.load_state_dict(enc_sd)
+        if args.fine_tune_encoder:
+            encoder.fine_tune(True)
+        decoder_params = AttentionDecoderParams()
+        decoder_params.attention_dim, decoder_params.decoder_dim = args.attention_dim, args.decoder_dim
+        decoder_params.embed_size, decoder_params.dropout = args.embed_size, args.decoder_dropout
+        decoder_params.vocab = vocab
+        decoder_params.use_bert = args.use_bert  # as the fresh-start branch (the pickle keeps it)
+        decoder = AttentionDecoder(device, decoder_params)
+        if dec_sd["embedding.weight"].dtype == torch.float64:
+            decoder.load_pretrained_embeddins(dec_sd["embedding.weight"].clone())
+        decoder.load_state_dict(dec_sd)
+        decoder.fine_tune_embeddings(args.fine_tune_embedding)
+
+    return encoder, decoder, start_epoch, metrics, opt_state, enc_opt_state
+
+
 def train(device, args):
     """Trains the attention model (reference :287-452), same loop and log line.
 
@@ -153,48 +203,12 @@ def train(device, args):
         dataset=dataset, batch_size=args.batch_size, shuffle=sampler is None, sampler=sampler,
         num_workers=args.workers, collate_fn=collate_fn, pin_memory=True)
 
-    if args.checkpoint is None:
-        encoder = EncoderAttention()
-        if args.fine_tune_encoder:
-            # the reference builds Adam over an all-frozen encoder here and crashes (Q9);
-            # fine-tuning means fine_tune(True): layer2-4 trainable (models/encoder.py:112-121)
-            encoder.fine_tune(True)
-        decoder_params = AttentionDecoderParams()
-        decoder_params.attention_dim = args.attention_dim
-        decoder_params.decoder_dim = args.decoder_dim
-        decoder_params.embed_size = args.embed_size
-        decoder_params.dropout = args.decoder_dropout
-        decoder_params.vocab = dataset.vocab
-        decoder_params.use_bert = args.use_bert
-        decoder = AttentionDecoder(device, decoder_params)
-        if args.use_glove:
-            from embed import load_glove_vectors
-            decoder.load_pretrained_embeddins(load_glove_vectors())
-        decoder.fine_tune_embeddings(args.fine_tune_embedding)
-        start_epoch, metrics, opt_state = 0, {}, None
-    else:
-        chkpt = load_checkpoint(device, args, weights_only=not getattr(args, 'trusted_checkpoint', False))
-        start_epoch, enc_sd, dec_sd, enc_opt_state, opt_state, metrics = unpack_checkpoint(chkpt)
-        # whole-module checkpoints (save_checkpoint(..., whole_modules=True), the reference's format)
-        enc_sd, dec_sd, enc_opt_state, opt_state = (
-            v.state_dict() if hasattr(v, 'state_dict') else v for v in (enc_sd, dec_sd, enc_opt_state, opt_state))
-        start_epoch += 1
-        encoder = EncoderAttention()
-        encoder.load_state_dict(enc_sd)
-        if args.fine_tune_encoder:
-            encoder.fine_tune(True)
-        decoder_params = AttentionDecoderParams()
-        decoder_params.attention_dim, decoder_params.decoder_dim = args.attention_dim, args.decoder_dim
-        decoder_params.embed_size, decoder_params.dropout = args.embed_size, args.decoder_dropout
-        decoder_params.vocab = dataset.vocab
-        decoder = AttentionDecoder(device, decoder_params)
-        if dec_sd["embedding.weight"].dtype == torch.float64:
-            decoder.load_pretrained_embeddins(dec_sd["embedding.weight"].clone())
-        decoder.load_state_dict(dec_sd)
-        decoder.fine_tune_embeddings(args.fine_tune_embedding)
-
+    encoder, decoder, start_epoch, metrics, opt_state, enc_opt_state = _build_models(args, dataset.vocab, device)
     encoder = encoder.to(device)
     decoder = decoder.to(device)
+    # every rank starts from rank 0's weights and BN buffers: without models/resnet101.pth the
+    # (frozen) ResNet keeps a random init that would differ per rank
+    cdist.broadcast_module(encoder, ctx)
     cdist.broadcast_module(decoder, ctx)
     decoder_optimizer = FusedAdam(filter(lambda p: p.requires_grad, decoder.parameters()),
                                   lr=args.decoder_lr)
@@ -202,7 +216,6 @@ def train(device, args):
         decoder_optimizer.load_state_dict(opt_state)
     encoder_optimizer = None
     if args.fine_tune_encoder:
-        cdist.broadcast_module(encoder, ctx)
         encoder_optimizer = FusedAdam(filter(lambda p: p.requires_grad, encoder.parameters()),
                                       lr=args.encoder_lr)
         if args.checkpoint is not None and enc_opt_state is not None:
@@ -248,6 +261,7 @@ def train(device, args):
             if (batch_idx % args.print_freq == 0 or batch_idx == num_batches - 1) and pending:
                 if device.type == "cuda":
                     torch.cuda.synchronize()  # losses live on the decoder stream
+                    K.sk_check()  # stream-K hand-off invariant (raises on a timed-out hand-off)
                 for l in torch.stack([p for p in pending if p is not None]).view(-1).tolist():
                     batch_losses.append(l)
                     accum_loss.update(l)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 9
+#define CAPMI_ABI_VERSION 10
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -95,6 +95,11 @@ int capmi_gemm_stat_tiles(int M, int tile);
  * before first use (the kernel leaves it reusable); one workspace per concurrently running
  * stream. */
 long long capmi_gemm_workspace_bytes(void);
+/* Bytes at the start of the stream-K workspace holding the hand-off flags and the spin-timeout
+ * error word. Every one of these int32 words is zero between launches; a nonzero word after a
+ * launch has completed means a hand-off timed out (result invalid): the host checks this at its
+ * sync points (capmi.kernels.sk_check), raises, and re-zeroes the workspace. */
+long long capmi_gemm_workspace_flag_bytes(void);
 int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int tile, void* workspace,
                   long long ws_bytes, void* stream);
 /* capmi_gemm_sk with flags: CAPMI_GEMM_BF16 = operands rounded to bf16 (RNE) when staged to LDS,

@@ -83,3 +83,28 @@ def test_whole_module_checkpoint_gpu(tmp_path, monkeypatch):
         p2 = d.eval()(f2, caps, [6, 6])[0]
     torch.cuda.synchronize()
     assert torch.equal(f1, f2) and torch.equal(p1, p2)
+
+
+@pytest.mark.parametrize("fmt", ["state_dict", "whole_modules"])
+def test_resume_keeps_use_bert(tmp_path, monkeypatch, fmt):
+    """train()'s resume branch rebuilds the decoder with the run's --use_bert (the reference
+    resumes the pickled module, which keeps it): a BERT checkpoint must not resume on the
+    word-embedding path."""
+    from models import attention as MA
+    from vocabulary import synthetic_vocab
+    monkeypatch.setattr(C, "CHECKPOINTS_DIR", str(tmp_path))
+    vocab = synthetic_vocab(50)
+    args = types.SimpleNamespace(model_name="bert_att", checkpoint=None, fine_tune_encoder=False,
+                                 attention_dim=32, decoder_dim=32, embed_size=768, decoder_dropout=0.5,
+                                 use_bert=True, use_glove=False, fine_tune_embedding=False)
+    enc, dec, _, _, _, _ = MA._build_models(args, vocab, "cpu")
+    assert dec.use_bert
+    from capmi.optim import Adam
+    opt = Adam([p for p in dec.parameters() if p.requires_grad], lr=1e-4)
+    C.save_checkpoint(args, 2, enc, dec, None, opt, {}, verbose=False, whole_modules=(fmt == "whole_modules"))
+    args.checkpoint = "bert_att_2.pth.tar"
+    args.trusted_checkpoint = fmt == "whole_modules"
+    enc2, dec2, ep, _, ost, _ = MA._build_models(args, vocab, "cpu")
+    assert ep == 3 and dec2.use_bert and ost is not None
+    for k, v in dec.state_dict().items():
+        assert torch.equal(dec2.state_dict()[k], v), k
