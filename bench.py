@@ -25,8 +25,8 @@ instantiation with the most time per step (the conv family is 86% of the step's 
 family aggregate is reported beside it). achieved = that kernel's algorithmic conv FLOPs /
 its summed launch time. The launch times come from a graph-node timing pass right after the
 timed region: the same step (same launch mode, same graphs structure) is captured again with
-timing events recorded as graph nodes (hipEventRecordWithFlags(External)) around every conv
-launch, on the launch stream, and --steps calls are replayed and read back one by one.
+timing events recorded as graph nodes (capmi_timing_event_record: hipEventRecordWithFlags(External))
+around every conv launch, on the launch stream, and --steps calls are replayed and read back one by one.
 ``cpu_baseline`` times the CPU oracle (op-for-op restatement of the reference step) on the
 host cores, rank 0 at N = 1 only: the full batch (64 images) for at least one step.
 
@@ -131,8 +131,8 @@ class ConvTimer:
             if self.label is None:
                 launch()
                 return
-            s = torch.cuda.Event(enable_timing=True, external=True)
-            e = torch.cuda.Event(enable_timing=True, external=True)
+            from capmi.kernels import TimingEvent
+            s, e = TimingEvent(), TimingEvent()
             s.record()
             launch()
             e.record()
@@ -154,7 +154,7 @@ class ConvTimer:
                 ent = self.acc.setdefault(key, [0, 0.0, 0.0])
                 ent[0] += 1
                 ent[1] += f
-                ent[2] += s.elapsed_time(e)
+                ent[2] += s.elapsed_ms(e)
 
     def result(self):
         """{kernel key: [launches, flops, ms]}."""

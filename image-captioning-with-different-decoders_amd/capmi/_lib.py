@@ -111,6 +111,10 @@ _SIGS = {
     "capmi_resize_normalize_u8": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,
                                   c_vp, c_vp],
     "capmi_resize_taps_max": [c_int, c_int],
+    "capmi_timing_event_create": [ctypes.POINTER(c_vp)],
+    "capmi_timing_event_destroy": [c_vp],
+    "capmi_timing_event_record": [c_vp, c_vp],
+    "capmi_timing_elapsed_ms": [c_vp, c_vp, ctypes.POINTER(c_float)],
     "capmi_strerror": [c_int],
     "capmi_abi_version": [],
 }

@@ -490,3 +490,30 @@ def embed_scatter_add(dx, ld_dx, caps, B, L, T, bt_dev, M, demb):
 
 TILE_128, TILE_64, TILE_128x64, TILE_AUTO = CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO
 BNB_RELU_Y, BNB_RELU_OUT = 0, 1
+
+
+# --------------------------------------------------------------------------------------
+# timing events that can live inside HIP graphs (bench.py)
+# --------------------------------------------------------------------------------------
+class TimingEvent:
+    """A HIP timing event; ``record()`` on the current stream becomes a graph node when that
+    stream is being captured (torch refuses external events on ROCm)."""
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        call("capmi_timing_event_create", ctypes.byref(h))
+        self.h = h
+
+    def record(self):
+        call("capmi_timing_event_record", self.h, stream())
+
+    def elapsed_ms(self, end):
+        ms = ctypes.c_float()
+        call("capmi_timing_elapsed_ms", self.h, end.h, ctypes.byref(ms))
+        return float(ms.value)
+
+    def __del__(self):
+        try:
+            lib.capmi_timing_event_destroy(self.h)
+        except Exception:  # noqa: BLE001  (interpreter shutdown)
+            pass

@@ -342,6 +342,15 @@ int capmi_adam_clamp_f64(double* p, const double* g, double* m, double* v, long 
 int capmi_embed_scatter_add(const float* dx, long long ld_dx, const long long* caps, int B, int L,
                             int T, const int* bt, int M, void* demb, int demb_is_f64, void* stream);
 
+/* ---- kernel timing inside HIP graphs (bench.py's roofline) -------------------------------
+ * Timing events whose record becomes a graph node when `stream` is being captured
+ * (hipEventRecordExternal), a plain record otherwise; after a replay has completed,
+ * capmi_timing_elapsed_ms gives the time between two records (milliseconds). */
+int capmi_timing_event_create(void** event);
+int capmi_timing_event_destroy(void* event);
+int capmi_timing_event_record(void* event, void* stream);
+int capmi_timing_elapsed_ms(void* start, void* end, float* ms);
+
 const char* capmi_strerror(int code);
 int capmi_abi_version(void);
 
