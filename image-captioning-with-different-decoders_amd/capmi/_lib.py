@@ -28,6 +28,8 @@ CAPMI_BNB_RELU_Y, CAPMI_BNB_RELU_OUT = 0, 1
 CAPMI_BNB_MAX_SLABS = 256
 CAPMI_GEMM_BF16 = 1
 CAPMI_GEMM_BF16_IO = 2
+CAPMI_GEMM_X3 = 4
+CAPMI_GEMM_X3P = 8
 
 
 class GemmProblem(ctypes.Structure):
@@ -111,6 +113,8 @@ _SIGS = {
     "capmi_resize_normalize_u8": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,
                                   c_vp, c_vp],
     "capmi_resize_taps_max": [c_int, c_int],
+    "capmi_split3_bf16": [c_vp, c_ll, c_vp, c_vp],
+    "capmi_bn_relu_split3": [c_vp, c_vp, c_vp, c_ll, c_int, c_vp, c_vp],
     "capmi_timing_event_create": [ctypes.POINTER(c_vp)],
     "capmi_timing_event_destroy": [c_vp],
     "capmi_timing_event_record": [c_vp, c_vp],

@@ -8,7 +8,8 @@ import weakref
 
 import torch
 
-from ._lib import (CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_GEMM_BF16_IO, CAPMI_COLSUM_GROUPS, CAPMI_TILE_128, CAPMI_TILE_64,
+from ._lib import (CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_GEMM_BF16_IO, CAPMI_GEMM_X3, CAPMI_GEMM_X3P,
+                   CAPMI_COLSUM_GROUPS, CAPMI_TILE_128, CAPMI_TILE_64,
                    CAPMI_TILE_128x64, CAPMI_TILE_AUTO, GemmProblem, call, lib)
 
 F32 = torch.float32
@@ -40,7 +41,9 @@ def problem(M, N, K, A, lda, B, ldb, C, ldc, *, a_r1=0, a_s2=0, c_r1=0, c_s2=0, 
             relu=False, stats=None, conv=None, in_scale=None, in_shift=None):
     """Build one ``capmi_gemm_problem``. A/B/C are tensors (or views) whose data_ptr is the
     operand origin; ld* are element strides. ``conv`` = dict(N,H,W,Cin,KH,KW,stride,pad,Ho,Wo)."""
-    _cuda(A, B, C, bias, bias2, stats, in_scale, in_shift)
+    _cuda(C, bias, bias2, stats, in_scale, in_shift)
+    for t_ in (A, B):  # bf16: the split planes of gemm_x3 (B) / gemm_x3p (A and B)
+        _cuda(t_, dtype=torch.bfloat16 if t_ is not None and t_.dtype == torch.bfloat16 else F32)
     p = GemmProblem()
     p.M, p.N, p.K, p.ksplit = int(M), int(N), int(K), int(ksplit)
     p.A, p.lda, p.a_r1, p.a_s2 = ptr(A), int(lda), int(a_r1), int(a_s2)
@@ -128,6 +131,55 @@ def gemm_bf16(prob, amode, workspace, tile=CAPMI_TILE_AUTO):
     _cuda(workspace, dtype=torch.int32)
     call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, tile, CAPMI_GEMM_BF16_IO,
          ptr(workspace), workspace.numel() * 4, stream())
+
+
+def split3_bf16(w, out):
+    """fp32 ``w`` (numel % 4 == 0) -> ``out`` bf16 [3][numel]: the exact three-term split (B operand
+    of gemm_x3)."""
+    _cuda(w)
+    _cuda(out, dtype=torch.bfloat16)
+    if out.numel() < 3 * w.numel():
+        raise ValueError("split3_bf16: out needs 3 * numel elements")
+    call("capmi_split3_bf16", ptr(w), w.numel(), ptr(out), stream())
+
+
+def gemm_x3(prob, amode, workspace, tile=CAPMI_TILE_AUTO):
+    """fp32-accurate GEMM on the bf16 matrix cores (CAPMI_GEMM_X3): fp32 A x B pre-split by
+    split3_bf16 (prob.B = plane 0, prob.ldb its row stride)."""
+    _cuda(workspace, dtype=torch.int32)
+    call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, tile, CAPMI_GEMM_X3,
+         ptr(workspace), workspace.numel() * 4, stream())
+
+
+def bn_relu_split3(y, scale, shift, rows, C, out):
+    """out[3][rows*C] bf16 = the exact split of relu(y*scale+shift) (scale None: of y)."""
+    _cuda(y, scale, shift)
+    _cuda(out, dtype=torch.bfloat16)
+    if out.numel() < 3 * rows * C:
+        raise ValueError("bn_relu_split3: out needs 3 * rows * C elements")
+    call("capmi_bn_relu_split3", ptr(y), ptr(scale), ptr(shift), int(rows), int(C), ptr(out), stream())
+
+
+def gemm_x3p(prob, amode, workspace):
+    """CAPMI_GEMM_X3P: A (prob.A) and B (prob.B) are both plane 0 of three bf16 split planes."""
+    _cuda(workspace, dtype=torch.int32)
+    call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3P,
+         ptr(workspace), workspace.numel() * 4, stream())
+
+
+def gemm_x3p_kernel_name(prob, amode):
+    v = [ctypes.c_int(0) for _ in range(5)]
+    call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3P,
+         *[ctypes.byref(x) for x in v])
+    return f"gemm_x3p_kernel<{amode}, {'true' if v[2].value else 'false'}>"
+
+
+def gemm_x3_kernel_name(prob, amode, tile=CAPMI_TILE_AUTO):
+    v = [ctypes.c_int(0) for _ in range(5)]
+    call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, tile, CAPMI_GEMM_X3,
+         *[ctypes.byref(x) for x in v])
+    b = lambda x: "true" if x else "false"  # noqa: E731
+    return f"gemm_x3_kernel<{v[1].value}, {amode}, {b(bool(prob.in_scale))}, {b(v[2].value)}>"
 
 
 def gemm_sk_plan(prob, amode, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W, bf16=False, threads=False):

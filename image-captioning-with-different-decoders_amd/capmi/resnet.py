@@ -129,6 +129,9 @@ class EncoderRunner:
         # bf16 forward (the bf16 config, BASELINE config 5): bf16 NHWC activations and weights, bf16
         # MFMA with fp32 accumulation, fp32 BN statistics (_forward_bf16); fp32 is the reference's
         self.bf16 = False
+        # fp32 convs as fp32-accurate three-term bf16 split GEMMs (CAPMI_GEMM_X3, gemm_x3.hip) instead
+        # of v_mfma_f32_32x32x2_f32; same fp32 activations, statistics and outputs
+        self.x3 = False
 
     def _workspace(self, N, H, W, device):
         key = (N, H, W, str(device))
@@ -144,8 +147,14 @@ class EncoderRunner:
             ws["ss"] = {}
             ws["sk"] = K.gemm_workspace(device)  # stream-K partials + flags (zeroed once)
             ws["img4"] = torch.empty(N * H * W * 4, **f)  # conv1 input, NHWC padded to 4 channels
+            ws["x3p"] = None
             self._ws, self._ws_key = ws, key
         return self._ws
+
+    def _x3p_buffer(self, ws):
+        if ws["x3p"] is None:  # three bf16 planes of the largest conv input (x3 path only)
+            ws["x3p"] = torch.empty(3 * ws["x"].numel(), device=ws["x"].device, dtype=torch.bfloat16)
+        return ws["x3p"]
 
     def _ss(self, ws, bn):
         ent = ws["ss"].get(id(bn))
@@ -189,13 +198,40 @@ class EncoderRunner:
             geo["Cin"] = 4
             prob = K.problem(rows, co, K4, img4, 0, w, K4, out, co, conv=geo, **kw_)
             mode = CAPMI_A_CONV_NHWC4
+        elif self.x3 and in_ss is not None and co >= 128 and ci % 32 == 0 and Kd % 32 == 0:
+            # x3p: the conv input relu(bn(y)) split once into three bf16 planes, then the GEMM with
+            # both operands pre-split (gemm_x3p.hip)
+            xp = self._x3p_buffer(self._ws)
+            K.bn_relu_split3(x, in_ss[0], in_ss[1], N * H * W, ci, xp)
+            w3 = self._packed_x3(conv)
+            if kh == 1 and st == 1:
+                prob, mode = K.problem(rows, co, Kd, xp, ci, w3, Kd, out, co, **kw_), CAPMI_A_KMAJOR
+            else:
+                prob, mode = K.problem(rows, co, Kd, xp, 0, w3, Kd, out, co, conv=geo, **kw_), CAPMI_A_CONV_NHWC
+            launch = lambda: K.gemm_x3p(prob, mode, self._ws["sk"])  # noqa: E731
+            if self.conv_hook is not None:
+                self.conv_hook(tag, 2.0 * rows * co * Kd, launch, K.gemm_x3p_kernel_name(prob, mode))
+            else:
+                launch()
+            return Ho, Wo, rows
         elif kh == 1 and st == 1 and in_ss is None:
+            if self.x3 and Kd % 32 == 0:
+                w = self._packed_x3(conv)
             prob = K.problem(rows, co, Kd, x, ci, w, Kd, out, co, **kw_)
             mode = CAPMI_A_KMAJOR
         else:
             sc, sh = in_ss if in_ss is not None else (None, None)
+            if self.x3 and Kd % 32 == 0 and ci % 32 == 0:
+                w = self._packed_x3(conv)
             prob = K.problem(rows, co, Kd, x, 0, w, Kd, out, co, conv=geo, in_scale=sc, in_shift=sh, **kw_)
             mode = CAPMI_A_CONV_NHWC
+        if w.dtype == torch.bfloat16:  # the three-plane split weight: fp32-accurate x3 GEMM
+            launch = lambda: K.gemm_x3(prob, mode, self._ws["sk"])  # noqa: E731
+            if self.conv_hook is not None:
+                self.conv_hook(tag, 2.0 * rows * co * Kd, launch, K.gemm_x3_kernel_name(prob, mode))
+            else:
+                launch()
+            return Ho, Wo, rows
         bf = self.bf16
         launch = lambda: K.gemm_sk(prob, mode, self._ws["sk"], K.TILE_AUTO, bf16=bf)  # noqa: E731
         if self.conv_hook is not None:
@@ -205,6 +241,21 @@ class EncoderRunner:
             launch()
         del stats
         return Ho, Wo, rows
+
+    def _packed_x3(self, conv):
+        """[3][Cout][K] bf16 split of the packed fp32 weight (B operand of gemm_x3), refreshed when the
+        weight tensor changes (FineTuneRunner drops the trainable convs' entries every step: the
+        fused Adam writes the weights in place without bumping their version)."""
+        w = conv.weight
+        key = ("x3", id(conv))
+        ent = self.packed.cache.get(key)
+        if ent is None or ent[0] != w._version or ent[1] != w.data_ptr():
+            src = self.packed.get(conv).contiguous()
+            dst = torch.empty(3 * src.numel(), device=w.device, dtype=torch.bfloat16)
+            K.split3_bf16(src, dst)
+            ent = (w._version, w.data_ptr(), dst)
+            self.packed.cache[key] = ent
+        return ent[2]
 
     # ---- bf16 activations (BASELINE config 5) -------------------------------------------------
     def _packed_bf16(self, conv):
@@ -438,6 +489,9 @@ class FineTuneRunner:
         for li in range(self.first, 5):
             for blk in getattr(net, f"layer{li}"):
                 r.packed.cache.pop(id(blk.conv2), None)
+                convs = [blk.conv1, blk.conv2, blk.conv3] + ([blk.downsample[0]] if blk.downsample is not None else [])
+                for c in convs:
+                    r.packed.cache.pop(("x3", id(c)), None)
         H1, W1, rows = r._conv("conv1", imgs, net.conv1, ws["y1"], N, H, W, True, nchw=True)
         s, b = r._bn(ws, net.bn1, rows, True)
         Hp, Wp = (H1 + 2 - 3) // 2 + 1, (W1 + 2 - 3) // 2 + 1

@@ -1,0 +1,409 @@
+// fp32-accurate GEMM / implicit-GEMM convolution with BOTH operands pre-split into three bf16
+// planes ("x3p"; the arithmetic of gemm_x3.hip: six cross products above 2^-23 |a||b|, fp32
+// accumulation on v_mfma_f32_32x32x16_bf16). The conv input relu(bn(y)) is split once per tensor
+// by capmi_bn_relu_split3 (a 3x3 conv reads every input element nine times, a 1x1 conv with
+// N = 1024 re-stages each A tile for eight column tiles: splitting in the GEMM repeated the VALU
+// work that often), the weights once per weight version (capmi_split3_bf16).
+//
+// Structure: 256 x 128 tile, 512 threads = 8 waves as 4 (M) x 2 (N), wave tile 64 x 64 (2 x 2
+// MFMA tiles: per 16-k k-tile 6 + 6 ds_read_b128 feed 24 MFMAs), BK = 16. Staging is LDS-DMA
+// (buffer_load_dwordx4 ... lds, no VGPRs, no ds_write): one wave-instruction moves 32 rows x 32 B
+// of one plane into a lane-linear 1 KiB LDS block; the 16-B chunk of row r in slot s holds the
+// logical k-chunk s ^ ((r >> 3) & 1) (the swizzle goes on the per-lane SOURCE address), so the
+// 16-lane groups of ds_read_b128 hit 64 distinct banks. Padding taps and rows past M read zeros
+// (buffer offsets past the descriptor's range). Three LDS buffers (3 x 36 KiB, one array): the DMA
+// of k-tile t+2 is issued right after the barrier that opens tile t, so every tile's DMA has two
+// tiles of MFMA work to land; the opening wait is a counted vmcnt (the next tile's DMA stays in
+// flight) and the barrier a raw s_barrier (__syncthreads would drain it). Epilogue (fp32 C,
+// alpha/bias/beta/relu, per-64-row BN statistics: a wave's 64 rows are one slice) and the stream-K
+// / hybrid schedule with the write-through hand-off are those of gemm_nt.hip.
+#include "gemm_args.h"
+
+namespace {
+
+constexpr int PBM = 256, PBN = 128, PBK = 16, PNT = 512;
+constexpr int PROWB = PBK * 2;                     // bytes per LDS row (16 bf16)
+constexpr int PA_BYTES = 3 * PBM * PROWB;          // 24 KiB: A planes of one k-tile
+constexpr int PB_BYTES = 3 * PBN * PROWB;          // 12 KiB
+constexpr int PBUF = PA_BYTES + PB_BYTES;          // 36 KiB per buffer
+constexpr int PNBUF = 3;
+typedef unsigned u32x4_p __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_p __attribute__((ext_vector_type(8)));
+constexpr unsigned kOOBp = 0x80000000u;
+constexpr int kSc1p = 16;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_p(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+template <int AMODE, bool SK>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+gemm_x3p_kernel(const GemmArgs args) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[PNBUF * PBUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm0 = (wid >> 1) * 64, wn0 = (wid & 1) * 64;
+  const int lr = lane & 31, lh = lane >> 5;
+  // DMA lane geometry: row (lane >> 1) of a 32-row block, slot (lane & 1)
+  const int drow = lane >> 1, dslot = lane & 1;
+
+  f32x16 acc[2][2];
+
+  auto mainloop = [&](const capmi_gemm_problem& P, int m0, int n0, int k_lo, int k_hi) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int nkt = (k_hi - k_lo) / PBK;
+    if (nkt <= 0) return;
+    const int M = P.M, N = P.N;
+    const int cH = P.cH, cW = P.cW, cCin = P.cCin, cKW = P.cKW;
+    const long long planeA = AMODE == 2 ? (long long)P.cN * cH * cW * cCin : (long long)M * P.lda;
+    const long long planeB = (long long)N * P.ldb;
+    const auto ra = rsrc_p(P.A, (unsigned)(3 * planeA * 2));
+    const auto rb = rsrc_p(P.B, (unsigned)(3 * planeB * 2));
+    // this lane's A row (row block wid: rows 32 wid ..) and, for waves 0-3, its B row
+    const int ar = wid * 32 + drow;
+    const int a_ch = dslot ^ ((ar >> 3) & 1);
+    const int arow = m0 + ar;
+    const bool a_ok = arow < M;
+    unsigned a_base;  // dense: byte offset of (row, chunk) in plane 0; conv: pixel index of (n, 0, 0)
+    int a_ih0 = 0, a_iw0 = 0;
+    if (AMODE == 0) {
+      a_base = (unsigned)(((long long)(a_ok ? arow : 0) * P.lda + a_ch * 8) * 2);
+    } else {
+      const int hw = P.cHo * P.cWo;
+      const int rr = a_ok ? arow : 0;
+      const int n = rr / hw, rem = rr - n * hw;
+      const int oh = rem / P.cWo, ow = rem - oh * P.cWo;
+      a_ih0 = oh * P.cStride - P.cPad;
+      a_iw0 = ow * P.cStride - P.cPad;
+      a_base = (unsigned)(n * cH * cW);
+    }
+    const bool bw = wid < 4;  // waves 0-3 also stage B (row block wid)
+    const int br = (wid & 3) * 32 + drow;
+    const int b_ch = dslot ^ ((br >> 3) & 1);
+    const bool b_ok = n0 + br < N;
+    const unsigned b_base = (unsigned)(((long long)(b_ok ? n0 + br : 0) * P.ldb + b_ch * 8) * 2);
+    int c_ci = 0, c_kh = 0, c_kw = 0;
+    if (AMODE == 2) {
+      const int kpos = k_lo / cCin;
+      c_ci = k_lo - kpos * cCin;
+      c_kh = kpos / cKW;
+      c_kw = kpos - c_kh * cKW;
+    }
+    const unsigned pA2 = (unsigned)(planeA * 2), pB2 = (unsigned)(planeB * 2);
+
+    // DMA of k-tile kt into buffer buf: 3 A (+ 3 B for waves 0-3) wave-instructions per wave
+    auto issue = [&](int kt, int buf) {
+      const int k = k_lo + kt * PBK;
+      const bool kok = k < k_hi;
+      unsigned aoff;
+      if (AMODE == 0) {
+        aoff = a_ok && kok ? a_base + (unsigned)k * 2 : kOOBp;
+      } else {
+        const int ih = a_ih0 + c_kh, iw = a_iw0 + c_kw;
+        const bool ok = a_ok && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
+        aoff = ok ? ((a_base + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + a_ch * 8)) * 2u : kOOBp;
+        c_ci += PBK;
+        if (c_ci >= cCin) {
+          c_ci = 0;
+          if (++c_kw == cKW) {
+            c_kw = 0;
+            ++c_kh;
+          }
+        }
+      }
+      unsigned char* base = lds + buf * PBUF;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(base + p * PBM * PROWB + wid * 32 * PROWB), 16,
+                                                 aoff == kOOBp ? kOOBp : aoff + p * pA2, 0, 0, 0);
+      if (bw) {
+        const unsigned boff = b_ok && kok ? b_base + (unsigned)k * 2 : kOOBp;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * 32 * PROWB), 16,
+              boff == kOOBp ? kOOBp : boff + p * pB2, 0, 0, 0);
+      }
+    };
+    auto compute = [&](int buf) {
+      const unsigned char* A_ = lds + buf * PBUF;
+      const unsigned char* B_ = A_ + PA_BYTES;
+      bf16x8_p a[2][3], b[2][3];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = wm0 + 32 * i + lr;
+        const int o = r * PROWB + ((lh ^ ((r >> 3) & 1)) << 4);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) a[i][p] = *reinterpret_cast<const bf16x8_p*>(A_ + p * PBM * PROWB + o);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wn0 + 32 * j + lr;
+        const int o = r * PROWB + ((lh ^ ((r >> 3) & 1)) << 4);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) b[j][p] = *reinterpret_cast<const bf16x8_p*>(B_ + p * PBN * PROWB + o);
+      }
+      // smallest terms first into each fp32 accumulator
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[j][0], acc[i][j], 0, 0, 0);
+        }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][0], acc[i][j], 0, 0, 0);
+        }
+    };
+    issue(0, 0);
+    issue(1, 1);
+    int cur = 0, nxt = 2;  // buffer of tile kt, buffer tile kt + 2 goes to
+    for (int kt = 0; kt < nkt; ++kt) {
+      // tile kt has landed when at most one tile's DMA (kt + 1) is still outstanding
+      if (bw)
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt landed; tile kt - 1 fully read
+      issue(kt + 2, nxt);            // past the end: OOB loads (zeros) into the free buffer
+      compute(cur);
+      cur = cur == 2 ? 0 : cur + 1;
+      nxt = nxt == 2 ? 0 : nxt + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // the buffers are free for the next tile (stream-K)
+  };
+
+  auto epilogue = [&](const capmi_gemm_problem& P, int tm, int tn) {
+    const int M = P.M, N = P.N;
+    const int m0 = tm * PBM, n0 = tn * PBN;
+    const float alpha = P.alpha * (P.alpha_ptr ? *P.alpha_ptr : 1.f);
+    float* C = P.C;
+    const float beta = P.beta;
+    const int relu = P.relu;
+    const long long ldc = P.ldc, c_r1 = P.c_r1, c_s2 = P.c_s2;
+    float csum[2], csq[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      csum[j] = 0.f;
+      csq[j] = 0.f;
+      const int col = n0 + wn0 + 32 * j + lr;
+      const bool cok = col < N;
+      float bias = 0.f;
+      if (cok) {
+        if (P.bias) bias += P.bias[col];
+        if (P.bias2) bias += P.bias2[col];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (cok && row < M) {
+            float* cp = C + remap(row, c_r1, ldc, c_s2) + col;
+            float v = fmaf(acc[i][j][r], alpha, bias);
+            if (beta != 0.f) v = fmaf(beta, *cp, v);
+            if (relu) v = fmaxf(v, 0.f);
+            *cp = v;
+            csum[j] += v;
+            csq[j] = fmaf(v, v, csq[j]);
+          }
+        }
+    }
+    float* __restrict__ stats = P.stats;
+    if (stats != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        csum[j] += __shfl_xor(csum[j], 32, 64);
+        csq[j] += __shfl_xor(csq[j], 32, 64);
+      }
+      if (lh == 0) {  // the wave's 64 rows are one 64-row slice
+        const long long sl = (m0 + wm0) >> 6;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int col = n0 + wn0 + 32 * j + lr;
+          if (col < N && m0 + wm0 < M) {
+            stats[(sl * N + col) * 2 + 0] = csum[j];
+            stats[(sl * N + col) * 2 + 1] = csq[j];
+          }
+        }
+      }
+    }
+  };
+
+  if (!SK) {
+    int bid = blockIdx.x;
+    {
+      const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = bid & 7;
+      bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+    }
+    const capmi_gemm_problem& P = args.p[0];
+    const int tiles_n = args.tiles_n[0];
+    const int tn = bid % tiles_n, tm = bid / tiles_n;
+    mainloop(P, tm * PBM, tn * PBN, 0, P.K);
+    epilogue(P, tm, tn);
+    return;
+  }
+
+  const capmi_gemm_problem& P = args.p[0];
+  const int nkt = args.sk_nkt, tiles_n = args.tiles_n[0];
+  const long long ngrp = args.sk_groups, grp = blockIdx.x % ngrp;
+  const long long T = args.sk_units / nkt, G = gridDim.x / ngrp, w = blockIdx.x / ngrp;
+  if (args.sk_dp_tiles > 0) {
+    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = blockIdx.x & 7;
+    const int pos = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (blockIdx.x >> 3);
+    for (long long t = T + pos; t < T + args.sk_dp_tiles; t += nwg) {
+      const int tm = (int)(t / tiles_n), tn = (int)(t % tiles_n);
+      mainloop(P, tm * PBM, tn * PBN, 0, P.K);
+      epilogue(P, tm, tn);
+    }
+  }
+  const long long ub = grp * T / ngrp * nkt, U = ((grp + 1) * T / ngrp) * nkt - ub;
+  const long long u0 = ub + w * U / G, u1 = ub + (w + 1) * U / G;
+  if (u0 >= u1) return;
+  constexpr int PART = PBM * PBN;
+  int* flags = args.sk_flags;
+  for (long long t = (u1 - 1) / nkt; t >= u0 / nkt; --t) {
+    const long long tb = t * nkt;
+    const int ks = (int)(max(u0, tb) - tb), ke = (int)(min(u1, tb + nkt) - tb);
+    const int tm = (int)(t / tiles_n), tn = (int)(t % tiles_n);
+    mainloop(P, tm * PBM, tn * PBN, ks * PBK, ke * PBK);
+    if (ke < nkt) {
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + (long long)blockIdx.x * PART, 0,
+                                                        PART * 4, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            u32x4_p v;
+            v.x = __float_as_uint(acc[i][j][4 * q + 0]);
+            v.y = __float_as_uint(acc[i][j][4 * q + 1]);
+            v.z = __float_as_uint(acc[i][j][4 * q + 2]);
+            v.w = __float_as_uint(acc[i][j][4 * q + 3]);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (((i * 2 + j) * 4 + q) * PNT + tid) * 16, 0, kSc1p);
+          }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(flags + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      continue;
+    }
+    if (ks > 0) {
+      for (long long w2 = w - 1;; --w2) {
+        const long long b2 = w2 * ngrp + grp;
+        if (tid == 0) {
+          int spins = 0;
+          while (__hip_atomic_load(flags + b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+                 ++spins < (1 << 22))
+            __builtin_amdgcn_s_sleep(2);
+          // never expected: raise the error word and leave b2's flag (capmi.kernels.sk_check)
+          if (spins >= (1 << 22))
+            __hip_atomic_store(flags + gridDim.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else
+            __hip_atomic_store(flags + b2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + b2 * PART, 0, PART * 4, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const u32x4_p v =
+                  __builtin_amdgcn_raw_buffer_load_b128(rs, (((i * 2 + j) * 4 + q) * PNT + tid) * 16, 0, kSc1p);
+              acc[i][j][4 * q + 0] += __uint_as_float(v.x);
+              acc[i][j][4 * q + 1] += __uint_as_float(v.y);
+              acc[i][j][4 * q + 2] += __uint_as_float(v.z);
+              acc[i][j][4 * q + 3] += __uint_as_float(v.w);
+            }
+        if (ub + w2 * U / G <= tb) break;
+      }
+    }
+    epilogue(P, tm, tn);
+  }
+}
+
+// x = relu(y * scale[c] + shift[c]) split into three bf16 planes out[p][i] (the x3p A operand)
+__global__ void __launch_bounds__(256) bn_relu_split3_kernel(const float4* __restrict__ y, const float* __restrict__ sc,
+                                                            const float* __restrict__ sh, long long n4, int C4,
+                                                            unsigned long long* __restrict__ out, int relu_bn) {
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += stride) {
+    float4 v = y[i];
+    if (relu_bn) {
+      const int c = (int)(i % C4) * 4;
+      const float4 s = *reinterpret_cast<const float4*>(sc + c), b = *reinterpret_cast<const float4*>(sh + c);
+      v = make_float4(fmaxf(fmaf(v.x, s.x, b.x), 0.f), fmaxf(fmaf(v.y, s.y, b.y), 0.f),
+                      fmaxf(fmaf(v.z, s.z, b.z), 0.f), fmaxf(fmaf(v.w, s.w, b.w), 0.f));
+    }
+    const float e[4] = {v.x, v.y, v.z, v.w};
+    unsigned short h[3][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const __bf16 h0 = (__bf16)e[q];
+      const float r1 = e[q] - (float)h0;
+      const __bf16 h1 = (__bf16)r1;
+      const __bf16 h2 = (__bf16)(r1 - (float)h1);
+      h[0][q] = __builtin_bit_cast(unsigned short, h0);
+      h[1][q] = __builtin_bit_cast(unsigned short, h1);
+      h[2][q] = __builtin_bit_cast(unsigned short, h2);
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      out[p * n4 + i] = (unsigned long long)h[p][0] | ((unsigned long long)h[p][1] << 16) |
+                        ((unsigned long long)h[p][2] << 32) | ((unsigned long long)h[p][3] << 48);
+  }
+}
+
+}  // namespace
+
+int gemm_x3p_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
+  const dim3 g(blocks), b(PNT);
+  const bool sk = a.sk_workers > 0;
+  if (amode == 2) {
+    if (sk)
+      hipLaunchKernelGGL((gemm_x3p_kernel<2, true>), g, b, 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm_x3p_kernel<2, false>), g, b, 0, s, a);
+  } else {
+    if (sk)
+      hipLaunchKernelGGL((gemm_x3p_kernel<0, true>), g, b, 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm_x3p_kernel<0, false>), g, b, 0, s, a);
+  }
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int capmi_bn_relu_split3(const float* y, const float* scale, const float* shift, long long rows, int C,
+                                    void* out, void* stream) {
+  CAPMI_REQUIRE(y && out && rows >= 0 && C > 0 && C % 4 == 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE((scale == nullptr) == (shift == nullptr), CAPMI_EINVAL);
+  CAPMI_REQUIRE(aligned16(y) && ((reinterpret_cast<uintptr_t>(out) & 7u) == 0) &&
+                    (scale == nullptr || (aligned16(scale) && aligned16(shift))),
+                CAPMI_EALIGN);
+  const long long n4 = rows * C / 4;
+  if (n4 == 0) return 0;
+  const unsigned blocks = (unsigned)std::min<long long>(std::max<long long>(cdiv(n4, 256), 1), 8192);
+  hipLaunchKernelGGL(bn_relu_split3_kernel, dim3(blocks), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const float4*>(y), scale, shift, n4, C / 4,
+                     static_cast<unsigned long long*>(out), scale != nullptr ? 1 : 0);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}

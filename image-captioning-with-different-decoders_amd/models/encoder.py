@@ -83,14 +83,17 @@ def _runner_free_state(module):
     runner = st.pop("_runner", None)
     st.pop("_ft_runner", None)
     st["_capmi_bf16"] = bool(runner is not None and runner.bf16)
+    st["_capmi_x3"] = bool(runner is not None and getattr(runner, "x3", False))
     return st
 
 
 def _runner_restore(module, st):
     bf16 = st.pop("_capmi_bf16", False)
+    x3 = st.pop("_capmi_x3", False)
     nn.Module.__setstate__(module, st)
     module._runner = EncoderRunner()
     module._runner.bf16 = bf16
+    module._runner.x3 = x3
 
 class Encoder(nn.Module):
     """CNN encoder of the baseline model (reference :22-69)."""
@@ -152,12 +155,16 @@ class EncoderAttention(nn.Module):
         _runner_restore(self, st)
 
     def set_compute_precision(self, precision):
-        """'fp32' (the reference's) or 'bf16': the frozen forward on bf16 NHWC activations and
-        weights, bf16 MFMA with fp32 accumulation and fp32 BatchNorm statistics, features returned
-        fp32 -- the bf16 config (BASELINE config 5)."""
-        if precision not in ("fp32", "bf16"):
+        """'fp32' (the reference's: v_mfma_f32_32x32x2_f32), 'fp32-x3' (fp32-accurate: the convs'
+        fp32 operands split exactly into three bf16 terms whose six significant cross products are
+        accumulated in fp32 on the bf16 matrix cores; fp32 activations, statistics and features) or
+        'bf16': the frozen forward on bf16 NHWC activations and weights, bf16 MFMA with fp32
+        accumulation and fp32 BatchNorm statistics, features returned fp32 -- the bf16 config
+        (BASELINE config 5)."""
+        if precision not in ("fp32", "fp32-x3", "bf16"):
             raise ValueError(precision)
         self._runner.bf16 = precision == "bf16"
+        self._runner.x3 = precision == "fp32-x3"
 
     def _out_hw(self):
         out_hw = self.adaptive_pool.output_size

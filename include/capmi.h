@@ -114,6 +114,21 @@ int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int t
  * alpha 1, beta 0, no bias / relu / prologue / ksplit (the bf16 encoder materialises the conv
  * input with capmi_bn_relu_bf16). Tile 128x128, or 128x64 for CAPMI_TILE_128x64 / N <= 64. */
 #define CAPMI_GEMM_BF16_IO 2
+/* CAPMI_GEMM_X3 (alone): fp32-accurate GEMM on the bf16 matrix cores. A is fp32 (CAPMI_A_KMAJOR,
+ * lda % 4 == 0, or CAPMI_A_CONV_NHWC, Cin % 32 == 0, with the optional BN-apply + ReLU prologue);
+ * B is the fp32 weight W[N][K] pre-split by capmi_split3_bf16 into three bf16 planes [3][N][ldb]
+ * (ldb % 8 == 0, ldb >= K; the B pointer is plane 0); K % 32 == 0; C, bias, alpha/beta, relu,
+ * output row remap and `stats` as capmi_gemm; no ksplit. Each operand is split exactly into three
+ * bf16 terms and the six cross products above 2^-23 |a||b| are accumulated in fp32 on
+ * v_mfma_f32_32x32x16_bf16 (the dropped three are below the fp32 rounding level). Tile 128x128
+ * (128x64 for CAPMI_TILE_128x64 / N <= 64), 512 threads, one workgroup per CU; stream-K as
+ * capmi_gemm_sk. */
+#define CAPMI_GEMM_X3 4
+/* CAPMI_GEMM_X3P (alone): as CAPMI_GEMM_X3 with A pre-split too: the A pointer is plane 0 of three
+ * bf16 planes (dense [3][M][lda], lda % 8 == 0; or the NHWC conv input [3][N*H*W][Cin], Cin % 32 ==
+ * 0, from capmi_bn_relu_split3 / capmi_split3_bf16); no prologue. Tile 256x128, 512 threads, LDS-DMA
+ * staging, one workgroup per CU; stream-K as capmi_gemm_sk. */
+#define CAPMI_GEMM_X3P 8
 int capmi_gemm_sk_ex(const capmi_gemm_problem* problem, int amode, int bmode, int tile, int flags, void* workspace,
                      long long ws_bytes, void* stream);
 /* the launch capmi_gemm_sk_ex(..., flags, ...) would make (no GPU work): tile bm x bn, stream_k 0/1,
@@ -341,6 +356,15 @@ int capmi_adam_clamp_f64(double* p, const double* g, double* m, double* v, long 
 /* embedding gradient: demb[caps[b*L+t]][:] += dx[t][b][0:M] (atomic; fp32 or fp64 table) */
 int capmi_embed_scatter_add(const float* dx, long long ld_dx, const long long* caps, int B, int L,
                             int T, const int* bt, int M, void* demb, int demb_is_f64, void* stream);
+
+/* in[n] fp32 -> out[3][n] bf16 (n % 4 == 0): the exact split in = out[0] + out[1] + out[2], each
+ * term the RNE bf16 rounding of the remainder (B operand of CAPMI_GEMM_X3). */
+int capmi_split3_bf16(const float* in, long long n, void* out, void* stream);
+
+/* x = relu(y * scale[c] + shift[c]) of y [rows][C] fp32 (scale = shift = NULL: x = y), written as
+ * the three bf16 split planes out[3][rows * C] (the CAPMI_GEMM_X3P A operand); C % 4 == 0. */
+int capmi_bn_relu_split3(const float* y, const float* scale, const float* shift, long long rows, int C, void* out,
+                         void* stream);
 
 /* ---- kernel timing inside HIP graphs (bench.py's roofline) -------------------------------
  * Timing events whose record becomes a graph node when `stream` is being captured

@@ -1,0 +1,199 @@
+"""GPU: the fp32-accurate three-term bf16 split GEMM (CAPMI_GEMM_X3, csrc/gemm_x3.hip).
+
+The split a = a0 + a1 + a2 (bf16 terms) is exact; the GEMM keeps the six cross products above
+2^-23 |a||b| and accumulates in fp32. Tolerance: the fp32 kernel's (tests/test_gpu_gemm.py),
+|C - C64| <= 4e-6 (|A||B|)_ij + 1e-6 element-wise against the fp64 product of the same fp32
+operands; and the relative L2 error may not exceed 2x the native fp32 MFMA kernel's on the same
+problem (it is measured, not assumed, to be of the same size)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _K():
+    from capmi import kernels as K
+    return K
+
+
+def rnd(*shape, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(*shape, generator=g, dtype=torch.float64) * 2 - 1).float()
+
+
+def split3(w):
+    K = _K()
+    out = torch.empty(3 * w.numel(), device=DEV, dtype=torch.bfloat16)
+    K.split3_bf16(w.contiguous(), out)
+    return out
+
+
+def _errs(C, ref, ref_abs):
+    err = (C.double().cpu() - ref).abs()
+    tol = 4e-6 * ref_abs + 1e-6
+    return float((err / tol).max()), float((C.double().cpu() - ref).norm() / ref.norm())
+
+
+def test_split3_exact():
+    """in = h0 + h1 + h2 exactly (fp64 sum of the bf16 terms), over a wide exponent range."""
+    g = torch.Generator().manual_seed(5)
+    x = (torch.randn(1 << 16, generator=g) * torch.exp2(torch.randint(-60, 60, (1 << 16,), generator=g).float()))
+    # exact for |x| below the bf16 maximum (3.39e38) and above 2^-110 (below it the low terms
+    # fall into the subnormal range: an absolute error under 2^-126, far beneath any activation)
+    x[:8] = torch.tensor([0.0, -0.0, 1.0, -1.0, 1e30, -3e-30, 1.0000001, 0.33333334])
+    h = split3(x.to(DEV)).cpu().view(3, -1).double()
+    assert torch.equal(h.sum(0), x.double())
+    assert bool((h[1].abs() <= h[0].abs() * 2 ** -8).all()) and bool((h[2].abs() <= h[0].abs() * 2 ** -16).all())
+
+
+@pytest.mark.parametrize("M,N,Kd,tile", [(300, 200, 96, 3), (12544, 512, 2048, 3), (1536, 8100, 512, 3),
+                                         (129, 64, 64, 3), (1, 7, 32, 3), (4096, 1024, 256, 2), (700, 128, 4608, 3)])
+def test_x3_dense(M, N, Kd, tile):
+    K = _K()
+    X, W, b = rnd(M, Kd, seed=1), rnd(N, Kd, seed=2), rnd(N, seed=3)
+    Xd, Wd = X.to(DEV), W.to(DEV)
+    ws = K.gemm_workspace(DEV)
+    C = torch.full((M, N), float("nan"), device=DEV)
+    K.gemm_x3(K.problem(M, N, Kd, Xd, Kd, split3(Wd), Kd, C, N, bias=b.to(DEV)), 0, ws, tile)
+    Cn = torch.empty(M, N, device=DEV)
+    K.gemm_sk(K.problem(M, N, Kd, Xd, Kd, Wd, Kd, Cn, N, bias=b.to(DEV)), 0, ws)
+    torch.cuda.synchronize()
+    K.sk_check([ws])
+    ref = X.double() @ W.double().T + b.double()
+    ref_abs = X.double().abs() @ W.double().abs().T + b.double().abs()
+    r3, e3 = _errs(C, ref, ref_abs)
+    rn, en = _errs(Cn, ref, ref_abs)
+    assert r3 <= 1.0, (r3, e3, rn, en)
+    assert e3 <= 2 * en + 1e-9, (e3, en)
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,k,stride,pro", [
+    (4, 14, 256, 256, 3, 1, True), (4, 28, 128, 128, 3, 2, True), (2, 56, 64, 64, 3, 1, True),
+    (3, 14, 1024, 256, 1, 1, False), (2, 28, 256, 512, 1, 2, False), (2, 7, 512, 2048, 1, 1, True),
+    (64, 14, 256, 256, 3, 1, True)])
+def test_x3_conv_prologue_stats(N, H, Cin, Cout, k, stride, pro):
+    """Implicit-GEMM conv on NHWC with the BN-apply + ReLU prologue (input relu(x*s+b), padding
+    zeros AFTER it) and the per-64-row-slice BN statistics of the stored output."""
+    K = _K()
+    pad = k // 2
+    Ho = (H + 2 * pad - k) // stride + 1
+    x = rnd(N, H, H, Cin, seed=4)
+    w = rnd(Cout, k, k, Cin, seed=5) * (2.0 / (k * k * Cin)) ** 0.5
+    s, b = rnd(Cin, seed=6) + 1.0, rnd(Cin, seed=7)
+    xin = torch.relu(x * s + b) if pro else x
+    rows = N * Ho * Ho
+    Kd = k * k * Cin
+    ws = K.gemm_workspace(DEV)
+    stats = torch.zeros(2 * K.stat_tiles(rows) * Cout, device=DEV)
+    out = torch.empty(rows, Cout, device=DEV)
+    geo = dict(N=N, H=H, W=H, Cin=Cin, KH=k, KW=k, stride=stride, pad=pad, Ho=Ho, Wo=Ho)
+    wd = w.reshape(Cout, Kd).to(DEV)
+    prob = K.problem(rows, Cout, Kd, x.to(DEV), 0, split3(wd), Kd, out, Cout, conv=geo, stats=stats,
+                     in_scale=s.to(DEV) if pro else None, in_shift=b.to(DEV) if pro else None)
+    K.gemm_x3(prob, 2, ws)
+    torch.cuda.synchronize()
+    K.sk_check([ws])
+    xi = xin.double().permute(0, 3, 1, 2)
+    wt = w.double().permute(0, 3, 1, 2)
+    ref = F.conv2d(xi, wt, stride=stride, padding=pad).permute(0, 2, 3, 1).reshape(rows, Cout)
+    ref_abs = F.conv2d(xi.abs(), wt.abs(), stride=stride, padding=pad).permute(0, 2, 3, 1).reshape(rows, Cout)
+    r3, _ = _errs(out, ref, ref_abs)
+    assert r3 <= 1.0, r3
+    o = out.double().cpu()
+    st = stats.double().cpu()[: 2 * ((rows + 63) // 64) * Cout].view(-1, Cout, 2)
+    torch.testing.assert_close(st[..., 0].sum(0), o.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(st[..., 1].sum(0), (o * o).sum(0), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("B,H", [(2, 224), (64, 224)])
+def test_encoder_x3_matches_oracle(B, H):
+    """The whole train-mode encoder with every eligible conv on the x3 GEMM: within 2x the fp32 CPU
+    path's own error against fp64 (the rule of tests/test_gpu_encoder.py)."""
+    import os
+    import gen
+    from helpers import rel_err, t
+    from models.encoder import EncoderAttention
+    from oracle.resnet_ref import build_resnet101, encoder_attention_forward
+    names = ["conv1", "bn1", "relu", "maxpool", "layer1", "layer2", "layer3", "layer4"]
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    torch.set_num_threads(int(env) if env.isdigit() and int(env) > 0 else 8)
+    seed = 77
+    params = gen.resnet101_params(seed)
+    enc = EncoderAttention()
+    sd = enc.state_dict()
+    for k_, v in params.items():
+        head, rest = k_.split(".", 1)
+        sd[f"resnet.{names.index(head)}.{rest}"] = t(v).clone()
+    enc.load_state_dict(sd)
+    enc = enc.to(DEV).train()
+    enc.set_compute_precision("fp32-x3")
+    x = gen.images(seed, B, H, H)
+    with torch.no_grad():
+        y = enc(t(x, DEV)).cpu()
+    r32, r64 = build_resnet101(params).train(), build_resnet101(params).double().train()
+    with torch.no_grad():
+        y32 = encoder_attention_forward(r32, t(x))
+        y64 = encoder_attention_forward(r64, t(x).double())
+    e_gpu, e_cpu = rel_err(y, y64), rel_err(y32, y64)
+    assert e_gpu <= 2 * e_cpu + 1e-6, (e_gpu, e_cpu)
+
+
+def test_bn_relu_split3_exact():
+    """The split planes of relu(y*s+b) sum exactly (fp64) to the fp32 value torch computes."""
+    K = _K()
+    rows, C = 1000, 96
+    y, s, b = rnd(rows, C, seed=8) * 3, rnd(C, seed=9) + 1.5, rnd(C, seed=10)
+    out = torch.empty(3 * rows * C, device=DEV, dtype=torch.bfloat16)
+    K.bn_relu_split3(y.to(DEV), s.to(DEV), b.to(DEV), rows, C, out)
+    torch.cuda.synchronize()
+    h = out.cpu().view(3, rows, C).double()
+    want = torch.relu(torch.addcmul(b, y, s))  # fma order: y*s + b, rounded once (as fmaf)
+    assert torch.equal(h.sum(0), want.double()) or float((h.sum(0) - want.double()).abs().max()) <= \
+        float(want.abs().max()) * 2 ** -23
+    out2 = torch.empty(3 * rows * C, device=DEV, dtype=torch.bfloat16)
+    K.bn_relu_split3(y.to(DEV), None, None, rows, C, out2)
+    torch.cuda.synchronize()
+    assert torch.equal(out2.cpu().view(3, rows, C).double().sum(0), y.double())
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,k,stride,pro", [
+    (4, 14, 256, 256, 3, 1, True), (4, 28, 128, 128, 3, 2, True), (2, 56, 64, 256, 1, 1, True),
+    (3, 14, 256, 1024, 1, 1, True), (2, 7, 512, 2048, 1, 1, False), (64, 14, 256, 256, 3, 1, True),
+    (1, 9, 64, 128, 3, 1, True), (64, 7, 512, 512, 3, 1, True)])
+def test_x3p_conv_stats(N, H, Cin, Cout, k, stride, pro):
+    """Both operands pre-split (CAPMI_GEMM_X3P): the conv of relu(x*s+b) (split pass) vs fp64, and
+    the BN statistics; ragged M (tiles of 256 rows), stream-K and data-parallel grids."""
+    K = _K()
+    pad = k // 2
+    Ho = (H + 2 * pad - k) // stride + 1
+    x = rnd(N, H, H, Cin, seed=11)
+    w = rnd(Cout, k, k, Cin, seed=12) * (2.0 / (k * k * Cin)) ** 0.5
+    s, b = rnd(Cin, seed=13) + 1.0, rnd(Cin, seed=14)
+    xin = torch.relu(torch.addcmul(b, x, s)) if pro else x
+    rows, Kd = N * Ho * Ho, k * k * Cin
+    ws = K.gemm_workspace(DEV)
+    xp = torch.empty(3 * x.numel(), device=DEV, dtype=torch.bfloat16)
+    K.bn_relu_split3(x.to(DEV), s.to(DEV) if pro else None, b.to(DEV) if pro else None, N * H * H, Cin, xp)
+    stats = torch.zeros(2 * K.stat_tiles(rows) * Cout, device=DEV)
+    out = torch.full((rows, Cout), float("nan"), device=DEV)
+    w3 = split3(w.reshape(Cout, Kd).to(DEV))
+    if k == 1 and stride == 1:
+        prob, mode = K.problem(rows, Cout, Kd, xp, Cin, w3, Kd, out, Cout, stats=stats), 0
+    else:
+        geo = dict(N=N, H=H, W=H, Cin=Cin, KH=k, KW=k, stride=stride, pad=pad, Ho=Ho, Wo=Ho)
+        prob, mode = K.problem(rows, Cout, Kd, xp, 0, w3, Kd, out, Cout, conv=geo, stats=stats), 2
+    K.gemm_x3p(prob, mode, ws)
+    torch.cuda.synchronize()
+    K.sk_check([ws])
+    xi = xin.double().permute(0, 3, 1, 2)
+    wt = w.double().permute(0, 3, 1, 2)
+    ref = F.conv2d(xi, wt, stride=stride, padding=pad).permute(0, 2, 3, 1).reshape(rows, Cout)
+    ref_abs = F.conv2d(xi.abs(), wt.abs(), stride=stride, padding=pad).permute(0, 2, 3, 1).reshape(rows, Cout)
+    r3, _ = _errs(out, ref, ref_abs)
+    assert r3 <= 1.0, r3
+    o = out.double().cpu()
+    st = stats.double().cpu()[: 2 * ((rows + 63) // 64) * Cout].view(-1, Cout, 2)
+    torch.testing.assert_close(st[..., 0].sum(0), o.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(st[..., 1].sum(0), (o * o).sum(0), rtol=1e-5, atol=1e-3)

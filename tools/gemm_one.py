@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--bf16", action="store_true")
     ap.add_argument("--bf16io", action="store_true", help="bf16 activations/weights/output (CAPMI_GEMM_BF16_IO)")
     ap.add_argument("--nopro", action="store_true", help="drop the BN-apply+ReLU prologue (1x1: dense A)")
+    ap.add_argument("--x3", action="store_true", help="fp32-accurate three-term bf16 split GEMM (CAPMI_GEMM_X3)")
+    ap.add_argument("--x3p", action="store_true", help="x3 with the A operand pre-split too (CAPMI_GEMM_X3P)")
     a = ap.parse_args()
     dev = "cuda"
     ci, H, W, co, k, pro, *st = SHAPES[a.shape]
@@ -66,6 +68,23 @@ def main():
             prob = K.problem_bf16(M, co, Kd, xb, 0, wb, Kd, yb, co, stats=stats, conv=geo)
             mode = CAPMI_A_CONV_NHWC
         run = lambda: K.gemm_bf16(prob, mode, ws, a.tile)  # noqa: E731
+    elif a.x3p:
+        w3 = torch.empty(3 * w.numel(), device=dev, dtype=torch.bfloat16)
+        K.split3_bf16(w, w3)
+        xp = torch.empty(3 * x.numel(), device=dev, dtype=torch.bfloat16)
+        K.bn_relu_split3(x, sc if pro else None, sh if pro else None, x.numel() // ci, ci, xp)
+        if k == 1 and stride == 1:
+            prob, mode = K.problem(M, co, Kd, xp, ci, w3, Kd, y, co, stats=stats), CAPMI_A_KMAJOR
+        else:
+            prob, mode = K.problem(M, co, Kd, xp, 0, w3, Kd, y, co, conv=geo, stats=stats), CAPMI_A_CONV_NHWC
+        print("x3p kernel:", K.gemm_x3p_kernel_name(prob, mode))
+        run = lambda: K.gemm_x3p(prob, mode, ws)  # noqa: E731
+    elif a.x3:
+        w3 = torch.empty(3 * w.numel(), device=dev, dtype=torch.bfloat16)
+        K.split3_bf16(w, w3)
+        prob.B = w3.data_ptr()
+        print("x3 kernel:", K.gemm_x3_kernel_name(prob, mode, a.tile))
+        run = lambda: K.gemm_x3(prob, mode, ws, a.tile)  # noqa: E731
     else:
         print("plan (bm, bn, stream_k, generic, threads):", K.gemm_sk_plan(prob, mode, a.tile, bf16=a.bf16, threads=True))
         run = lambda: K.gemm_sk(prob, mode, ws, a.tile, bf16=a.bf16)  # noqa: E731
