@@ -76,7 +76,14 @@ def test_gemm_sk_plan_on_host():
     assert rc == 0 and (bm, bn, generic, nt) == (128, 128, 0, 512)
     assert plan(64)[1][4] == 256
     assert plan(256, flags=1)[1][4] == 256
-    assert plan(256, flags=4)[0] == 1001
+    assert plan(256, flags=16)[0] == 1001  # unknown flag
+    # CAPMI_GEMM_X3 (4): 128x128 tiles, 512 threads; CAPMI_GEMM_X3P (8): 256x128
+    rc, (bm, bn, sk, generic, nt) = plan(256, flags=4)
+    assert rc == 0 and (bm, bn, generic, nt) == (128, 128, 0, 512)
+    assert plan(64, flags=4)[1][1] == 64
+    rc, (bm, bn, sk, generic, nt) = plan(256, flags=8)
+    assert rc == 0 and (bm, bn, generic, nt) == (256, 128, 0, 512) and sk == 1  # 98 tiles < 256 CUs
+    assert plan(256, flags=8, Cin=20)[0] == 1001  # Cin % 32 != 0
 
     def wgrad_plan(Cout, Cin, k):
         # dW[Cout, (kh, kw, ci)] over k = 64*14*14 output pixels (A_MMAJOR x B_CONV_NHWC)
