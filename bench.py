@@ -75,6 +75,10 @@ def parse():
                          "bert_attention = config 5 (768-d word features instead of the table, synthetic); "
                          "baseline_cpu = config 1 (baseline LSTM captioner, batch 4, CPU, gloo)")
     ap.add_argument("--fp32", action="store_true", help="bert_attention: keep the encoder convs fp32")
+    ap.add_argument("--conv", default="x3", choices=["x3", "native"],
+                    help="fp32 configs: x3 = fp32-accurate convs on the bf16 matrix cores (operands split exactly "
+                         "into three bf16 terms, six cross products accumulated in fp32; gemm_x3*.hip), native = "
+                         "v_mfma_f32_32x32x2_f32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="cpu_baseline: keep stepping the oracle at the full batch until this much time "
@@ -392,6 +396,8 @@ def main():
         decoder.bert_embedder = SyntheticBertEmbedder(args.vocab, 768, device=dev)
         if not args.fp32:
             encoder.set_compute_precision("bf16")  # config 5 is the bf16 config
+    if not encoder._runner.bf16 and args.conv == "x3":
+        encoder.set_compute_precision("fp32-x3")
     if ft:
         # synthetic GloVe-300 table, fp64 like load_glove_vectors (embed.py:64-68, Q7)
         g = torch.Generator().manual_seed(300)
@@ -467,6 +473,10 @@ def main():
         fam_ms = sum(v[2] for v in per.values())
         per_img = sum(v[1] for v in per.values()) / args.steps / B
         peak = BF16_MFMA_PEAK_TF if encoder._runner.bf16 else FP32_MFMA_PEAK_TF
+        if "x3" in key:
+            # the x3 kernels run six bf16 MFMAs per fp32 multiply-add: their matrix-core bound for
+            # fp32 arithmetic is the dense bf16 peak / 6 (417 TF/s)
+            peak = round(BF16_MFMA_PEAK_TF / 6, 1)
         roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(ach / peak, 4), "traffic": _traffic(key, args.config),
                 "kernel": key,
@@ -488,6 +498,11 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16" if encoder._runner.bf16 else "fp32",
+            "conv_arithmetic": ("bf16 MFMA, fp32 accumulate" if encoder._runner.bf16 else
+                                "fp32-accurate x3: each fp32 operand split exactly into three bf16 terms, the six cross "
+                                "products above 2^-23|a||b| accumulated in fp32 on bf16 MFMA (error vs fp64 <= the "
+                                "fp32-MFMA kernel's, tests/test_gpu_x3.py)" if encoder._runner.x3 else
+                                "fp32 MFMA (v_mfma_f32_32x32x2_f32)"),
             "data": "synthetic (resident in HBM; random-init weights, torch.manual_seed(0))",
             "config": {"workload": ("'glove_att' decoder (GloVe-300 fp64 embedding, fine-tuned) + ResNet-101 "
                                     "encoder fine-tuned (layer2-4, BN train mode), one training step per batch")

@@ -770,7 +770,7 @@ int gemm_x3p(const capmi_gemm_problem* prob, int amode, int bmode, void* workspa
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
   const int cus = cu_count();
   const long long slots = cus;
-  a.sk_nkt = prob->K / 32;
+  a.sk_nkt = prob->K / kX3pBK;  // k-tiles of the x3p kernel
   a.sk_dp_tiles = sk_hybrid() && total >= 2 * slots ? (int)((total / slots - 1) * slots) : 0;
   a.sk_units = (total - a.sk_dp_tiles) * a.sk_nkt;
   a.sk_workers = (int)std::min<long long>(slots, a.sk_units);

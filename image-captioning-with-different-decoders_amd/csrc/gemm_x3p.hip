@@ -6,27 +6,27 @@
 // work that often), the weights once per weight version (capmi_split3_bf16).
 //
 // Structure: 256 x 128 tile, 512 threads = 8 waves as 4 (M) x 2 (N), wave tile 64 x 64 (2 x 2
-// MFMA tiles: per 16-k k-tile 6 + 6 ds_read_b128 feed 24 MFMAs), BK = 16. Staging is LDS-DMA
-// (buffer_load_dwordx4 ... lds, no VGPRs, no ds_write): one wave-instruction moves 32 rows x 32 B
+// MFMA tiles: per 16-k chunk 6 + 6 ds_read_b128 feed 24 MFMAs), BK = 32. Staging is LDS-DMA
+// (buffer_load_dwordx4 ... lds, no VGPRs, no ds_write): one wave-instruction moves 16 rows x 64 B
 // of one plane into a lane-linear 1 KiB LDS block; the 16-B chunk of row r in slot s holds the
-// logical k-chunk s ^ ((r >> 3) & 1) (the swizzle goes on the per-lane SOURCE address), so the
+// logical k-chunk s ^ ((r >> 2) & 3) (the swizzle goes on the per-lane SOURCE address), so the
 // 16-lane groups of ds_read_b128 hit 64 distinct banks. Padding taps and rows past M read zeros
-// (buffer offsets past the descriptor's range). Three LDS buffers (3 x 36 KiB, one array): the DMA
-// of k-tile t+2 is issued right after the barrier that opens tile t, so every tile's DMA has two
-// tiles of MFMA work to land; the opening wait is a counted vmcnt (the next tile's DMA stays in
-// flight) and the barrier a raw s_barrier (__syncthreads would drain it). Epilogue (fp32 C,
-// alpha/bias/beta/relu, per-64-row BN statistics: a wave's 64 rows are one slice) and the stream-K
-// / hybrid schedule with the write-through hand-off are those of gemm_nt.hip.
+// (buffer offsets past the descriptor's range). LDS double buffer (2 x 72 KiB, one array), one
+// barrier per k-tile: the DMA of tile t+1 is issued before tile t is multiplied and retired by
+// `vmcnt(0)` + the barrier that ends tile t. (Measured alternative: BK = 16 with three buffers and
+// the DMA two tiles ahead behind a counted vmcnt -- the extra barrier per 32 k cost more than the
+// deeper prefetch gained: layer3 3x3 101 us vs 85.) Epilogue (fp32 C, alpha/bias/beta/relu,
+// per-64-row BN statistics: a wave's 64 rows are one slice) and the stream-K / hybrid schedule with
+// the write-through hand-off are those of gemm_nt.hip.
 #include "gemm_args.h"
 
 namespace {
 
-constexpr int PBM = 256, PBN = 128, PBK = 16, PNT = 512;
-constexpr int PROWB = PBK * 2;                     // bytes per LDS row (16 bf16)
-constexpr int PA_BYTES = 3 * PBM * PROWB;          // 24 KiB: A planes of one k-tile
-constexpr int PB_BYTES = 3 * PBN * PROWB;          // 12 KiB
-constexpr int PBUF = PA_BYTES + PB_BYTES;          // 36 KiB per buffer
-constexpr int PNBUF = 3;
+constexpr int PBM = 256, PBN = 128, PBK = kX3pBK, PNT = 512;
+constexpr int PROWB = PBK * 2;                     // bytes per LDS row (32 bf16)
+constexpr int PA_BYTES = 3 * PBM * PROWB;          // 48 KiB: A planes of one k-tile
+constexpr int PB_BYTES = 3 * PBN * PROWB;          // 24 KiB
+constexpr int PBUF = PA_BYTES + PB_BYTES;          // 72 KiB per buffer
 typedef unsigned u32x4_p __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_p __attribute__((ext_vector_type(8)));
 constexpr unsigned kOOBp = 0x80000000u;
@@ -40,13 +40,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_p(const void* p, unsigned
 template <int AMODE, bool SK>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
 gemm_x3p_kernel(const GemmArgs args) {
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[PNBUF * PBUF];
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * PBUF];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases in SGPRs
   const int wm0 = (wid >> 1) * 64, wn0 = (wid & 1) * 64;
   const int lr = lane & 31, lh = lane >> 5;
-  // DMA lane geometry: row (lane >> 1) of a 32-row block, slot (lane & 1)
-  const int drow = lane >> 1, dslot = lane & 1;
+  // DMA lane geometry: row (lane >> 2) of a 16-row block, slot (lane & 3)
+  const int drow = lane >> 2, dslot = lane & 3;
 
   f32x16 acc[2][2];
 
@@ -65,27 +66,31 @@ gemm_x3p_kernel(const GemmArgs args) {
     const long long planeB = (long long)N * P.ldb;
     const auto ra = rsrc_p(P.A, (unsigned)(3 * planeA * 2));
     const auto rb = rsrc_p(P.B, (unsigned)(3 * planeB * 2));
-    // this lane's A row (row block wid: rows 32 wid ..) and, for waves 0-3, its B row
-    const int ar = wid * 32 + drow;
-    const int a_ch = dslot ^ ((ar >> 3) & 1);
-    const int arow = m0 + ar;
-    const bool a_ok = arow < M;
-    unsigned a_base;  // dense: byte offset of (row, chunk) in plane 0; conv: pixel index of (n, 0, 0)
-    int a_ih0 = 0, a_iw0 = 0;
-    if (AMODE == 0) {
-      a_base = (unsigned)(((long long)(a_ok ? arow : 0) * P.lda + a_ch * 8) * 2);
-    } else {
-      const int hw = P.cHo * P.cWo;
-      const int rr = a_ok ? arow : 0;
-      const int n = rr / hw, rem = rr - n * hw;
-      const int oh = rem / P.cWo, ow = rem - oh * P.cWo;
-      a_ih0 = oh * P.cStride - P.cPad;
-      a_iw0 = ow * P.cStride - P.cPad;
-      a_base = (unsigned)(n * cH * cW);
+    // this lane's two A rows (row blocks 2 wid, 2 wid + 1) and one B row (row block wid)
+    unsigned a_base[2];  // dense: byte offset of (row, chunk) in plane 0; conv: pixel index of (n, 0, 0)
+    int a_ih0[2], a_iw0[2], a_ch[2];
+    bool a_ok[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (2 * wid + i) * 16 + drow;
+      const int row = m0 + r;
+      a_ch[i] = dslot ^ ((r >> 2) & 3);
+      a_ok[i] = row < M;
+      if (AMODE == 0) {
+        a_base[i] = (unsigned)(((long long)(a_ok[i] ? row : 0) * P.lda + a_ch[i] * 8) * 2);
+        a_ih0[i] = a_iw0[i] = 0;
+      } else {
+        const int hw = P.cHo * P.cWo;
+        const int rr = a_ok[i] ? row : 0;
+        const int n = rr / hw, rem = rr - n * hw;
+        const int oh = rem / P.cWo, ow = rem - oh * P.cWo;
+        a_ih0[i] = oh * P.cStride - P.cPad;
+        a_iw0[i] = ow * P.cStride - P.cPad;
+        a_base[i] = (unsigned)(n * cH * cW);
+      }
     }
-    const bool bw = wid < 4;  // waves 0-3 also stage B (row block wid)
-    const int br = (wid & 3) * 32 + drow;
-    const int b_ch = dslot ^ ((br >> 3) & 1);
+    const int br = wid * 16 + drow;
+    const int b_ch = dslot ^ ((br >> 2) & 3);
     const bool b_ok = n0 + br < N;
     const unsigned b_base = (unsigned)(((long long)(b_ok ? n0 + br : 0) * P.ldb + b_ch * 8) * 2);
     int c_ci = 0, c_kh = 0, c_kw = 0;
@@ -97,17 +102,23 @@ gemm_x3p_kernel(const GemmArgs args) {
     }
     const unsigned pA2 = (unsigned)(planeA * 2), pB2 = (unsigned)(planeB * 2);
 
-    // DMA of k-tile kt into buffer buf: 3 A (+ 3 B for waves 0-3) wave-instructions per wave
+    // DMA of k-tile kt into buffer buf: 6 A + 3 B wave-instructions per wave
     auto issue = [&](int kt, int buf) {
       const int k = k_lo + kt * PBK;
       const bool kok = k < k_hi;
-      unsigned aoff;
-      if (AMODE == 0) {
-        aoff = a_ok && kok ? a_base + (unsigned)k * 2 : kOOBp;
-      } else {
-        const int ih = a_ih0 + c_kh, iw = a_iw0 + c_kw;
-        const bool ok = a_ok && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
-        aoff = ok ? ((a_base + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + a_ch * 8)) * 2u : kOOBp;
+      unsigned aoff[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if (AMODE == 0) {
+          aoff[i] = a_ok[i] && kok ? a_base[i] + (unsigned)k * 2 : kOOBp;
+        } else {
+          const int ih = a_ih0[i] + c_kh, iw = a_iw0[i] + c_kw;
+          const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
+          aoff[i] = ok ? ((a_base[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + a_ch[i] * 8)) * 2u
+                       : kOOBp;
+        }
+      }
+      if (AMODE == 2) {
         c_ci += PBK;
         if (c_ci >= cCin) {
           c_ci = 0;
@@ -120,71 +131,67 @@ gemm_x3p_kernel(const GemmArgs args) {
       unsigned char* base = lds + buf * PBUF;
 #pragma unroll
       for (int p = 0; p < 3; ++p)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(base + p * PBM * PROWB + wid * 32 * PROWB), 16,
-                                                 aoff == kOOBp ? kOOBp : aoff + p * pA2, 0, 0, 0);
-      if (bw) {
-        const unsigned boff = b_ok && kok ? b_base + (unsigned)k * 2 : kOOBp;
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int i = 0; i < 2; ++i)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * 32 * PROWB), 16,
-              boff == kOOBp ? kOOBp : boff + p * pB2, 0, 0, 0);
-      }
+              ra, (lds_ptr_t)(base + p * PBM * PROWB + (2 * wid + i) * 16 * PROWB), 16,
+              aoff[i] == kOOBp ? kOOBp : aoff[i] + p * pA2, 0, 0, 0);
+      const unsigned boff = b_ok && kok ? b_base + (unsigned)k * 2 : kOOBp;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * 16 * PROWB), 16,
+            boff == kOOBp ? kOOBp : boff + p * pB2, 0, 0, 0);
     };
     auto compute = [&](int buf) {
       const unsigned char* A_ = lds + buf * PBUF;
       const unsigned char* B_ = A_ + PA_BYTES;
-      bf16x8_p a[2][3], b[2][3];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int r = wm0 + 32 * i + lr;
-        const int o = r * PROWB + ((lh ^ ((r >> 3) & 1)) << 4);
+      for (int g = 0; g < PBK / 16; ++g) {
+        const int c = 2 * g + lh;  // logical 16-B chunk (8 k) this lane reads
+        bf16x8_p a[2][3], b[2][3];
 #pragma unroll
-        for (int p = 0; p < 3; ++p) a[i][p] = *reinterpret_cast<const bf16x8_p*>(A_ + p * PBM * PROWB + o);
-      }
+        for (int i = 0; i < 2; ++i) {
+          const int r = wm0 + 32 * i + lr;
+          const int o = r * PROWB + ((c ^ ((r >> 2) & 3)) << 4);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int r = wn0 + 32 * j + lr;
-        const int o = r * PROWB + ((lh ^ ((r >> 3) & 1)) << 4);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) b[j][p] = *reinterpret_cast<const bf16x8_p*>(B_ + p * PBN * PROWB + o);
-      }
-      // smallest terms first into each fp32 accumulator
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[j][0], acc[i][j], 0, 0, 0);
+          for (int p = 0; p < 3; ++p) a[i][p] = *reinterpret_cast<const bf16x8_p*>(A_ + p * PBM * PROWB + o);
         }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
         for (int j = 0; j < 2; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][1], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][0], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][0], acc[i][j], 0, 0, 0);
+          const int r = wn0 + 32 * j + lr;
+          const int o = r * PROWB + ((c ^ ((r >> 2) & 3)) << 4);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) b[j][p] = *reinterpret_cast<const bf16x8_p*>(B_ + p * PBN * PROWB + o);
         }
+        // smallest terms first into each fp32 accumulator
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[j][0], acc[i][j], 0, 0, 0);
+          }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][0], acc[i][j], 0, 0, 0);
+          }
+      }
     };
     issue(0, 0);
-    issue(1, 1);
-    int cur = 0, nxt = 2;  // buffer of tile kt, buffer tile kt + 2 goes to
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     for (int kt = 0; kt < nkt; ++kt) {
-      // tile kt has landed when at most one tile's DMA (kt + 1) is still outstanding
-      if (bw)
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt landed; tile kt - 1 fully read
-      issue(kt + 2, nxt);            // past the end: OOB loads (zeros) into the free buffer
-      compute(cur);
-      cur = cur == 2 ? 0 : cur + 1;
-      nxt = nxt == 2 ? 0 : nxt + 1;
+      issue(kt + 1, (kt + 1) & 1);  // past the end: OOB loads (zeros) into the idle buffer
+      compute(kt & 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
     }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // the buffers are free for the next tile (stream-K)
   };
 
   auto epilogue = [&](const capmi_gemm_problem& P, int tm, int tn) {

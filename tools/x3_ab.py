@@ -64,7 +64,7 @@ def main():
         p3 = K.problem(rows, Cout, Kd, x, Cin if dense else 0, w3, Kd, out, Cout, **kw)
         res = {}
         arms = [("native", lambda: K.gemm_sk(pn, mode, ws)), ("x3", lambda: K.gemm_x3(p3, mode, ws))]
-        if pro and Cout >= 128:  # the encoder's x3p path: split pass + pre-split GEMM
+        if pro and Cout >= 128 and Cin % 32 == 0:  # x3p candidates: split pass + pre-split GEMM
             xp = torch.empty(3 * x.numel(), device=dev, dtype=torch.bfloat16)
             if k == 1 and st == 1:
                 pp, mp = K.problem(rows, Cout, Kd, xp, Cin, w3, Kd, out, Cout, stats=stats), 0
