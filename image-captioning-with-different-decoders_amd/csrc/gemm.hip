@@ -748,6 +748,13 @@ int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
   a.p[0] = p;
   a.tiles_m[0] = (int)cdiv(p.M, 256);
   a.tiles_n[0] = (int)cdiv(p.N, 128);
+  {  // A/B knob: CAPMI_X3P_ORDER=col walks tiles column-major (an XCD's contiguous range shares B)
+    static const int col = [] {
+      const char* e = getenv("CAPMI_X3P_ORDER");
+      return e && e[0] == 'c' ? 1 : 0;
+    }();
+    a.tile_cols_first = col;
+  }
   total = (long long)a.tiles_m[0] * a.tiles_n[0];
   a.tiles_begin[1] = (int)total;
   const long long slots = cu_count();

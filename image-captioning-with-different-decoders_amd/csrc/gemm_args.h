@@ -19,6 +19,7 @@ struct GemmArgs {
   int sk_groups;         // 1, or 8: tiles and workers split into blockIdx%8 groups (XCD-local)
   float* sk_part;        // [workers][BM*BN] parked k-prefix partials
   int* sk_flags;         // [workers + 1], zero between launches; [workers] = spin-timeout flag
+  int tile_cols_first;   // x3p: tile t = (tm, tn) as tm = t % tiles_m, tn = t / tiles_m (column-major)
 };
 
 __device__ __forceinline__ long long remap(long long r, long long r1, long long ld, long long s2) {

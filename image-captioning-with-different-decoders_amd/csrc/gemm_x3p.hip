@@ -64,8 +64,12 @@ gemm_x3p_kernel(const GemmArgs args) {
     const int cH = P.cH, cW = P.cW, cCin = P.cCin, cKW = P.cKW;
     const long long planeA = AMODE == 2 ? (long long)P.cN * cH * cW * cCin : (long long)M * P.lda;
     const long long planeB = (long long)N * P.ldb;
-    const auto ra = rsrc_p(P.A, (unsigned)(3 * planeA * 2));
-    const auto rb = rsrc_p(P.B, (unsigned)(3 * planeB * 2));
+#ifndef X3P_PRICE
+#define X3P_PRICE 0
+#endif
+    // X3P_PRICE (timing-only builds): 1 = A descriptor with zero records (no A traffic), 2 = B, 3 = both
+    const auto ra = rsrc_p(P.A, (X3P_PRICE & 1) ? 0u : (unsigned)(3 * planeA * 2));
+    const auto rb = rsrc_p(P.B, (X3P_PRICE & 2) ? 0u : (unsigned)(3 * planeB * 2));
     // this lane's two A rows (row blocks 2 wid, 2 wid + 1) and one B row (row block wid)
     unsigned a_base[2];  // dense: byte offset of (row, chunk) in plane 0; conv: pixel index of (n, 0, 0)
     int a_ih0[2], a_iw0[2], a_ch[2];
@@ -259,21 +263,24 @@ gemm_x3p_kernel(const GemmArgs args) {
     }
     const capmi_gemm_problem& P = args.p[0];
     const int tiles_n = args.tiles_n[0];
-    const int tn = bid % tiles_n, tm = bid / tiles_n;
+    const int tiles_m = args.tiles_m[0];
+    const int tn = args.tile_cols_first ? bid / tiles_m : bid % tiles_n;
+    const int tm = args.tile_cols_first ? bid % tiles_m : bid / tiles_n;
     mainloop(P, tm * PBM, tn * PBN, 0, P.K);
     epilogue(P, tm, tn);
     return;
   }
 
   const capmi_gemm_problem& P = args.p[0];
-  const int nkt = args.sk_nkt, tiles_n = args.tiles_n[0];
+  const int nkt = args.sk_nkt, tiles_n = args.tiles_n[0], tiles_m = args.tiles_m[0];
+  const bool cf = args.tile_cols_first != 0;
   const long long ngrp = args.sk_groups, grp = blockIdx.x % ngrp;
   const long long T = args.sk_units / nkt, G = gridDim.x / ngrp, w = blockIdx.x / ngrp;
   if (args.sk_dp_tiles > 0) {
     const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = blockIdx.x & 7;
     const int pos = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (blockIdx.x >> 3);
     for (long long t = T + pos; t < T + args.sk_dp_tiles; t += nwg) {
-      const int tm = (int)(t / tiles_n), tn = (int)(t % tiles_n);
+      const int tm = cf ? (int)(t % tiles_m) : (int)(t / tiles_n), tn = cf ? (int)(t / tiles_m) : (int)(t % tiles_n);
       mainloop(P, tm * PBM, tn * PBN, 0, P.K);
       epilogue(P, tm, tn);
     }
@@ -286,7 +293,7 @@ gemm_x3p_kernel(const GemmArgs args) {
   for (long long t = (u1 - 1) / nkt; t >= u0 / nkt; --t) {
     const long long tb = t * nkt;
     const int ks = (int)(max(u0, tb) - tb), ke = (int)(min(u1, tb + nkt) - tb);
-    const int tm = (int)(t / tiles_n), tn = (int)(t % tiles_n);
+    const int tm = cf ? (int)(t % tiles_m) : (int)(t / tiles_n), tn = cf ? (int)(t / tiles_m) : (int)(t % tiles_n);
     mainloop(P, tm * PBM, tn * PBN, ks * PBK, ke * PBK);
     if (ke < nkt) {
       const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + (long long)blockIdx.x * PART, 0,
