@@ -218,7 +218,7 @@ class DecoderCore:
 
     # ------------------------------------------------------------------ backward
     def backward(self, p, st, grads, dpred, dpred_time_major=False, dreg=None, dalphas=None,
-                 need=None, denc=None):
+                 need=None, denc=None, on_fc_grads=None):
         """Writes parameter gradients into ``grads`` (dict name->tensor, pre-allocated).
 
         dpred: gradient of the (B,T,V) predictions (batch-major), or time-major (T*B, V)
@@ -226,7 +226,9 @@ class DecoderCore:
         (the fused regulariser). dalphas: (B,T,P) gradient of the alphas output
         (generic autograd path). ``need``: names whose gradient is wanted (default: all
         present in ``grads``). ``denc``: (B,P,E) buffer receiving d(loss)/d(encoder_out) when
-        the encoder is fine-tuned (models/encoder.py:112-121), else None."""
+        the encoder is fine-tuned (models/encoder.py:112-121), else None. ``on_fc_grads``: called
+        once the fc gradients are final, before the backward-through-time loop (data parallel: their
+        all-reduce is issued there and runs beside the loop)."""
         dm, ws = st["dm"], st["ws"]
         B, T, L, P, A, D, M, V, E, X = dm.B, dm.T, dm.L, dm.P, dm.A, dm.D, dm.M, dm.V, dm.E, dm.X
         enc, bt = st["enc"], st["bt"]
@@ -250,6 +252,8 @@ class DecoderCore:
             self._gemm_into(ws, grads["fc.weight"], D, V, D, TB, dpred, lda_p, st["Hd"], D, AMM, BKR, **ar)
         if "fc.bias" in need:
             K.colsum(dpred, TB, V, V, grads["fc.bias"], ws.work)
+        if on_fc_grads is not None:
+            on_fc_grads()
         if st["dropout_p"] > 0:
             K.dropout(ws.DHD, ws.DHD.numel(), st["dropout_p"], st["seed"], ws.DHD, seed_dev=st["seed_dev"])
 

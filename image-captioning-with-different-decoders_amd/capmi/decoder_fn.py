@@ -127,13 +127,14 @@ _FS = FusedStepState()
 
 
 def fused_loss_and_grads(dec, encoder_out, captions, caption_lengths, alpha_c, grads, need=None,
-                         seed_dev=None, denc=None):
+                         seed_dev=None, denc=None, on_fc_grads=None):
     """Forward + loss + backward of one decoder training step (models/attention.py:393-420).
 
     Writes d(loss)/d(param) into ``grads`` (name -> tensor, e.g. the optimizer's flat
     views); returns (loss (1,) device tensor, predictions, alphas). ``seed_dev``: an int64
     device counter driving the dropout mask (graph-replayable); else a host seed is drawn.
-    ``denc``: optional (B,14,14,2048)-sized buffer receiving d(loss)/d(encoder_out) (fine-tune)."""
+    ``denc``: optional (B,14,14,2048)-sized buffer receiving d(loss)/d(encoder_out) (fine-tune).
+    ``on_fc_grads``: callback once the fc gradients are final (before the BPTT loop)."""
     enc, caps = _prep_inputs(dec, encoder_out, captions)
     p = decoder_params(dec)
     decode_lengths = [int(l) - 1 for l in caption_lengths]
@@ -156,7 +157,7 @@ def fused_loss_and_grads(dec, encoder_out, captions, caption_lengths, alpha_c, g
     if "attention.full_att.weight" in g:
         g["attention.full_att.weight"] = g["attention.full_att.weight"].view(-1)
     CORE.backward(p, st, g, fs.dlogits, dpred_time_major=True, dreg=fs.dreg,
-                  denc=None if denc is None else denc.view(B, P, -1))
+                  denc=None if denc is None else denc.view(B, P, -1), on_fc_grads=on_fc_grads)
     return fs.loss, preds, alphas
 
 

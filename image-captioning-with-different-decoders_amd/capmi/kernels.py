@@ -160,6 +160,15 @@ def bn_relu_split3(y, scale, shift, rows, C, out):
     call("capmi_bn_relu_split3", ptr(y), ptr(scale), ptr(shift), int(rows), int(C), ptr(out), stream())
 
 
+def conv_weight_order_x3p(w, KH, KW, Cin):
+    """Packed conv weight [Cout][KH][KW][Cin] (or [Cout][K]) -> the k order of the x3p conv GEMM,
+    (ci / 32, kh, kw, ci % 32): the taps of one 32-channel slice consecutive (gemm_x3p.hip)."""
+    Cout = w.shape[0]
+    if KH * KW == 1:
+        return w.reshape(Cout, -1)
+    return w.reshape(Cout, KH, KW, Cin // 32, 32).permute(0, 3, 1, 2, 4).reshape(Cout, KH * KW * Cin)
+
+
 def gemm_x3p(prob, amode, workspace):
     """CAPMI_GEMM_X3P: A (prob.A) and B (prob.B) are both plane 0 of three bf16 split planes."""
     _cuda(workspace, dtype=torch.int32)

@@ -60,6 +60,28 @@ class Adam:
     def grad_buffers(self):
         return [f[2] for f in self.flats]
 
+    def grad_buckets(self, first):
+        """Split the flat gradient buffers into two lists of contiguous views: the span covering the
+        parameters in ``first`` (a set of Parameter objects; 256-B aligned slots, so the span also
+        holds their zero padding) and the rest. Data-parallel steps all-reduce ``first`` as soon as
+        those gradients are final, the rest after the backward."""
+        head, rest = [], []
+        for dt, pf, gf, m, v, layout in self.flats:
+            idx = [i for i, (p, off, k) in enumerate(layout) if any(p is q for q in first)]
+            if not idx:
+                rest.append(gf)
+                continue
+            lo = layout[idx[0]][1]
+            hi = layout[idx[-1] + 1][1] if idx[-1] + 1 < len(layout) else gf.numel()
+            if idx != list(range(idx[0], idx[-1] + 1)):
+                raise ValueError("grad_buckets: the parameters of the first bucket are not contiguous")
+            head.append(gf[lo:hi])
+            if lo > 0:
+                rest.append(gf[:lo])
+            if hi < gf.numel():
+                rest.append(gf[hi:])
+        return head, rest
+
     def zero_grad(self, set_to_none=False):
         for f in self.flats:
             f[2].zero_()

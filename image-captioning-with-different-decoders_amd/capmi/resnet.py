@@ -205,7 +205,7 @@ class EncoderRunner:
             # k-loops (K < 256) and layer4's 3136-row grids keep the in-kernel split (gemm_x3.hip)
             xp = self._x3p_buffer(self._ws)
             K.bn_relu_split3(x, in_ss[0], in_ss[1], N * H * W, ci, xp)
-            w3 = self._packed_x3(conv)
+            w3 = self._packed_x3(conv, tap_inner=True)
             if kh == 1 and st == 1:
                 prob, mode = K.problem(rows, co, Kd, xp, ci, w3, Kd, out, co, **kw_), CAPMI_A_KMAJOR
             else:
@@ -244,15 +244,20 @@ class EncoderRunner:
         del stats
         return Ho, Wo, rows
 
-    def _packed_x3(self, conv):
-        """[3][Cout][K] bf16 split of the packed fp32 weight (B operand of gemm_x3), refreshed when the
-        weight tensor changes (FineTuneRunner drops the trainable convs' entries every step: the
-        fused Adam writes the weights in place without bumping their version)."""
+    def _packed_x3(self, conv, tap_inner=False):
+        """[3][Cout][K] bf16 split of the packed fp32 weight (B operand of gemm_x3; with ``tap_inner``
+        in gemm_x3p's conv k order), refreshed when the weight tensor changes (FineTuneRunner drops
+        the trainable convs' entries every step: the fused Adam writes the weights in place without
+        bumping their version)."""
         w = conv.weight
-        key = ("x3", id(conv))
+        key = ("x3p" if tap_inner else "x3", id(conv))
         ent = self.packed.cache.get(key)
         if ent is None or ent[0] != w._version or ent[1] != w.data_ptr():
-            src = self.packed.get(conv).contiguous()
+            src = self.packed.get(conv)
+            if tap_inner:
+                co, ci, kh, kw = w.shape
+                src = K.conv_weight_order_x3p(src, kh, kw, ci)
+            src = src.contiguous()
             dst = torch.empty(3 * src.numel(), device=w.device, dtype=torch.bfloat16)
             K.split3_bf16(src, dst)
             ent = (w._version, w.data_ptr(), dst)
@@ -494,6 +499,7 @@ class FineTuneRunner:
                 convs = [blk.conv1, blk.conv2, blk.conv3] + ([blk.downsample[0]] if blk.downsample is not None else [])
                 for c in convs:
                     r.packed.cache.pop(("x3", id(c)), None)
+                    r.packed.cache.pop(("x3p", id(c)), None)
         H1, W1, rows = r._conv("conv1", imgs, net.conv1, ws["y1"], N, H, W, True, nchw=True)
         s, b = r._bn(ws, net.bn1, rows, True)
         Hp, Wp = (H1 + 2 - 3) // 2 + 1, (W1 + 2 - 3) // 2 + 1

@@ -58,6 +58,10 @@ class AttentionTrainStep:
         named = dict(decoder.named_parameters())
         self.need = [n for n in PNAMES if named[n].requires_grad]
         self.params = named
+        # data parallel: the fc gradients are final before the backward-through-time loop starts
+        # (decoder_core.backward computes them first), so their bucket is all-reduced beside the
+        # loop; the rest after it
+        self._b_fc, self._b_rest = optimizer.grad_buckets({named["fc.weight"], named["fc.bias"]})
         s = int(torch.randint(0, 2 ** 62, (1,)).item()) if seed is None else int(seed)
         self.seed_dev = torch.full((1,), s, dtype=torch.int64, device=dev)
         self._graph = None
@@ -160,12 +164,12 @@ class AttentionTrainStep:
             self.opt.step()
         return loss
 
-    def _dec_body(self, feats, captions, caption_lengths, with_update):
+    def _dec_body(self, feats, captions, caption_lengths, with_update, on_fc=None):
         K.counter_add(self.seed_dev, 1)
         self._apply_pending()
         loss, _, _ = DF.fused_loss_and_grads(self.decoder, feats, captions, caption_lengths,
                                              self.alpha_c, self._grads(), need=self.need,
-                                             seed_dev=self.seed_dev)
+                                             seed_dev=self.seed_dev, on_fc_grads=on_fc)
         if with_update:
             self.opt.step()
         return loss
@@ -230,14 +234,53 @@ class AttentionTrainStep:
                 self.encoder.forward_into(st["imgs"], self._feats[slot])
             st["g_enc"] = g
             st["feats"] = self._feats[slot]  # the graphs hold raw pointers: keep the buffer alive
-            g = torch.cuda.CUDAGraph()
             if self.capture_hook is not None:
                 self.capture_hook(f"dec{slot}")
-            with torch.cuda.graph(g):
-                st["loss"] = self._dec_body(self._feats[slot], st["caps"], st["lens"], with_update=upd)
-            st["g_dec"] = g
+            if upd:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    st["loss"] = self._dec_body(self._feats[slot], st["caps"], st["lens"], with_update=True)
+                st["g_dec"] = g
+            else:
+                # data parallel: two graphs cut where the fc gradients are final, so their all-reduce
+                # is issued between the replays and runs beside the backward-through-time graph
+                st["loss"], st["g_dec"], st["g_dec2"] = self._capture_split(
+                    lambda cut: self._dec_body(self._feats[slot], st["caps"], st["lens"], with_update=False, on_fc=cut))
         torch.cuda.synchronize()
         self._pg, self._pg_key = pg, key
+
+    @staticmethod
+    def _capture_split(body):
+        """Capture ``body(cut)`` into two HIP graphs sharing one memory pool: the first ends where
+        body calls ``cut()``. Returns (body's result, graph 1, graph 2)."""
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        pool = torch.cuda.graph_pool_handle()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        cs = torch.cuda.Stream()
+        cs.wait_stream(torch.cuda.current_stream())
+        cut_done = []
+
+        def cut():
+            g1.capture_end()
+            g2.capture_begin(pool=pool)
+            cut_done.append(True)
+
+        with torch.cuda.stream(cs):
+            g1.capture_begin(pool=pool)
+            out = body(cut)
+            if not cut_done:  # body never cut: everything is in graph 1, graph 2 stays empty
+                cut()
+            g2.capture_end()
+        torch.cuda.current_stream().wait_stream(cs)
+        return out, g1, g2
+
+    def _dp_update(self, fc_works):
+        """All-reduce the remaining gradient bucket, wait for both (stream-level), clamp + Adam."""
+        works = list(fc_works) + cdist.allreduce_mean_(self._b_rest, self.ctx, async_op=True)
+        for w in works:
+            w.wait()
+        self.opt.step()
 
     def _pg_call(self, imgs, captions, caption_lengths):
         key = (tuple(imgs.shape), tuple(captions.shape), tuple(caption_lengths))
@@ -283,8 +326,9 @@ class AttentionTrainStep:
                 st["g_dec"].replay()
                 self.replayed.append(f"dec{pslot}")
                 if self.ctx.distributed:
-                    cdist.allreduce_mean_(self.opt.grad_buffers(), self.ctx)
-                    self.opt.step()
+                    fc_works = cdist.allreduce_mean_(self._b_fc, self.ctx, async_op=True)
+                    st["g_dec2"].replay()
+                    self._dp_update(fc_works)
                 loss = st["loss"].detach().clone()
                 self._ev_dec = torch.cuda.Event()
                 self._ev_dec.record(self.s_dec)
@@ -295,9 +339,11 @@ class AttentionTrainStep:
         self.s_dec.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.s_dec):
             if self.ctx.distributed:
-                loss = self._dec_body(self._feats[pslot], caps, lens, with_update=False)
-                cdist.allreduce_mean_(self.opt.grad_buffers(), self.ctx)
-                self.opt.step()
+                fc_works = []
+                loss = self._dec_body(self._feats[pslot], caps, lens, with_update=False,
+                                      on_fc=lambda: fc_works.extend(
+                                          cdist.allreduce_mean_(self._b_fc, self.ctx, async_op=True)))
+                self._dp_update(fc_works)
             else:
                 loss = self._dec_body(self._feats[pslot], caps, lens, with_update=True)
             loss = loss.detach().clone()  # the loss buffer is reused by the next decoder step

@@ -67,6 +67,9 @@ gemm_x3p_kernel(const GemmArgs args) {
 #ifndef X3P_PRICE
 #define X3P_PRICE 0
 #endif
+#ifndef X3P_SKIP
+#define X3P_SKIP 0
+#endif
     // X3P_PRICE (timing-only builds): 1 = A descriptor with zero records (no A traffic), 2 = B, 3 = both
     const auto ra = rsrc_p(P.A, (X3P_PRICE & 1) ? 0u : (unsigned)(3 * planeA * 2));
     const auto rb = rsrc_p(P.B, (X3P_PRICE & 2) ? 0u : (unsigned)(3 * planeB * 2));
@@ -97,17 +100,25 @@ gemm_x3p_kernel(const GemmArgs args) {
     const int b_ch = dslot ^ ((br >> 2) & 3);
     const bool b_ok = n0 + br < N;
     const unsigned b_base = (unsigned)(((long long)(b_ok ? n0 + br : 0) * P.ldb + b_ch * 8) * 2);
+    // conv k order (ci / 32, kh, kw, ci % 32): the taps of one 32-channel slice are consecutive
+    // k-tiles, so the input rows a tile re-reads for its KH*KW taps are re-read within KH*KW k-tiles
+    // (L2-resident) instead of once per full sweep over Cin; the weights are packed to match
+    // (capmi.kernels.pack_conv_weight_x3p)
     int c_ci = 0, c_kh = 0, c_kw = 0;
     if (AMODE == 2) {
-      const int kpos = k_lo / cCin;
-      c_ci = k_lo - kpos * cCin;
-      c_kh = kpos / cKW;
-      c_kw = kpos - c_kh * cKW;
+      const int taps = cKW * P.cKH, kt0 = k_lo / PBK;
+      const int tap = kt0 % taps;
+      c_ci = (kt0 / taps) * PBK;
+      c_kh = tap / cKW;
+      c_kw = tap - c_kh * cKW;
     }
     const unsigned pA2 = (unsigned)(planeA * 2), pB2 = (unsigned)(planeB * 2);
 
     // DMA of k-tile kt into buffer buf: 6 A + 3 B wave-instructions per wave
     auto issue = [&](int kt, int buf) {
+#if X3P_SKIP & 1  // timing-only: no DMA
+      return;
+#endif
       const int k = k_lo + kt * PBK;
       const bool kok = k < k_hi;
       unsigned aoff[2];
@@ -123,12 +134,11 @@ gemm_x3p_kernel(const GemmArgs args) {
         }
       }
       if (AMODE == 2) {
-        c_ci += PBK;
-        if (c_ci >= cCin) {
-          c_ci = 0;
-          if (++c_kw == cKW) {
-            c_kw = 0;
-            ++c_kh;
+        if (++c_kw == cKW) {
+          c_kw = 0;
+          if (++c_kh == P.cKH) {
+            c_kh = 0;
+            c_ci += PBK;
           }
         }
       }
@@ -150,40 +160,55 @@ gemm_x3p_kernel(const GemmArgs args) {
     auto compute = [&](int buf) {
       const unsigned char* A_ = lds + buf * PBUF;
       const unsigned char* B_ = A_ + PA_BYTES;
+      // every fragment of the k-tile is requested up front (2 x 12 ds_read_b128): the second
+      // chunk's reads land while the first chunk's 24 MFMAs run
+      bf16x8_p a[PBK / 16][2][3], b[PBK / 16][2][3];
 #pragma unroll
       for (int g = 0; g < PBK / 16; ++g) {
         const int c = 2 * g + lh;  // logical 16-B chunk (8 k) this lane reads
-        bf16x8_p a[2][3], b[2][3];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int r = wm0 + 32 * i + lr;
           const int o = r * PROWB + ((c ^ ((r >> 2) & 3)) << 4);
+#if X3P_SKIP & 2  // timing-only: no LDS reads
 #pragma unroll
-          for (int p = 0; p < 3; ++p) a[i][p] = *reinterpret_cast<const bf16x8_p*>(A_ + p * PBM * PROWB + o);
+          for (int p = 0; p < 3; ++p) a[g][i][p] = bf16x8_p{} + (__bf16)(float)(o + p);
+#else
+#pragma unroll
+          for (int p = 0; p < 3; ++p) a[g][i][p] = *reinterpret_cast<const bf16x8_p*>(A_ + p * PBM * PROWB + o);
+#endif
         }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int r = wn0 + 32 * j + lr;
           const int o = r * PROWB + ((c ^ ((r >> 2) & 3)) << 4);
+#if X3P_SKIP & 2
 #pragma unroll
-          for (int p = 0; p < 3; ++p) b[j][p] = *reinterpret_cast<const bf16x8_p*>(B_ + p * PBN * PROWB + o);
+          for (int p = 0; p < 3; ++p) b[g][j][p] = bf16x8_p{} + (__bf16)(float)(o - p);
+#else
+#pragma unroll
+          for (int p = 0; p < 3; ++p) b[g][j][p] = *reinterpret_cast<const bf16x8_p*>(B_ + p * PBN * PROWB + o);
+#endif
         }
+      }
+#pragma unroll
+      for (int g = 0; g < PBK / 16; ++g) {
         // smallest terms first into each fp32 accumulator
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[g][i][1], b[g][j][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[g][i][0], b[g][j][2], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[g][i][2], b[g][j][0], acc[i][j], 0, 0, 0);
           }
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][1], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[g][i][0], b[g][j][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[g][i][1], b[g][j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[g][i][0], b[g][j][0], acc[i][j], 0, 0, 0);
           }
       }
     };
@@ -276,23 +301,38 @@ gemm_x3p_kernel(const GemmArgs args) {
   const bool cf = args.tile_cols_first != 0;
   const long long ngrp = args.sk_groups, grp = blockIdx.x % ngrp;
   const long long T = args.sk_units / nkt, G = gridDim.x / ngrp, w = blockIdx.x / ngrp;
-  if (args.sk_dp_tiles > 0) {
-    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = blockIdx.x & 7;
-    const int pos = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (blockIdx.x >> 3);
-    for (long long t = T + pos; t < T + args.sk_dp_tiles; t += nwg) {
-      const int tm = cf ? (int)(t % tiles_m) : (int)(t / tiles_n), tn = cf ? (int)(t / tiles_m) : (int)(t % tiles_n);
-      mainloop(P, tm * PBM, tn * PBN, 0, P.K);
-      epilogue(P, tm, tn);
-    }
+  const int nwg = gridDim.x;
+  long long pos;
+  {
+    const int q = nwg >> 3, r = nwg & 7, x = blockIdx.x & 7;
+    pos = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (blockIdx.x >> 3);
   }
   const long long ub = grp * T / ngrp * nkt, U = ((grp + 1) * T / ngrp) * nkt - ub;
   const long long u0 = ub + w * U / G, u1 = ub + (w + 1) * U / G;
-  if (u0 >= u1) return;
   constexpr int PART = PBM * PBN;
   int* flags = args.sk_flags;
-  for (long long t = (u1 - 1) / nkt; t >= u0 / nkt; --t) {
+  // one segment loop (a single mainloop call site keeps the register allocation of the
+  // data-parallel kernel): first the hybrid's whole tiles T + pos, T + pos + nwg, ..., then this
+  // worker's stream-K tiles from the last to the first
+  long long t_dp = T + pos, t_sk = u0 < u1 ? (u1 - 1) / nkt : -1;
+  const long long t_sk_end = u0 / nkt;
+  for (;;) {
+    long long t;
+    int ks, ke;
+    if (t_dp < T + args.sk_dp_tiles) {
+      t = t_dp;
+      t_dp += nwg;
+      ks = 0;
+      ke = nkt;
+    } else if (t_sk >= 0 && t_sk >= t_sk_end) {
+      t = t_sk--;
+      const long long tb = t * nkt;
+      ks = (int)(max(u0, tb) - tb);
+      ke = (int)(min(u1, tb + nkt) - tb);
+    } else {
+      break;
+    }
     const long long tb = t * nkt;
-    const int ks = (int)(max(u0, tb) - tb), ke = (int)(min(u1, tb + nkt) - tb);
     const int tm = cf ? (int)(t % tiles_m) : (int)(t / tiles_n), tn = cf ? (int)(t / tiles_m) : (int)(t % tiles_n);
     mainloop(P, tm * PBM, tn * PBN, ks * PBK, ke * PBK);
     if (ke < nkt) {

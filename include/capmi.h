@@ -126,8 +126,10 @@ int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int t
 #define CAPMI_GEMM_X3 4
 /* CAPMI_GEMM_X3P (alone): as CAPMI_GEMM_X3 with A pre-split too: the A pointer is plane 0 of three
  * bf16 planes (dense [3][M][lda], lda % 8 == 0; or the NHWC conv input [3][N*H*W][Cin], Cin % 32 ==
- * 0, from capmi_bn_relu_split3 / capmi_split3_bf16); no prologue. Tile 256x128, 512 threads, LDS-DMA
- * staging, one workgroup per CU; stream-K as capmi_gemm_sk. */
+ * 0, from capmi_bn_relu_split3 / capmi_split3_bf16); no prologue. For a conv the k order of B is
+ * (ci / 32, kh, kw, ci % 32) -- the KH*KW taps of a 32-channel slice consecutive, so a tile re-reads
+ * its input rows within KH*KW k-tiles (L2-resident); 1x1 convs: the plain order. Tile 256x128,
+ * 512 threads, LDS-DMA staging, one workgroup per CU; stream-K as capmi_gemm_sk. */
 #define CAPMI_GEMM_X3P 8
 int capmi_gemm_sk_ex(const capmi_gemm_problem* problem, int amode, int bmode, int tile, int flags, void* workspace,
                      long long ws_bytes, void* stream);

@@ -88,3 +88,28 @@ def test_dp_gloo_world2():
 
 
 PORT = [_free_port()]
+
+
+def test_grad_buckets_partition_flat_buffer():
+    """The data-parallel buckets (fc first, the rest after the backward) cover every gradient word of
+    the optimizer's flat buffers exactly once, and the first holds exactly fc.weight / fc.bias (plus
+    their alignment padding)."""
+    from capmi.optim import Adam
+    from helpers import make_decoder
+    dec, _ = make_decoder(32, 32, 16, 50, 3, "cpu")
+    for ft in (False, True):
+        dec.fine_tune_embeddings(ft)
+        opt = Adam([q for q in dec.parameters() if q.requires_grad], lr=1e-4)
+        head, rest = opt.grad_buckets({dec.fc.weight, dec.fc.bias})
+        gf = opt.grad_buffers()[0]
+        seen = torch.zeros(gf.numel(), dtype=torch.int32)
+        for v in head + rest:
+            off = (v.data_ptr() - gf.data_ptr()) // gf.element_size()
+            seen[off:off + v.numel()] += 1
+        assert bool((seen == 1).all())
+        (h,) = head
+        lo = (h.data_ptr() - gf.data_ptr()) // 4
+        for q in (dec.fc.weight, dec.fc.bias):
+            o = (q.grad.data_ptr() - gf.data_ptr()) // 4
+            assert lo <= o and o + q.numel() <= lo + h.numel()
+        assert h.numel() - (dec.fc.weight.numel() + dec.fc.bias.numel()) < 2 * 64  # padding only

@@ -178,7 +178,7 @@ def test_x3p_conv_stats(N, H, Cin, Cout, k, stride, pro):
     K.bn_relu_split3(x.to(DEV), s.to(DEV) if pro else None, b.to(DEV) if pro else None, N * H * H, Cin, xp)
     stats = torch.zeros(2 * K.stat_tiles(rows) * Cout, device=DEV)
     out = torch.full((rows, Cout), float("nan"), device=DEV)
-    w3 = split3(w.reshape(Cout, Kd).to(DEV))
+    w3 = split3(K.conv_weight_order_x3p(w.reshape(Cout, Kd), k, k, Cin).contiguous().to(DEV))
     if k == 1 and stride == 1:
         prob, mode = K.problem(rows, Cout, Kd, xp, Cin, w3, Kd, out, Cout, stats=stats), 0
     else:

@@ -70,7 +70,7 @@ def main():
         run = lambda: K.gemm_bf16(prob, mode, ws, a.tile)  # noqa: E731
     elif a.x3p:
         w3 = torch.empty(3 * w.numel(), device=dev, dtype=torch.bfloat16)
-        K.split3_bf16(w, w3)
+        K.split3_bf16(K.conv_weight_order_x3p(w, k, k, ci).contiguous(), w3)
         xp = torch.empty(3 * x.numel(), device=dev, dtype=torch.bfloat16)
         K.bn_relu_split3(x, sc if pro else None, sh if pro else None, x.numel() // ci, ci, xp)
         if k == 1 and stride == 1:

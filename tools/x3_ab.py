@@ -66,10 +66,12 @@ def main():
         arms = [("native", lambda: K.gemm_sk(pn, mode, ws)), ("x3", lambda: K.gemm_x3(p3, mode, ws))]
         if pro and Cout >= 128 and Cin % 32 == 0:  # x3p candidates: split pass + pre-split GEMM
             xp = torch.empty(3 * x.numel(), device=dev, dtype=torch.bfloat16)
+            w3p = torch.empty_like(w3)
+            K.split3_bf16(K.conv_weight_order_x3p(w, k, k, Cin).contiguous(), w3p)
             if k == 1 and st == 1:
-                pp, mp = K.problem(rows, Cout, Kd, xp, Cin, w3, Kd, out, Cout, stats=stats), 0
+                pp, mp = K.problem(rows, Cout, Kd, xp, Cin, w3p, Kd, out, Cout, stats=stats), 0
             else:
-                pp, mp = K.problem(rows, Cout, Kd, xp, 0, w3, Kd, out, Cout, conv=geo, stats=stats), 2
+                pp, mp = K.problem(rows, Cout, Kd, xp, 0, w3p, Kd, out, Cout, conv=geo, stats=stats), 2
             arms.append(("split", lambda: K.bn_relu_split3(x, sc, sh, N * H * H, Cin, xp)))
             arms.append(("x3p", lambda: K.gemm_x3p(pp, mp, ws)))
         for name, fn in arms:
