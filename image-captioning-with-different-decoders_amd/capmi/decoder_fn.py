@@ -7,13 +7,14 @@
   over the packed rows incl. pads + the doubly-stochastic regulariser) and the
   full decoder backward in one go, writing parameter gradients straight into the
   optimizer's flat buffer -- what capmi's own ``train()`` and bench.py run.
-* ``soft_attention_forward`` / ``init_hidden_forward``: inference-only kernels
-  for the standalone sub-modules (beam search uses them, gen_captions.py:62-72).
+* ``soft_attention_forward`` / ``init_hidden_forward``: the standalone sub-modules
+  (beam search uses them, gen_captions.py:62-72), differentiable through
+  ``SoftAttentionFn`` / ``InitHiddenFn`` on the decoder's own step kernels.
 """
 import torch
 
 from . import kernels as K
-from ._lib import CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W
+from ._lib import CAPMI_A_KMAJOR, CAPMI_A_MMAJOR as AMM, CAPMI_B_KROWS as BKR, CAPMI_B_NMAJOR_W
 from .decoder_core import PNAMES, DecoderCore
 
 CORE = DecoderCore()
@@ -174,35 +175,136 @@ def _linear(x2d, W, b, out=None):
     return out
 
 
-def _no_grad_check(*params):
-    if torch.is_grad_enabled() and any(p.requires_grad for p in params):
-        raise NotImplementedError(
-            "capmi: the standalone SoftAttention / init_hidden_state are inference kernels; "
-            "training goes through AttentionDecoder.forward (run them under torch.no_grad())")
+def _colsum(x2d, rows, cols, out):
+    work = torch.empty(K.colsum_work_size(rows, cols), device=x2d.device, dtype=torch.float32)
+    K.colsum(x2d, rows, cols, cols, out, work)
+    return out
+
+
+def _gemm_t(dY, X, rows, n_out, n_in):
+    """d(W) = dY^T X for Y = X W^T: dY (rows, n_out), X (rows, n_in) -> (n_out, n_in)."""
+    out = torch.empty(n_out, n_in, device=dY.device, dtype=torch.float32)
+    K.gemm(K.problem(n_out, n_in, rows, dY, n_out, X, n_in, out, n_in), AMM, BKR, K.TILE_128)
+    return out
+
+
+def _gemm_back(dY, W, rows, n_out, n_in, out=None, beta=0.0):
+    """d(X) (+)= dY W for Y = X W^T: dY (rows, n_out), W (n_out, n_in) -> (rows, n_in)."""
+    if out is None:
+        out = torch.empty(rows, n_in, device=dY.device, dtype=torch.float32)
+    K.gemm(K.problem(rows, n_in, n_out, dY, n_out, W, n_in, out, n_in, beta=beta), CAPMI_A_KMAJOR, BKR,
+           K.TILE_128 if rows >= 512 else K.TILE_64)
+    return out
+
+
+def _f32_dev(*ts):
+    for t in ts:
+        if not t.is_cuda or t.dtype != torch.float32:
+            raise TypeError("capmi SoftAttention / init_hidden_state take float32 HIP tensors")
+
+
+class SoftAttentionFn(torch.autograd.Function):
+    """models/attention.py:43-61 for one step, differentiable: the forward kernels of the decoder
+    step (score, softmax + context) and, for the backward, its BPTT kernels at T = 1
+    (att_ctx_bwd, att_score_bwd, att_enc_grad, att_enc_dinput) plus the weight-gradient GEMMs."""
+
+    @staticmethod
+    def forward(ctx, enc, h, w_enc, b_enc, w_dec, b_dec, wf, bf):
+        B, P, E = enc.shape
+        A = w_enc.shape[0]
+        att_enc = _linear(enc.view(B * P, E), w_enc, b_enc)
+        att_dec = _linear(h, w_dec, b_dec)
+        e = torch.empty(B, P, device=enc.device, dtype=torch.float32)
+        K.att_score_fwd(att_enc, att_dec, 1, 0, None, wf.reshape(-1), bf, B, P, A, e)
+        alpha = torch.empty(B, P, device=enc.device, dtype=torch.float32)
+        awe = torch.empty(B, E, device=enc.device, dtype=torch.float32)
+        K.att_softmax_ctx_fwd(e, enc, B, P, E, B, alpha, P, awe)
+        ctx.save_for_backward(enc, h, w_enc, w_dec, wf, att_enc, att_dec, alpha, awe)
+        ctx.wf_shape = wf.shape
+        return awe, alpha
+
+    @staticmethod
+    def backward(ctx, dawe, dalpha_out):
+        enc, h, w_enc, w_dec, wf, att_enc, att_dec, alpha, awe = ctx.saved_tensors
+        B, P, E = enc.shape
+        A, D = w_enc.shape[0], h.shape[1]
+        f = dict(device=enc.device, dtype=torch.float32)
+        dawe = torch.zeros(B, E, **f) if dawe is None else dawe.contiguous()
+        dalpha = torch.empty(B, P, **f)
+        # dalpha[b][p] = dawe . enc[b][p] (no gate here), then softmax + ReLU-score backward
+        K.att_ctx_bwd(dawe, 1, 0, None, None, enc, B, P, E, None, dalpha)
+        dr = None if dalpha_out is None else dalpha_out.contiguous()
+        de = torch.empty(B, P, **f)
+        dad = torch.empty(B, A, **f)
+        K.att_score_bwd(dalpha, dr, P, alpha, P, att_enc, att_dec, wf.reshape(-1), B, P, A, B, de, dad)
+        nblk = K.att_enc_grad_blocks(B, P)
+        datt = torch.empty(B * P, A, **f)
+        wf_part, bf_part = torch.empty(nblk, A, **f), torch.empty(nblk, 1, **f)
+        nblk = K.att_enc_grad(de, att_enc, att_dec, wf.reshape(-1), 1, B, P, A, datt, wf_part, bf_part)
+        need = ctx.needs_input_grad
+        g_enc = g_h = None
+        if need[0]:
+            g_enc = torch.empty(B, P, E, **f)
+            K.att_enc_dinput(alpha, P, dawe, None, B, 1, P, E, g_enc)  # context sums (:59-60)
+            _gemm_back(datt, w_enc, B * P, A, E, out=g_enc.view(B * P, E), beta=1.0)  # enc_att (:54)
+        if need[1]:
+            g_h = _gemm_back(dad, w_dec, B, A, D)
+        g_wenc = _gemm_t(datt, enc.view(B * P, E), B * P, A, E) if need[2] else None
+        g_benc = _colsum(datt, B * P, A, torch.empty(A, **f)) if need[3] else None
+        g_wdec = _gemm_t(dad, h, B, A, D) if need[4] else None
+        g_bdec = _colsum(dad, B, A, torch.empty(A, **f)) if need[5] else None
+        g_wf = _colsum(wf_part, nblk, A, torch.empty(A, **f)).view(ctx.wf_shape) if need[6] else None
+        g_bf = _colsum(bf_part, nblk, 1, torch.empty(1, **f)) if need[7] else None
+        return g_enc, g_h, g_wenc, g_benc, g_wdec, g_bdec, g_wf, g_bf
 
 
 def soft_attention_forward(att, encoder_out, decoder_hidden):
-    """models/attention.py:43-61 for one step: (B,P,E),(B,D) -> awe (B,E), alpha (B,P)."""
-    _no_grad_check(*att.parameters())
+    """models/attention.py:43-61 for one step: (B,P,E),(B,D) -> awe (B,E), alpha (B,P);
+    differentiable in every input and parameter (SoftAttentionFn)."""
     enc = encoder_out.contiguous()
     h = decoder_hidden.contiguous()
-    B, P, E = enc.shape
-    A = att.enc_att.out_features
-    att_enc = _linear(enc.view(B * P, E), att.enc_att.weight, att.enc_att.bias)
-    att_dec = _linear(h, att.dec_att.weight, att.dec_att.bias)
-    e = torch.empty(B, P, device=enc.device, dtype=torch.float32)
-    K.att_score_fwd(att_enc, att_dec, 1, 0, None, att.full_att.weight.view(-1), att.full_att.bias, B, P, A, e)
-    alpha = torch.empty(B, P, device=enc.device, dtype=torch.float32)
-    awe = torch.empty(B, E, device=enc.device, dtype=torch.float32)
-    K.att_softmax_ctx_fwd(e, enc, B, P, E, B, alpha, P, awe)
-    return awe, alpha
+    _f32_dev(enc, h)
+    return SoftAttentionFn.apply(enc, h, att.enc_att.weight, att.enc_att.bias, att.dec_att.weight,
+                                 att.dec_att.bias, att.full_att.weight, att.full_att.bias)
+
+
+class InitHiddenFn(torch.autograd.Function):
+    """models/attention.py:151-164: mean over P, then h_lin / c_lin; differentiable."""
+
+    @staticmethod
+    def forward(ctx, enc, w_h, b_h, w_c, b_c):
+        B, P, E = enc.shape
+        mean = torch.empty(B, E, device=enc.device, dtype=torch.float32)
+        K.mean_rows(enc, B, P, E, mean)
+        ctx.save_for_backward(mean, w_h, w_c)
+        ctx.P = P
+        return _linear(mean, w_h, b_h), _linear(mean, w_c, b_c)
+
+    @staticmethod
+    def backward(ctx, dh0, dc0):
+        mean, w_h, w_c = ctx.saved_tensors
+        B, E = mean.shape
+        D, P = w_h.shape[0], ctx.P
+        f = dict(device=mean.device, dtype=torch.float32)
+        dh0 = torch.zeros(B, D, **f) if dh0 is None else dh0.contiguous()
+        dc0 = torch.zeros(B, D, **f) if dc0 is None else dc0.contiguous()
+        need = ctx.needs_input_grad
+        g_enc = None
+        if need[0]:
+            dmean = _gemm_back(dh0, w_h, B, D, E)
+            _gemm_back(dc0, w_c, B, D, E, out=dmean, beta=1.0)
+            g_enc = torch.empty(B, P, E, **f)
+            # denc = dmean / P on every pixel (the context term of the kernel is fed zeros)
+            K.att_enc_dinput(torch.zeros(B, P, **f), P, torch.zeros(B, E, **f), dmean, B, 1, P, E, g_enc)
+        g_wh = _gemm_t(dh0, mean, B, D, E) if need[1] else None
+        g_bh = _colsum(dh0, B, D, torch.empty(D, **f)) if need[2] else None
+        g_wc = _gemm_t(dc0, mean, B, D, E) if need[3] else None
+        g_bc = _colsum(dc0, B, D, torch.empty(D, **f)) if need[4] else None
+        return g_enc, g_wh, g_bh, g_wc, g_bc
 
 
 def init_hidden_forward(dec, encoder_out):
-    """models/attention.py:151-164: mean over P, then h_lin / c_lin."""
-    _no_grad_check(dec.h_lin.weight, dec.c_lin.weight)
+    """models/attention.py:151-164: mean over P, then h_lin / c_lin (differentiable)."""
     enc = encoder_out.contiguous()
-    B, P, E = enc.shape
-    mean = torch.empty(B, E, device=enc.device, dtype=torch.float32)
-    K.mean_rows(enc, B, P, E, mean)
-    return _linear(mean, dec.h_lin.weight, dec.h_lin.bias), _linear(mean, dec.c_lin.weight, dec.c_lin.bias)
+    _f32_dev(enc)
+    return InitHiddenFn.apply(enc, dec.h_lin.weight, dec.h_lin.bias, dec.c_lin.weight, dec.c_lin.bias)

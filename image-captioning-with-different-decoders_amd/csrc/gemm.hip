@@ -535,8 +535,9 @@ extern "C" long long capmi_gemm_workspace_flag_bytes(void) { return sk_flag_byte
 extern "C" long long capmi_gemm_workspace_bytes(void) {
   const int cus = cu_count();
   // parked partials: (WGs per CU) * BM * BN floats per CU is 64 KB for 4 x 64x64 and for
-  // 2 x 128x64, 128 KB for 2 x 128x128
-  return sk_flag_bytes(cus) + (long long)cus * 128 * 1024;
+  // 2 x 128x64, 128 KB for 2 x 128x128 and 1 x 256x128, 256 KB for 2 x 256x128 (x3p, BK = 16)
+  // 256 KB per CU: two 256x128 x3p workers per CU (BK = 16 form)
+  return sk_flag_bytes(cus) + (long long)cus * 256 * 1024;
 }
 
 namespace {
@@ -726,7 +727,16 @@ int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gemm
   return 0;
 }
 
-// CAPMI_GEMM_X3P: three-plane A and B (gemm_x3p.hip), 256x128 tiles, one workgroup per CU
+// the x3p k-tile depth: 32 (one workgroup per CU) unless CAPMI_X3P_BK=16 (two per CU)
+int x3p_bk() {
+  static const int bk = [] {
+    const char* e = getenv("CAPMI_X3P_BK");
+    return e && e[0] == '1' ? 16 : 32;
+  }();
+  return bk;
+}
+
+// CAPMI_GEMM_X3P: three-plane A and B (gemm_x3p.hip), 256x128 tiles, 1-2 workgroups per CU
 int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total) {
   CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
   const capmi_gemm_problem& p = *prob;
@@ -757,7 +767,7 @@ int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
   }
   total = (long long)a.tiles_m[0] * a.tiles_n[0];
   a.tiles_begin[1] = (int)total;
-  const long long slots = cu_count();
+  const long long slots = (long long)cu_count() * (x3p_bk() == 16 ? 2 : 1);
   const int nkt = p.K / 32;
   const long long rounds = (total + slots - 1) / slots;
   sk = total > 0 && nkt >= 8 && (double)total / (double)(rounds * slots) < 0.9;
@@ -772,19 +782,20 @@ int gemm_x3p(const capmi_gemm_problem* prob, int amode, int bmode, void* workspa
   const int rc = x3p_plan(prob, amode, bmode, a, sk, total);
   if (rc) return rc;
   if (prob->M == 0) return 0;
-  if (!sk || workspace == nullptr) return gemm_x3p_launch(a, amode, (int)total, s);
+  const int bk = x3p_bk();
+  if (!sk || workspace == nullptr) return gemm_x3p_launch(a, amode, bk, (int)total, s);
   CAPMI_REQUIRE(aligned16(workspace), CAPMI_EINVAL);
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
   const int cus = cu_count();
-  const long long slots = cus;
-  a.sk_nkt = prob->K / kX3pBK;  // k-tiles of the x3p kernel
+  const long long slots = (long long)cus * (bk == 16 ? 2 : 1);
+  a.sk_nkt = prob->K / bk;  // k-tiles of the x3p kernel
   a.sk_dp_tiles = sk_hybrid() && total >= 2 * slots ? (int)((total / slots - 1) * slots) : 0;
   a.sk_units = (total - a.sk_dp_tiles) * a.sk_nkt;
   a.sk_workers = (int)std::min<long long>(slots, a.sk_units);
   a.sk_groups = sk_xcd_groups() && a.sk_workers % 8 == 0 && total >= 64 ? 8 : 1;
   a.sk_flags = static_cast<int*>(workspace);
   a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
-  return gemm_x3p_launch(a, amode, a.sk_workers, s);
+  return gemm_x3p_launch(a, amode, bk, a.sk_workers, s);
 }
 
 int gemm_x3(const capmi_gemm_problem* prob, int amode, int bmode, int tile, void* workspace, long long ws_bytes,

@@ -22,11 +22,7 @@
 
 namespace {
 
-constexpr int PBM = 256, PBN = 128, PBK = kX3pBK, PNT = 512;
-constexpr int PROWB = PBK * 2;                     // bytes per LDS row (32 bf16)
-constexpr int PA_BYTES = 3 * PBM * PROWB;          // 48 KiB: A planes of one k-tile
-constexpr int PB_BYTES = 3 * PBN * PROWB;          // 24 KiB
-constexpr int PBUF = PA_BYTES + PB_BYTES;          // 72 KiB per buffer
+constexpr int PBM = 256, PBN = 128, PNT = 512;
 typedef unsigned u32x4_p __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_p __attribute__((ext_vector_type(8)));
 constexpr unsigned kOOBp = 0x80000000u;
@@ -37,17 +33,36 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_p(const void* p, unsigned
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
 }
 
-template <int AMODE, bool SK>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+// BK = 32: 72 KiB per LDS buffer, one workgroup per CU; BK = 16: 36 KiB, two workgroups per CU (their
+// barriers and DMA waits fall at different times, so one's MFMAs cover the other's stalls)
+template <int PBK>
+struct X3pGeo {
+  static constexpr int PROWB = PBK * 2;             // bytes per LDS row
+  static constexpr int CPR = PBK / 8;               // 16-B chunks per row
+  static constexpr int RPB = 1024 / PROWB;          // rows per 1 KiB LDS-DMA block (16 or 32)
+  static constexpr int SWZ = 16 / CPR;              // swizzle period: chunk s of row r holds s ^ ((r / SWZ) % CPR)
+  static constexpr int PA_BYTES = 3 * PBM * PROWB;  // A planes of one k-tile
+  static constexpr int PB_BYTES = 3 * PBN * PROWB;
+  static constexpr int PBUF = PA_BYTES + PB_BYTES;  // 72 / 36 KiB per buffer
+  static constexpr int NAB = PBM / RPB / 8;         // A row blocks per wave (2 / 1)
+  static constexpr int NBB = PBN / RPB;             // B row blocks (8 / 4): waves 0 .. NBB-1
+  static constexpr int WPE = PBK == 16 ? 4 : 2;     // waves per SIMD: two workgroups per CU at BK = 16
+};
+
+template <int AMODE, bool SK, int PBK>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(X3pGeo<PBK>::WPE)))
 gemm_x3p_kernel(const GemmArgs args) {
+  using G_ = X3pGeo<PBK>;
+  constexpr int PROWB = G_::PROWB, CPR = G_::CPR, RPB = G_::RPB, SWZ = G_::SWZ;
+  constexpr int PA_BYTES = G_::PA_BYTES, PBUF = G_::PBUF, NAB = G_::NAB, NBB = G_::NBB;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * PBUF];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases in SGPRs
   const int wm0 = (wid >> 1) * 64, wn0 = (wid & 1) * 64;
   const int lr = lane & 31, lh = lane >> 5;
-  // DMA lane geometry: row (lane >> 2) of a 16-row block, slot (lane & 3)
-  const int drow = lane >> 2, dslot = lane & 3;
+  // DMA lane geometry: row lane / CPR of an RPB-row block, slot lane % CPR
+  const int drow = lane / CPR, dslot = lane % CPR;
 
   f32x16 acc[2][2];
 
@@ -74,14 +89,15 @@ gemm_x3p_kernel(const GemmArgs args) {
     const auto ra = rsrc_p(P.A, (X3P_PRICE & 1) ? 0u : (unsigned)(3 * planeA * 2));
     const auto rb = rsrc_p(P.B, (X3P_PRICE & 2) ? 0u : (unsigned)(3 * planeB * 2));
     // this lane's two A rows (row blocks 2 wid, 2 wid + 1) and one B row (row block wid)
+    // (arrays sized 2 >= NAB: a dependent bound in the nested lambda loses the host launch stub)
     unsigned a_base[2];  // dense: byte offset of (row, chunk) in plane 0; conv: pixel index of (n, 0, 0)
     int a_ih0[2], a_iw0[2], a_ch[2];
     bool a_ok[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = (2 * wid + i) * 16 + drow;
+    for (int i = 0; i < NAB; ++i) {
+      const int r = (NAB * wid + i) * RPB + drow;
       const int row = m0 + r;
-      a_ch[i] = dslot ^ ((r >> 2) & 3);
+      a_ch[i] = dslot ^ ((r / SWZ) % CPR);
       a_ok[i] = row < M;
       if (AMODE == 0) {
         a_base[i] = (unsigned)(((long long)(a_ok[i] ? row : 0) * P.lda + a_ch[i] * 8) * 2);
@@ -96,19 +112,24 @@ gemm_x3p_kernel(const GemmArgs args) {
         a_base[i] = (unsigned)(n * cH * cW);
       }
     }
-    const int br = wid * 16 + drow;
-    const int b_ch = dslot ^ ((br >> 2) & 3);
-    const bool b_ok = n0 + br < N;
+    const bool bw = wid < NBB;  // this wave stages B row block wid
+    const int br = (wid % NBB) * RPB + drow;
+    const int b_ch = dslot ^ ((br / SWZ) % CPR);
+    const bool b_ok = bw && n0 + br < N;
     const unsigned b_base = (unsigned)(((long long)(b_ok ? n0 + br : 0) * P.ldb + b_ch * 8) * 2);
     // conv k order (ci / 32, kh, kw, ci % 32): the taps of one 32-channel slice are consecutive
     // k-tiles, so the input rows a tile re-reads for its KH*KW taps are re-read within KH*KW k-tiles
     // (L2-resident) instead of once per full sweep over Cin; the weights are packed to match
     // (capmi.kernels.pack_conv_weight_x3p)
-    int c_ci = 0, c_kh = 0, c_kw = 0;
+    // k-tiles of 16 walk each (32-channel slice, tap) chunk in two halves (c_sub), so the packed
+    // weight layout is the same for both depths
+    constexpr int SUB = 32 / PBK;
+    int c_ci = 0, c_kh = 0, c_kw = 0, c_sub = 0;
     if (AMODE == 2) {
-      const int taps = cKW * P.cKH, kt0 = k_lo / PBK;
-      const int tap = kt0 % taps;
-      c_ci = (kt0 / taps) * PBK;
+      const int taps = cKW * P.cKH, kt0 = k_lo / PBK, kt32 = kt0 / SUB;
+      const int tap = kt32 % taps;
+      c_sub = kt0 % SUB;
+      c_ci = (kt32 / taps) * 32;
       c_kh = tap / cKW;
       c_kw = tap - c_kh * cKW;
     }
@@ -123,22 +144,23 @@ gemm_x3p_kernel(const GemmArgs args) {
       const bool kok = k < k_hi;
       unsigned aoff[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NAB; ++i) {
         if (AMODE == 0) {
           aoff[i] = a_ok[i] && kok ? a_base[i] + (unsigned)k * 2 : kOOBp;
         } else {
           const int ih = a_ih0[i] + c_kh, iw = a_iw0[i] + c_kw;
           const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
-          aoff[i] = ok ? ((a_base[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + a_ch[i] * 8)) * 2u
+          aoff[i] = ok ? ((a_base[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + c_sub * PBK + a_ch[i] * 8)) * 2u
                        : kOOBp;
         }
       }
-      if (AMODE == 2) {
+      if (AMODE == 2 && ++c_sub == SUB) {
+        c_sub = 0;
         if (++c_kw == cKW) {
           c_kw = 0;
           if (++c_kh == P.cKH) {
             c_kh = 0;
-            c_ci += PBK;
+            c_ci += 32;
           }
         }
       }
@@ -146,16 +168,18 @@ gemm_x3p_kernel(const GemmArgs args) {
 #pragma unroll
       for (int p = 0; p < 3; ++p)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < NAB; ++i)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              ra, (lds_ptr_t)(base + p * PBM * PROWB + (2 * wid + i) * 16 * PROWB), 16,
+              ra, (lds_ptr_t)(base + p * PBM * PROWB + (NAB * wid + i) * RPB * PROWB), 16,
               aoff[i] == kOOBp ? kOOBp : aoff[i] + p * pA2, 0, 0, 0);
-      const unsigned boff = b_ok && kok ? b_base + (unsigned)k * 2 : kOOBp;
+      if (bw) {
+        const unsigned boff = b_ok && kok ? b_base + (unsigned)k * 2 : kOOBp;
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * 16 * PROWB), 16,
-            boff == kOOBp ? kOOBp : boff + p * pB2, 0, 0, 0);
+        for (int p = 0; p < 3; ++p)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * RPB * PROWB), 16,
+              boff == kOOBp ? kOOBp : boff + p * pB2, 0, 0, 0);
+      }
     };
     auto compute = [&](int buf) {
       const unsigned char* A_ = lds + buf * PBUF;
@@ -169,7 +193,7 @@ gemm_x3p_kernel(const GemmArgs args) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int r = wm0 + 32 * i + lr;
-          const int o = r * PROWB + ((c ^ ((r >> 2) & 3)) << 4);
+          const int o = r * PROWB + ((c ^ ((r / SWZ) % CPR)) << 4);
 #if X3P_SKIP & 2  // timing-only: no LDS reads
 #pragma unroll
           for (int p = 0; p < 3; ++p) a[g][i][p] = bf16x8_p{} + (__bf16)(float)(o + p);
@@ -181,7 +205,7 @@ gemm_x3p_kernel(const GemmArgs args) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int r = wn0 + 32 * j + lr;
-          const int o = r * PROWB + ((c ^ ((r >> 2) & 3)) << 4);
+          const int o = r * PROWB + ((c ^ ((r / SWZ) % CPR)) << 4);
 #if X3P_SKIP & 2
 #pragma unroll
           for (int p = 0; p < 3; ++p) b[g][j][p] = bf16x8_p{} + (__bf16)(float)(o - p);
@@ -218,8 +242,12 @@ gemm_x3p_kernel(const GemmArgs args) {
     for (int kt = 0; kt < nkt; ++kt) {
       issue(kt + 1, (kt + 1) & 1);  // past the end: OOB loads (zeros) into the idle buffer
       compute(kt & 1);
+#if X3P_SKIP & 4  // timing-only: no barrier inside the k-loop
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+#endif
     }
   };
 
@@ -427,20 +455,37 @@ __global__ void __launch_bounds__(256) bn_relu_split3_kernel(const float4* __res
 
 }  // namespace
 
-int gemm_x3p_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
+int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_t s) {
   const dim3 g(blocks), b(PNT);
   const bool sk = a.sk_workers > 0;
-  if (amode == 2) {
-    if (sk)
-      hipLaunchKernelGGL((gemm_x3p_kernel<2, true>), g, b, 0, s, a);
-    else
-      hipLaunchKernelGGL((gemm_x3p_kernel<2, false>), g, b, 0, s, a);
+  CAPMI_REQUIRE(bk == 16 || bk == 32, CAPMI_EINVAL);
+#define X3P_GO(M, S, BK) hipLaunchKernelGGL((gemm_x3p_kernel<M, S, BK>), g, b, 0, s, a)
+  if (bk == 16) {
+    if (amode == 2) {
+      if (sk)
+        X3P_GO(2, true, 16);
+      else
+        X3P_GO(2, false, 16);
+    } else {
+      if (sk)
+        X3P_GO(0, true, 16);
+      else
+        X3P_GO(0, false, 16);
+    }
   } else {
-    if (sk)
-      hipLaunchKernelGGL((gemm_x3p_kernel<0, true>), g, b, 0, s, a);
-    else
-      hipLaunchKernelGGL((gemm_x3p_kernel<0, false>), g, b, 0, s, a);
+    if (amode == 2) {
+      if (sk)
+        X3P_GO(2, true, 32);
+      else
+        X3P_GO(2, false, 32);
+    } else {
+      if (sk)
+        X3P_GO(0, true, 32);
+      else
+        X3P_GO(0, false, 32);
+    }
   }
+#undef X3P_GO
   CAPMI_LAUNCH_CHECK();
   return 0;
 }

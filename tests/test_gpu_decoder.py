@@ -63,6 +63,65 @@ def test_soft_attention_matches_golden(golden, tag):
     assert_close(awe, t(fx["awe"]), 1e-4, 1e-5, "awe")
 
 
+def _attention_ref64(enc, h, ps):
+    """SoftAttention.forward (models/attention.py:43-61) in fp64 torch: the autograd reference."""
+    att = torch.relu(enc @ ps["ea.w"].T + ps["ea.b"] + (h @ ps["da.w"].T + ps["da.b"])[:, None, :])
+    alpha = torch.softmax((att @ ps["fa.w"].T).squeeze(2) + ps["fa.b"], dim=1)
+    return (enc * alpha[:, :, None]).sum(1), alpha
+
+
+def test_soft_attention_and_init_hidden_backward():
+    """The standalone SoftAttention / init_hidden_state are differentiable (verdict r01 weak 10):
+    every input and parameter gradient vs fp64 torch autograd, rtol 1e-4 + 1e-5 * max|g|."""
+    from models.attention import SoftAttention
+    g = torch.Generator().manual_seed(5)
+    B, P, E, D, A = 3, 13, 64, 32, 48
+    att = SoftAttention(E, D, A).to(DEV)
+    enc = torch.rand(B, P, E, generator=g)
+    h = torch.rand(B, D, generator=g) * 2 - 1
+    r1, r2 = torch.randn(B, E, generator=g), torch.randn(B, P, generator=g)
+    e_d, h_d = enc.to(DEV).requires_grad_(), h.to(DEV).requires_grad_()
+    awe, alpha = att(e_d, h_d)
+    ((awe * r1.to(DEV)).sum() + (alpha * r2.to(DEV)).sum()).backward()
+    names = {"ea": att.enc_att, "da": att.dec_att, "fa": att.full_att}
+    ps = {f"{k}.{w}": getattr(m, "weight" if w == "w" else "bias").detach().cpu().double().requires_grad_()
+          for k, m in names.items() for w in ("w", "b")}
+    e64, h64 = enc.double().requires_grad_(), h.double().requires_grad_()
+    a64, al64 = _attention_ref64(e64, h64, ps)
+    ((a64 * r1.double()).sum() + (al64 * r2.double()).sum()).backward()
+    torch.cuda.synchronize()
+
+    def close(got, want, name):
+        want = want.float()
+        assert_close(got.detach().cpu().reshape(want.shape), want, 1e-4, 1e-5 * float(want.abs().max()), name)
+    close(awe, a64.detach(), "awe")
+    close(alpha, al64.detach(), "alpha")
+    close(e_d.grad, e64.grad, "d enc")
+    close(h_d.grad, h64.grad, "d h")
+    for k, m in names.items():
+        close(m.weight.grad, ps[f"{k}.w"].grad, f"d {k}.weight")
+        close(m.bias.grad, ps[f"{k}.b"].grad, f"d {k}.bias")
+
+    # init_hidden_state (:151-164) on the decoder's E = 2048 features
+    dec, _ = make_decoder(A, D, 16, 40, 3, DEV)
+    enc = torch.rand(B, P, 2048, generator=g)
+    rh, rc = torch.randn(B, D, generator=g), torch.randn(B, D, generator=g)
+    e_d = enc.to(DEV).requires_grad_()
+    h0, c0 = dec.init_hidden_state(e_d)
+    ((h0 * rh.to(DEV)).sum() + (c0 * rc.to(DEV)).sum()).backward()
+    m64 = enc.double().requires_grad_()
+    wl = {n: dict(dec.named_parameters())[n].detach().cpu().double().requires_grad_()
+          for n in ("h_lin.weight", "h_lin.bias", "c_lin.weight", "c_lin.bias")}
+    mean = m64.mean(1)
+    h64 = mean @ wl["h_lin.weight"].T + wl["h_lin.bias"]
+    c64 = mean @ wl["c_lin.weight"].T + wl["c_lin.bias"]
+    ((h64 * rh.double()).sum() + (c64 * rc.double()).sum()).backward()
+    torch.cuda.synchronize()
+    close(e_d.grad, m64.grad, "init d enc")
+    for n, w in wl.items():
+        close(dict(dec.named_parameters())[n].grad, w.grad, f"init d {n}")
+
+
 KINK_ROWS = ("attention.enc_att.weight", "attention.enc_att.bias", "attention.dec_att.weight",
              "attention.dec_att.bias")
 
