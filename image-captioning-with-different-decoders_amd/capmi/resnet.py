@@ -198,11 +198,12 @@ class EncoderRunner:
             geo["Cin"] = 4
             prob = K.problem(rows, co, K4, img4, 0, w, K4, out, co, conv=geo, **kw_)
             mode = CAPMI_A_CONV_NHWC4
-        elif self.x3 and in_ss is not None and co >= 128 and ci % 32 == 0 and Kd >= 256 and rows >= 12544:
+        elif self.x3 and in_ss is not None and co >= 128 and ci % 32 == 0 and Kd >= 128 and rows >= 12544:
             # x3p: the conv input relu(bn(y)) split once into three bf16 planes, then the GEMM with
             # both operands pre-split (gemm_x3p.hip). Where it pays (tools/x3_ab.py, batch 64): the
-            # 3x3 convs of layer2/3 and layer3's c3 (their A tiles are re-staged 9x / 8x); short
-            # k-loops (K < 256) and layer4's 3136-row grids keep the in-kernel split (gemm_x3.hip)
+            # 3x3 convs of layer2/3 and the c3 convs of layer2/3 (their A tiles are re-staged 9x /
+            # 4-8x); layer1's K = 64 c3 (no gain once the split pass is counted) and layer4's
+            # 3136-row grids keep the in-kernel split (gemm_x3.hip)
             xp = self._x3p_buffer(self._ws)
             K.bn_relu_split3(x, in_ss[0], in_ss[1], N * H * W, ci, xp)
             w3 = self._packed_x3(conv, tap_inner=True)

@@ -535,9 +535,8 @@ extern "C" long long capmi_gemm_workspace_flag_bytes(void) { return sk_flag_byte
 extern "C" long long capmi_gemm_workspace_bytes(void) {
   const int cus = cu_count();
   // parked partials: (WGs per CU) * BM * BN floats per CU is 64 KB for 4 x 64x64 and for
-  // 2 x 128x64, 128 KB for 2 x 128x128 and 1 x 256x128, 256 KB for 2 x 256x128 (x3p, BK = 16)
-  // 256 KB per CU: two 256x128 x3p workers per CU (BK = 16 form)
-  return sk_flag_bytes(cus) + (long long)cus * 256 * 1024;
+  // 2 x 128x64, 128 KB for 2 x 128x128 and 1 x 256x128
+  return sk_flag_bytes(cus) + (long long)cus * 128 * 1024;
 }
 
 namespace {
@@ -600,7 +599,8 @@ int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, bo
 namespace {
 int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, GemmArgs& a, int& bn, bool& sk,
             long long& total);
-int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total);
+int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total,
+             int& bk);
 }  // namespace
 
 extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, int flags,
@@ -610,13 +610,14 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
   if (flags == CAPMI_GEMM_X3P) {
     GemmArgs a;
     long long total = 0;
-    const int rc = x3p_plan(prob, amode, bmode, a, sk, total);
+    int bk = 32;
+    const int rc = x3p_plan(prob, amode, bmode, a, sk, total, bk);
     if (rc) return rc;
     if (threads) *threads = 512;
     if (bm) *bm = 256;
     if (bn) *bn = 128;
     if (stream_k) *stream_k = sk ? 1 : 0;
-    if (generic) *generic = 0;
+    if (generic) *generic = bk;  // CAPMI_GEMM_X3P: the k-tile depth
     return 0;
   }
   if (flags == CAPMI_GEMM_X3) {
@@ -727,17 +728,22 @@ int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gemm
   return 0;
 }
 
-// the x3p k-tile depth: 32 (one workgroup per CU) unless CAPMI_X3P_BK=16 (two per CU)
-int x3p_bk() {
-  static const int bk = [] {
+// CAPMI_X3P_BK=32 forces the one-workgroup-per-CU form (A/B measurements)
+bool x3p_force32() {
+  static const bool f = [] {
     const char* e = getenv("CAPMI_X3P_BK");
-    return e && e[0] == '1' ? 16 : 32;
+    return e && e[0] == '3';
   }();
-  return bk;
+  return f;
 }
 
 // CAPMI_GEMM_X3P: three-plane A and B (gemm_x3p.hip), 256x128 tiles, 1-2 workgroups per CU
-int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total) {
+// Two forms: BK = 16 with two workgroups per CU (their DMA waits and barriers interleave) as a
+// plain data-parallel grid when there are at least 2 x CUs tiles and they fill >= 70 % of the last
+// round; otherwise BK = 32, one workgroup per CU, stream-K when the tile count leaves the chip
+// under-filled (l3 c3, 392 tiles: 49 us stream-K vs 102 us as one 2-per-CU round).
+int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total,
+             int& bk) {
   CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
   const capmi_gemm_problem& p = *prob;
   CAPMI_REQUIRE(bmode == CAPMI_B_NMAJOR_W && (amode == CAPMI_A_KMAJOR || amode == CAPMI_A_CONV_NHWC), CAPMI_EINVAL);
@@ -767,7 +773,15 @@ int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
   }
   total = (long long)a.tiles_m[0] * a.tiles_n[0];
   a.tiles_begin[1] = (int)total;
-  const long long slots = (long long)cu_count() * (x3p_bk() == 16 ? 2 : 1);
+  const long long slots2 = 2LL * cu_count();
+  const long long rounds2 = (total + slots2 - 1) / slots2;
+  if (!x3p_force32() && total >= slots2 && (double)total / (double)(rounds2 * slots2) >= 0.7) {
+    bk = 16;
+    sk = false;
+    return 0;
+  }
+  bk = 32;
+  const long long slots = cu_count();
   const int nkt = p.K / 32;
   const long long rounds = (total + slots - 1) / slots;
   sk = total > 0 && nkt >= 8 && (double)total / (double)(rounds * slots) < 0.9;
@@ -779,15 +793,15 @@ int gemm_x3p(const capmi_gemm_problem* prob, int amode, int bmode, void* workspa
   GemmArgs a;
   bool sk = false;
   long long total = 0;
-  const int rc = x3p_plan(prob, amode, bmode, a, sk, total);
+  int bk = 32;
+  const int rc = x3p_plan(prob, amode, bmode, a, sk, total, bk);
   if (rc) return rc;
   if (prob->M == 0) return 0;
-  const int bk = x3p_bk();
   if (!sk || workspace == nullptr) return gemm_x3p_launch(a, amode, bk, (int)total, s);
   CAPMI_REQUIRE(aligned16(workspace), CAPMI_EINVAL);
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
   const int cus = cu_count();
-  const long long slots = (long long)cus * (bk == 16 ? 2 : 1);
+  const long long slots = cus;
   a.sk_nkt = prob->K / bk;  // k-tiles of the x3p kernel
   a.sk_dp_tiles = sk_hybrid() && total >= 2 * slots ? (int)((total / slots - 1) * slots) : 0;
   a.sk_units = (total - a.sk_dp_tiles) * a.sk_nkt;

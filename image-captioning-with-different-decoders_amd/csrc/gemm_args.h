@@ -36,7 +36,8 @@ int gemm_bf16_launch(const GemmArgs& a, int amode, int bm, int bn, int blocks, h
 // amode 0 (dense) / 2 (conv, optional prologue)
 int gemm_x3_launch(const GemmArgs& a, int amode, int bn, int blocks, hipStream_t s);
 // x3 with both operands pre-split (gemm_x3p.hip): 256x128 tiles, 512 threads, amode 0 / 2; k-tile depth
-// bk (16: two workgroups per CU, 32: one) is the unit of GemmArgs::sk_nkt for it
+// bk (16: two workgroups per CU, data-parallel grids only; 32: one, stream-K capable) is the unit
+// of GemmArgs::sk_nkt for it
 int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_t s);
 // resident workgroups per CU of the NT kernel for a tile shape (LDS / register bound)
 inline int gemm_nt_wg_per_cu(int bm, int bn) { return bm == 64 && bn == 64 ? 4 : 2; }

@@ -458,32 +458,25 @@ __global__ void __launch_bounds__(256) bn_relu_split3_kernel(const float4* __res
 int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_t s) {
   const dim3 g(blocks), b(PNT);
   const bool sk = a.sk_workers > 0;
-  CAPMI_REQUIRE(bk == 16 || bk == 32, CAPMI_EINVAL);
+  // the two-workgroup form runs data-parallel grids only (its 128-VGPR budget has no room for
+  // the stream-K hand-off)
+  CAPMI_REQUIRE(bk == 32 || (bk == 16 && !sk), CAPMI_EINVAL);
 #define X3P_GO(M, S, BK) hipLaunchKernelGGL((gemm_x3p_kernel<M, S, BK>), g, b, 0, s, a)
   if (bk == 16) {
-    if (amode == 2) {
-      if (sk)
-        X3P_GO(2, true, 16);
-      else
-        X3P_GO(2, false, 16);
-    } else {
-      if (sk)
-        X3P_GO(0, true, 16);
-      else
-        X3P_GO(0, false, 16);
-    }
+    if (amode == 2)
+      X3P_GO(2, false, 16);
+    else
+      X3P_GO(0, false, 16);
+  } else if (amode == 2) {
+    if (sk)
+      X3P_GO(2, true, 32);
+    else
+      X3P_GO(2, false, 32);
   } else {
-    if (amode == 2) {
-      if (sk)
-        X3P_GO(2, true, 32);
-      else
-        X3P_GO(2, false, 32);
-    } else {
-      if (sk)
-        X3P_GO(0, true, 32);
-      else
-        X3P_GO(0, false, 32);
-    }
+    if (sk)
+      X3P_GO(0, true, 32);
+    else
+      X3P_GO(0, false, 32);
   }
 #undef X3P_GO
   CAPMI_LAUNCH_CHECK();

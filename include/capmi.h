@@ -129,13 +129,16 @@ int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int t
  * 0, from capmi_bn_relu_split3 / capmi_split3_bf16); no prologue. For a conv the k order of B is
  * (ci / 32, kh, kw, ci % 32) -- the KH*KW taps of a 32-channel slice consecutive, so a tile re-reads
  * its input rows within KH*KW k-tiles (L2-resident); 1x1 convs: the plain order. Tile 256x128,
- * 512 threads, LDS-DMA staging, one workgroup per CU; stream-K as capmi_gemm_sk. */
+ * 512 threads, LDS-DMA staging; k-tiles of 16 with two workgroups per CU (data-parallel grid)
+ * when there are >= 2 x CUs tiles filling >= 70 % of the last round, else k-tiles of 32, one
+ * workgroup per CU, stream-K as capmi_gemm_sk. */
 #define CAPMI_GEMM_X3P 8
 int capmi_gemm_sk_ex(const capmi_gemm_problem* problem, int amode, int bmode, int tile, int flags, void* workspace,
                      long long ws_bytes, void* stream);
 /* the launch capmi_gemm_sk_ex(..., flags, ...) would make (no GPU work): tile bm x bn, stream_k 0/1,
- * generic = 1 when the problem falls back to the generic kernel, threads = workgroup size (256, or
- * 512 for the CAPMI_TILE_128_W8 form AUTO picks for wide convs). Used by the benchmark to attribute
+ * generic = 1 when the problem falls back to the generic kernel (for CAPMI_GEMM_X3P: the k-tile
+ * depth, 16 or 32), threads = workgroup size (256, or 512 for the CAPMI_TILE_128_W8 form AUTO picks
+ * for wide convs). Used by the benchmark to attribute
  * time. Any out pointer may be NULL. */
 int capmi_gemm_sk_plan(const capmi_gemm_problem* problem, int amode, int bmode, int tile, int flags, int* bm,
                        int* bn, int* stream_k, int* generic, int* threads);

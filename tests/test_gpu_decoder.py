@@ -72,7 +72,7 @@ def _attention_ref64(enc, h, ps):
 
 def test_soft_attention_and_init_hidden_backward():
     """The standalone SoftAttention / init_hidden_state are differentiable (verdict r01 weak 10):
-    every input and parameter gradient vs fp64 torch autograd, rtol 1e-4 + 1e-5 * max|g|."""
+    every input and parameter gradient vs fp64 torch autograd, rtol 1e-4 + max(1e-5 * max|g|, 1e-6)."""
     from models.attention import SoftAttention
     g = torch.Generator().manual_seed(5)
     B, P, E, D, A = 3, 13, 64, 32, 48
@@ -91,9 +91,11 @@ def test_soft_attention_and_init_hidden_backward():
     ((a64 * r1.double()).sum() + (al64 * r2.double()).sum()).backward()
     torch.cuda.synchronize()
 
-    def close(got, want, name):
+    def close(got, want, name, floor=1e-6):
+        # floor: d full_att.bias is exactly 0 (softmax is shift-invariant); fp32 leaves ~1e-7
         want = want.float()
-        assert_close(got.detach().cpu().reshape(want.shape), want, 1e-4, 1e-5 * float(want.abs().max()), name)
+        atol = max(1e-5 * float(want.abs().max()), floor)
+        assert_close(got.detach().cpu().reshape(want.shape), want, 1e-4, atol, name)
     close(awe, a64.detach(), "awe")
     close(alpha, al64.detach(), "alpha")
     close(e_d.grad, e64.grad, "d enc")

@@ -81,8 +81,12 @@ def test_gemm_sk_plan_on_host():
     rc, (bm, bn, sk, generic, nt) = plan(256, flags=4)
     assert rc == 0 and (bm, bn, generic, nt) == (128, 128, 0, 512)
     assert plan(64, flags=4)[1][1] == 64
+    # X3P reports its k-tile depth in `generic`: 32 + stream-K for 98 tiles (< 256 CUs), 16 (two
+    # workgroups per CU, data-parallel) for 1568 tiles (0.77 of 4 rounds of 512 slots)
     rc, (bm, bn, sk, generic, nt) = plan(256, flags=8)
-    assert rc == 0 and (bm, bn, generic, nt) == (256, 128, 0, 512) and sk == 1  # 98 tiles < 256 CUs
+    assert rc == 0 and (bm, bn, generic, nt) == (256, 128, 32, 512) and sk == 1
+    rc, (bm, bn, sk, generic, nt) = plan(256, flags=8, M=200704)
+    assert rc == 0 and (bm, bn, generic, nt) == (256, 128, 16, 512) and sk == 0
     assert plan(256, flags=8, Cin=20)[0] == 1001  # Cin % 32 != 0
 
     def wgrad_plan(Cout, Cin, k):
