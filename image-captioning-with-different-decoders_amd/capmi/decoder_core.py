@@ -135,12 +135,22 @@ class DecoderCore:
 
     # ------------------------------------------------------------------ forward
     def forward(self, p, enc, caps, decode_lengths, *, dropout_p=0.0, training=False, seed=0,
-                seed_dev=None, emb_dense=None):
+                seed_dev=None, emb_dense=None, dup=1):
         """p: dict name->tensor (PNAMES). enc: (B,P,E) contiguous fp32. caps: (B,L) int64.
         emb_dense: optional (B, Le, M) fp32 word embeddings used instead of the embedding table
         (the BERT variant, :242-244; frozen: no gradient flows into it).
-        Returns (predictions (B,T,V), alphas (B,T,P), state)."""
+        dup > 1: enc holds the F*F DISTINCT rows of pixel-duplicated features (the reference's
+        AdaptiveAvgPool2d of an F x F map to (F dup)^2 positions, models/encoder.py:92,108, repeats
+        every pixel dup x dup times). Everything runs on the distinct rows -- the softmax over the
+        (F dup)^2 positions is the softmax over the distinct ones / dup^2, the context sum and the
+        init mean are unchanged -- and only the returned alphas are expanded.
+        Returns (predictions (B,T,V), alphas (B,T,P) [P = (F dup)^2 with dup], state)."""
         B, P, E = enc.shape
+        F = 0
+        if dup > 1:
+            F = int(round(P ** 0.5))
+            if F * F != P:
+                raise ValueError(f"dup={dup} needs a square map of distinct rows (got {P})")
         L = caps.shape[1]
         T = max(decode_lengths)
         A = p["attention.enc_att.weight"].shape[0]
@@ -177,7 +187,7 @@ class DecoderCore:
         self._gemm_into(ws, ws.XEMB, 4 * D, T * B, 4 * D, M, ws.X, X, W_ih, X, AK, BW,
                         bias=p["decode_step.bias_ih"], bias2=p["decode_step.bias_hh"])
 
-        alphas = torch.empty(B, T, P, device=enc.device, dtype=torch.float32)
+        alphas = torch.empty(B, T, P, device=enc.device, dtype=torch.float32)  # over the rows enc holds
         s_a, s_g, s_hh = dm.s_h
         W_ih_awe = W_ih[:, M:]
         wf = p["attention.full_att.weight"]
@@ -211,10 +221,14 @@ class DecoderCore:
                         c_r1=B, c_s2=V)
         if ragged:
             K.mask_rows_tb(preds, bt_dev, T, B, V, T * V, B, V)
+        alphas_out = alphas
+        if dup > 1:
+            alphas_out = torch.empty(B, T, P * dup * dup, device=enc.device, dtype=torch.float32)
+            K.att_alpha_expand(alphas, B * T, F, dup, alphas_out)
         state = dict(dm=dm, ws=ws, enc=enc, caps=caps, bt=bt, bt_dev=bt_dev, ragged=ragged, alphas=alphas,
-                     dense_emb=emb_dense is not None,
+                     dense_emb=emb_dense is not None, dup=dup, F=F,
                      Hd=Hd, dropout_p=dropout_p if training else 0.0, seed=seed, seed_dev=seed_dev)
-        return preds, alphas, state
+        return preds, alphas_out, state
 
     # ------------------------------------------------------------------ backward
     def backward(self, p, st, grads, dpred, dpred_time_major=False, dreg=None, dalphas=None,
@@ -231,6 +245,10 @@ class DecoderCore:
         all-reduce is issued there and runs beside the loop)."""
         dm, ws = st["dm"], st["ws"]
         B, T, L, P, A, D, M, V, E, X = dm.B, dm.T, dm.L, dm.P, dm.A, dm.D, dm.M, dm.V, dm.E, dm.X
+        if st.get("dup", 1) > 1 and (dalphas is not None or denc is not None):
+            # the fused path's regulariser gradient arrives on the distinct rows (decoder_fn); a
+            # per-position alphas gradient or d(encoder_out) needs the full (B, P) layout
+            raise ValueError("capmi decoder: dalphas / denc need the full (non-deduplicated) features")
         enc, bt = st["enc"], st["bt"]
         need = set(grads) if need is None else set(need)
         W_ih = p["decode_step.weight_ih"]

@@ -119,6 +119,7 @@ class FusedStepState:
             self.dlogits = torch.empty(T * B, V, **f)
             self.reg = torch.empty(K.alpha_reg_parts(B, P), **f)
             self.dreg = torch.empty(B, P, **f)
+            self.dreg_q = torch.empty(B, P, **f)  # the distinct rows' share (dup > 1), <= P
             self.loss = torch.empty(1, **f)
             self.key = key
         return self
@@ -128,24 +129,29 @@ _FS = FusedStepState()
 
 
 def fused_loss_and_grads(dec, encoder_out, captions, caption_lengths, alpha_c, grads, need=None,
-                         seed_dev=None, denc=None, on_fc_grads=None):
+                         seed_dev=None, denc=None, on_fc_grads=None, dup=1):
     """Forward + loss + backward of one decoder training step (models/attention.py:393-420).
 
     Writes d(loss)/d(param) into ``grads`` (name -> tensor, e.g. the optimizer's flat
     views); returns (loss (1,) device tensor, predictions, alphas). ``seed_dev``: an int64
     device counter driving the dropout mask (graph-replayable); else a host seed is drawn.
     ``denc``: optional (B,14,14,2048)-sized buffer receiving d(loss)/d(encoder_out) (fine-tune).
-    ``on_fc_grads``: callback once the fc gradients are final (before the BPTT loop)."""
+    ``on_fc_grads``: callback once the fc gradients are final (before the BPTT loop).
+    ``dup`` > 1: ``encoder_out`` is the (B, F, F, E) map whose pooled (B, F dup, F dup, E) form the
+    reference would decode (every pooled pixel repeated dup x dup times, DecoderCore.forward); the
+    loss, predictions and alphas (B, T, (F dup)^2) are the pooled form's."""
     enc, caps = _prep_inputs(dec, encoder_out, captions)
     p = decoder_params(dec)
     decode_lengths = [int(l) - 1 for l in caption_lengths]
     drop = dec.dropout.p if dec.training else 0.0
     host_seed = 0x5EED if seed_dev is not None else (_seed() if drop > 0 else 0)
     preds, alphas, st = CORE.forward(p, enc, caps, decode_lengths, dropout_p=drop, training=dec.training,
-                                     seed=host_seed, seed_dev=seed_dev, emb_dense=dense_embeddings(dec, caps))
+                                     seed=host_seed, seed_dev=seed_dev, emb_dense=dense_embeddings(dec, caps),
+                                     dup=dup)
     _GEN[0] += 1
     dm = st["dm"]
-    B, T, V, P, L = dm.B, dm.T, dm.V, dm.P, dm.L
+    B, T, V, L = dm.B, dm.T, dm.V, dm.L
+    P = alphas.shape[2]  # the reference's positions ((F dup)^2 with dup)
     fs = _FS.get(B, T, V, P, enc.device)
     nrows = sum(decode_lengths)
     # CE over the packed rows (no ignore_index: pads are scored, Q2) -> time-major dlogits
@@ -153,11 +159,17 @@ def fused_loss_and_grads(dec, encoder_out, captions, caption_lengths, alpha_c, g
                  dl_time_major=True)
     K.alpha_reg(alphas, B, T, P, alpha_c, fs.reg, fs.dreg)
     K.loss_finalize(fs.loss_rows, B * T, nrows, fs.reg, fs.loss)
+    dreg = fs.dreg
+    if dup > 1:
+        # d(loss)/d(alpha_q) of a distinct row: the group's dup^2 equal positions each contribute
+        # dreg_p / dup^2 -- the value at one representative
+        K.att_dup_pick(fs.dreg, B, st["F"], dup, fs.dreg_q)
+        dreg = fs.dreg_q
     g = {n: grads[n] for n in (need if need is not None else grads)
          if not (st["dense_emb"] and n == "embedding.weight")}
     if "attention.full_att.weight" in g:
         g["attention.full_att.weight"] = g["attention.full_att.weight"].view(-1)
-    CORE.backward(p, st, g, fs.dlogits, dpred_time_major=True, dreg=fs.dreg,
+    CORE.backward(p, st, g, fs.dlogits, dpred_time_major=True, dreg=dreg,
                   denc=None if denc is None else denc.view(B, P, -1), on_fc_grads=on_fc_grads)
     return fs.loss, preds, alphas
 

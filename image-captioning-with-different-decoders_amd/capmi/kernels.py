@@ -497,6 +497,20 @@ def lstm_cell_bwd(dhd, dh_part, S, slab, dc_in, act, c_prev, c_cur, B, D, bt, dg
          ptr(c_cur), B, D, bt, ptr(dgates), ptr(dc_out), stream())
 
 
+def att_alpha_expand(aq, rows, F, d, ap):
+    """alphas over the F*F distinct rows -> over the reference's (F d)^2 positions (/ d^2)."""
+    _cuda(aq, ap)
+    assert aq.numel() >= rows * F * F and ap.numel() >= rows * (F * d) ** 2
+    call("capmi_att_alpha_expand", ptr(aq), rows, F, d, ptr(ap), stream())
+
+
+def att_dup_pick(inp, B, F, d, out):
+    """out[b][qi][qj] = inp[b][qi*d][qj*d] (one representative per duplicated group)."""
+    _cuda(inp, out)
+    assert inp.numel() >= B * (F * d) ** 2 and out.numel() >= B * F * F
+    call("capmi_att_dup_pick", ptr(inp), B, F, d, ptr(out), stream())
+
+
 def att_ctx_bwd(part, S, slab, gate, awe, enc, B, P, E, dgp, dalpha, dawe_out=None):
     _cuda(part, gate, awe, enc, dgp, dalpha, dawe_out)
     call("capmi_att_ctx_bwd", ptr(part), S, slab, ptr(gate), ptr(awe), ptr(enc), B, P, E, ptr(dgp),

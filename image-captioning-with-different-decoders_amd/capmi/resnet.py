@@ -117,6 +117,28 @@ class _Packed:
         return ent[2]
 
 
+def feature_hw(H, W):
+    """Side of ResNet-101's layer4 map for an H x W image (conv1 7x7/2, maxpool 3x3/2, three
+    stride-2 stages): 224 -> 7."""
+    def down(x, k, st, pad):
+        return (x + 2 * pad - k) // st + 1
+    h, w = down(down(H, 7, 2, 3), 3, 2, 1), down(down(W, 7, 2, 3), 3, 2, 1)
+    for _ in range(3):
+        h, w = down(h, 3, 2, 1), down(w, 3, 2, 1)
+    return h, w
+
+
+def pool_dup(H, W, out_hw):
+    """d when AdaptiveAvgPool2d(out_hw) of the H x W image's layer4 map only repeats pixels
+    (out side = d x map side, d integer, equal in both directions; every window holds one input
+    pixel, so the pooled value IS that pixel), else 1."""
+    fh, fw = feature_hw(H, W)
+    oh, ow = out_hw
+    if fh <= 0 or fw <= 0 or oh % fh or ow % fw or oh // fh != ow // fw:
+        return 1
+    return oh // fh
+
+
 class EncoderRunner:
     """Launch plan for the frozen ResNet-101 conv stack (children()[:-2] of torchvision's
     resnet101) on NHWC fp32 activations. Buffers are cached per input shape."""
@@ -364,7 +386,9 @@ class EncoderRunner:
     @torch.no_grad()
     def forward(self, net, imgs, out_hw=(14, 14), train=True, out=None):
         """imgs (N,3,H,W) fp32 contiguous on the device -> (N, OH, OW, 2048) NHWC (= the
-        reference's adaptive_pool + permute(0,2,3,1), models/encoder.py:107-110)."""
+        reference's adaptive_pool + permute(0,2,3,1), models/encoder.py:107-110). out_hw=None:
+        the layer4 map itself (N, H/32, W/32, 2048), written by the last block straight into
+        ``out`` (the decoder's distinct rows when the pool only repeats pixels, feature_hw)."""
         if imgs.dtype != torch.float32 or not imgs.is_contiguous():
             raise TypeError("encoder input must be contiguous float32 (N,3,H,W)")
         N, C0, H, W = imgs.shape
@@ -379,8 +403,12 @@ class EncoderRunner:
         x, xo = ws["x"], ws["out"]
         H, W, Cx = Hp, Wp, 64
         bns = []
+        direct = out_hw is None and out is not None
+        n4 = len(net.layer4)
         for li in range(1, 5):
             for bi, blk in enumerate(getattr(net, f"layer{li}")):
+                if direct and li == 4 and bi == n4 - 1:
+                    xo = out  # the last block's output is the result
                 tag = f"layer{li}.{bi}"
                 _, _, r1 = self._conv(tag + ".conv1", x, blk.conv1, ws["y1"], N, H, W, train)
                 ss1 = self._bn(ws, blk.bn1, r1, train)
@@ -404,6 +432,8 @@ class EncoderRunner:
             nbt = [m.num_batches_tracked for m in bns if m.num_batches_tracked is not None]
             if nbt:
                 torch._foreach_add_(nbt, 1)
+        if out_hw is None:
+            return x if direct else x.view(N, H, W, Cx).clone()
         OH, OW = out_hw
         if out is None:
             out = torch.empty(N, OH, OW, Cx, device=imgs.device, dtype=torch.float32)

@@ -35,6 +35,7 @@ from . import decoder_fn as DF
 from . import dist as cdist
 from . import kernels as K
 from .decoder_core import PNAMES
+from .resnet import feature_hw, pool_dup
 
 
 class AttentionTrainStep:
@@ -52,6 +53,9 @@ class AttentionTrainStep:
         dev = next(decoder.parameters()).device
         self.ctx = ctx or cdist.DistCtx(device=dev)
         self.alpha_c = alpha_c
+        # the decoder on the distinct rows of pixel-duplicated features (the 7x7 map the reference
+        # pools to 14x14, DecoderCore.forward); CAPMI_ATT_DEDUP=0 decodes the pooled map (A/B)
+        self.dedup = os.environ.get("CAPMI_ATT_DEDUP", "1") != "0"
         self.overlap = overlap and self.ctx.distributed and not graph
         self.graph_mode = graph
         self._pending = None
@@ -92,6 +96,26 @@ class AttentionTrainStep:
 
     def _grads(self):
         return {n: self.params[n].grad for n in self.need}
+
+    def _feat_layout(self, imgs):
+        """(feature buffer shape, dup) for a batch: the layer4 map when the encoder's pool only
+        repeats its pixels (dup = 2 at 224x224: 7x7 -> 14x14), else the pooled map (dup = 1)."""
+        N, _, H, W = imgs.shape
+        enc = self.encoder
+        out_hw = enc._out_hw() if hasattr(enc, "_out_hw") else (14, 14)
+        d = 1
+        if self.dedup and not self.fine_tune and hasattr(enc, "_runner") and not enc._runner.bf16:
+            d = pool_dup(H, W, out_hw)
+        if d > 1:
+            fh, fw = feature_hw(H, W)
+            return (N, fh, fw, 2048), d
+        return (N, out_hw[0], out_hw[1], 2048), 1
+
+    def _encode_into(self, imgs, out, dup):
+        if dup > 1:
+            self.encoder.forward_into(imgs, out, pooled=False)
+        else:
+            self.encoder.forward_into(imgs, out)
 
     def _snapshot(self):
         """Device state a capture warm-up must not change: the encoder's BatchNorm buffers
@@ -155,21 +179,26 @@ class AttentionTrainStep:
         if self.fine_tune:
             return self._body_ft(imgs, captions, caption_lengths, with_update)
         K.counter_add(self.seed_dev, 1)
-        feats = self.encoder(imgs)
+        shape, dup = self._feat_layout(imgs)
+        if hasattr(self.encoder, "forward_into"):
+            feats = torch.empty(shape, device=imgs.device, dtype=torch.float32)
+            self._encode_into(imgs, feats, dup)
+        else:
+            feats, dup = self.encoder(imgs), 1
         self._apply_pending()
         loss, _, _ = DF.fused_loss_and_grads(self.decoder, feats, captions, caption_lengths,
                                              self.alpha_c, self._grads(), need=self.need,
-                                             seed_dev=self.seed_dev)
+                                             seed_dev=self.seed_dev, dup=dup)
         if with_update:
             self.opt.step()
         return loss
 
-    def _dec_body(self, feats, captions, caption_lengths, with_update, on_fc=None):
+    def _dec_body(self, feats, captions, caption_lengths, with_update, on_fc=None, dup=1):
         K.counter_add(self.seed_dev, 1)
         self._apply_pending()
         loss, _, _ = DF.fused_loss_and_grads(self.decoder, feats, captions, caption_lengths,
                                              self.alpha_c, self._grads(), need=self.need,
-                                             seed_dev=self.seed_dev, on_fc_grads=on_fc)
+                                             seed_dev=self.seed_dev, on_fc_grads=on_fc, dup=dup)
         if with_update:
             self.opt.step()
         return loss
@@ -182,15 +211,15 @@ class AttentionTrainStep:
         self.replayed = []
         slot = self._slot
         self._slot ^= 1
-        N, _, H, W = imgs.shape
-        if self._feats[slot] is None or self._feats[slot].shape[0] != N:
-            self._feats[slot] = torch.empty(N, 14, 14, 2048, device=imgs.device, dtype=torch.float32)
+        shape, dup = self._feat_layout(imgs)
+        if self._feats[slot] is None or tuple(self._feats[slot].shape) != shape:
+            self._feats[slot] = torch.empty(shape, device=imgs.device, dtype=torch.float32)
         # the slot's previous reader is the decoder of call k-1
         self.s_enc.wait_stream(cur)
         if self._ev_dec is not None:
             self.s_enc.wait_event(self._ev_dec)
         with torch.cuda.stream(self.s_enc):
-            self.encoder.forward_into(imgs, self._feats[slot])
+            self._encode_into(imgs, self._feats[slot], dup)
             ev_enc = torch.cuda.Event()
             ev_enc.record(self.s_enc)
         # the caller's tensors are read on the side streams: keep their blocks from being handed
@@ -198,7 +227,7 @@ class AttentionTrainStep:
         imgs.record_stream(self.s_enc)
         captions.record_stream(self.s_dec)
         loss = self._pipe_decoder()
-        self._pend = ("eager", slot, captions, caption_lengths, ev_enc)
+        self._pend = ("eager", slot, captions, caption_lengths, ev_enc, dup)
         return loss
 
     # ------------------------------------------------------- pipelined graphs
@@ -211,7 +240,8 @@ class AttentionTrainStep:
         N = imgs.shape[0]
         upd = not self.ctx.distributed
         snap = self._snapshot()
-        self._feats = [torch.empty(N, 14, 14, 2048, device=dev, dtype=torch.float32) for _ in range(2)]
+        shape, dup = self._feat_layout(imgs)
+        self._feats = [torch.empty(shape, device=dev, dtype=torch.float32) for _ in range(2)]
         pg = []
         for slot in range(2):
             pg.append({"imgs": imgs.detach().clone(), "caps": captions.detach().clone(),
@@ -221,8 +251,8 @@ class AttentionTrainStep:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
-                self.encoder.forward_into(pg[0]["imgs"], self._feats[0])
-                self._dec_body(self._feats[0], pg[0]["caps"], pg[0]["lens"], with_update=False)
+                self._encode_into(pg[0]["imgs"], self._feats[0], dup)
+                self._dec_body(self._feats[0], pg[0]["caps"], pg[0]["lens"], with_update=False, dup=dup)
         torch.cuda.current_stream().wait_stream(s)
         self._restore(snap)
         for slot in range(2):
@@ -231,7 +261,7 @@ class AttentionTrainStep:
             if self.capture_hook is not None:
                 self.capture_hook(f"enc{slot}")
             with torch.cuda.graph(g):
-                self.encoder.forward_into(st["imgs"], self._feats[slot])
+                self._encode_into(st["imgs"], self._feats[slot], dup)
             st["g_enc"] = g
             st["feats"] = self._feats[slot]  # the graphs hold raw pointers: keep the buffer alive
             if self.capture_hook is not None:
@@ -239,13 +269,15 @@ class AttentionTrainStep:
             if upd:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    st["loss"] = self._dec_body(self._feats[slot], st["caps"], st["lens"], with_update=True)
+                    st["loss"] = self._dec_body(self._feats[slot], st["caps"], st["lens"], with_update=True,
+                                                dup=dup)
                 st["g_dec"] = g
             else:
                 # data parallel: two graphs cut where the fc gradients are final, so their all-reduce
                 # is issued between the replays and runs beside the backward-through-time graph
                 st["loss"], st["g_dec"], st["g_dec2"] = self._capture_split(
-                    lambda cut: self._dec_body(self._feats[slot], st["caps"], st["lens"], with_update=False, on_fc=cut))
+                    lambda cut: self._dec_body(self._feats[slot], st["caps"], st["lens"], with_update=False, on_fc=cut,
+                                               dup=dup))
         torch.cuda.synchronize()
         self._pg, self._pg_key = pg, key
 
@@ -308,7 +340,7 @@ class AttentionTrainStep:
             ev_enc.record(self.s_enc)
         self.replayed = [f"enc{slot}"]
         loss = self._pipe_decoder()
-        self._pend = ("graph", slot, captions, caption_lengths, ev_enc)
+        self._pend = ("graph", slot, captions, caption_lengths, ev_enc, None)
         return loss
 
     def _pipe_decoder(self):
@@ -317,7 +349,7 @@ class AttentionTrainStep:
         # dispatch on how the pending batch's encoder was launched (a ragged batch runs eagerly
         # between graph-replayed ones)
         if self._pend[0] == "graph":
-            _, pslot, _, _, ev = self._pend
+            _, pslot, _, _, ev, _ = self._pend
             self._pend = None
             self.s_dec.wait_event(ev)
             self.s_dec.wait_stream(torch.cuda.current_stream())
@@ -333,7 +365,7 @@ class AttentionTrainStep:
                 self._ev_dec = torch.cuda.Event()
                 self._ev_dec.record(self.s_dec)
             return loss
-        _, pslot, caps, lens, ev = self._pend
+        _, pslot, caps, lens, ev, dup = self._pend
         self._pend = None
         self.s_dec.wait_event(ev)
         self.s_dec.wait_stream(torch.cuda.current_stream())
@@ -342,10 +374,10 @@ class AttentionTrainStep:
                 fc_works = []
                 loss = self._dec_body(self._feats[pslot], caps, lens, with_update=False,
                                       on_fc=lambda: fc_works.extend(
-                                          cdist.allreduce_mean_(self._b_fc, self.ctx, async_op=True)))
+                                          cdist.allreduce_mean_(self._b_fc, self.ctx, async_op=True)), dup=dup)
                 self._dp_update(fc_works)
             else:
-                loss = self._dec_body(self._feats[pslot], caps, lens, with_update=True)
+                loss = self._dec_body(self._feats[pslot], caps, lens, with_update=True, dup=dup)
             loss = loss.detach().clone()  # the loss buffer is reused by the next decoder step
             self._ev_dec = torch.cuda.Event()
             self._ev_dec.record(self.s_dec)

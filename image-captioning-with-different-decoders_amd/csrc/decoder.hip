@@ -570,6 +570,58 @@ __global__ void __launch_bounds__(256) att_ctx_bwd_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Pixel-duplicated encoder features. The reference pools the 7x7 ResNet map to 14x14
+// (models/encoder.py:92,108: AdaptiveAvgPool2d(14)); when the output side is a multiple d of the
+// input side every pooled pixel IS one input pixel, repeated d x d times. The decoder then runs on
+// the F*F distinct rows: softmax over the (F d)^2 positions equals the softmax over the distinct
+// ones divided by d^2, and the context sum is unchanged.
+// ---------------------------------------------------------------------------------
+// ap[r][pi][pj] = aq[r][pi / d][pj / d] * scale   (rows r = b*T + t; scale = 1 / d^2)
+__global__ void __launch_bounds__(256) att_alpha_expand_kernel(const float* __restrict__ aq, long long rows,
+                                                               int F, int d, float scale,
+                                                               float* __restrict__ ap) {
+  const int S = F * d, P = S * S, Q = F * F;
+  const long long n = rows * P;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const long long r = i / P;
+    const int p = (int)(i - r * P), pi = p / S, pj = p - pi * S;
+    ap[i] = aq[r * Q + (pi / d) * F + pj / d] * scale;
+  }
+}
+
+// out[b][qi][qj] = in[b][qi d][qj d]: one representative of each duplicated group
+__global__ void __launch_bounds__(256) att_dup_pick_kernel(const float* __restrict__ in, int B, int F, int d,
+                                                           float* __restrict__ out) {
+  const int S = F * d, Q = F * F;
+  const long long n = (long long)B * Q;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const long long b = i / Q;
+    const int q = (int)(i - b * Q), qi = q / F, qj = q - qi * F;
+    out[i] = in[b * S * S + (long long)(qi * d) * S + qj * d];
+  }
+}
+
+extern "C" int capmi_att_alpha_expand(const float* aq, long long rows, int F, int d, float* ap, void* stream) {
+  CAPMI_REQUIRE(aq && ap && rows >= 0 && F > 0 && d > 0, CAPMI_EINVAL);
+  const long long n = rows * (long long)(F * d) * (F * d);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(att_alpha_expand_kernel, dim3((unsigned)std::min<long long>(cdiv(n, 256), 4096)), dim3(256),
+                     0, as_stream(stream), aq, rows, F, d, 1.0f / (float)(d * d), ap);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int capmi_att_dup_pick(const float* in, int B, int F, int d, float* out, void* stream) {
+  CAPMI_REQUIRE(in && out && B >= 0 && F > 0 && d > 0, CAPMI_EINVAL);
+  const long long n = (long long)B * F * F;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(att_dup_pick_kernel, dim3((unsigned)std::min<long long>(cdiv(n, 256), 4096)), dim3(256), 0,
+                     as_stream(stream), in, B, F, d, out);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int capmi_att_ctx_bwd(const float* part, int S, long long slab, const float* gate,
                                  const float* awe, const float* enc, int B, int P, int E,
                                  float* dgp, float* dalpha, float* dawe_out, void* stream) {

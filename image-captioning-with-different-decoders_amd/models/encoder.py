@@ -201,14 +201,16 @@ class EncoderAttention(nn.Module):
         ``grads`` (dict id(param) -> tensor)."""
         self._ft().backward(dfeat, grads, hook=hook)
 
-    def forward_into(self, imgs, out):
+    def forward_into(self, imgs, out, pooled=True):
         """forward() writing the (B,14,14,2048) features into a caller-owned buffer (the
-        pipelined training step keeps two of them)."""
+        pipelined training step keeps two of them). pooled=False: the (B,7,7,2048) layer4 map
+        before adaptive_pool -- the distinct rows of the pooled features when the pool only
+        repeats pixels (capmi.resnet.pool_dup; the training step's decoder runs on them)."""
         _check_frozen(self.resnet)
-        out_hw = self.adaptive_pool.output_size
-        out_hw = (out_hw, out_hw) if isinstance(out_hw, int) else tuple(out_hw)
-        return self._runner.forward(_ResNetView(self.resnet), imgs.contiguous(), out_hw,
-                                    train=self.training, out=out)
+        if not pooled and self._runner.bf16:
+            raise NotImplementedError("capmi: the unpooled map is an fp32-path output")
+        return self._runner.forward(_ResNetView(self.resnet), imgs.contiguous(),
+                                    self._out_hw() if pooled else None, train=self.training, out=out)
 
     def fine_tune(self, on=True):
         for conv_block in list(self.resnet.children())[5:]:

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 10
+#define CAPMI_ABI_VERSION 11
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -321,6 +321,14 @@ int capmi_lstm_cell_bwd(const float* dhd, const float* dh_part, int S, long long
                         const float* dc_in, const float* act, const float* c_prev,
                         const float* c_cur, int B, int D, int bt, float* dgates, float* dc_out,
                         void* stream);
+/* Pixel-duplicated features (models/encoder.py:92,108, AdaptiveAvgPool2d of an F x F map to
+ * (F d) x (F d) with integer d: every pooled pixel is one input pixel repeated d x d times). The
+ * decoder runs on the F*F distinct rows; these map its results back to the reference's positions.
+ * alpha expansion: ap[r][pi][pj] = aq[r][pi/d][pj/d] / d^2 for rows r (= b*T + t), aq (rows, F*F). */
+int capmi_att_alpha_expand(const float* aq, long long rows, int F, int d, float* ap, void* stream);
+/* representatives: out[b][qi][qj] = in[b][qi*d][qj*d], in (B, (F d)^2), out (B, F*F) -- the
+ * regulariser's d(loss)/d(alpha), equal over a duplicated group, as seen by the distinct rows */
+int capmi_att_dup_pick(const float* in, int B, int F, int d, float* out, void* stream);
 /* d(awe_g) = sum_s part[s]; dawe = d*gate; dgp = d*awe*gate*(1-gate) (if gate != NULL)
  * dalpha[b][p] = dawe . enc[b][p][:]; dawe -> dawe_out[b][E] when non-NULL (encoder fine-tune) */
 int capmi_att_ctx_bwd(const float* part, int S, long long slab, const float* gate,

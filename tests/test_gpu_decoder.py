@@ -197,6 +197,53 @@ def test_fused_train_step_matches_oracle(cfg):
     _ = rnew
 
 
+@pytest.mark.parametrize("F,d,cfg", [
+    (7, 2, dict(A=512, D=512, M=512, V=8100, B=4, L=25, seed=44)),  # 224x224: 7x7 -> 14x14
+    (2, 7, dict(A=32, D=32, M=16, V=50, B=3, L=7, seed=45))])       # 64x64: 2x2 -> 14x14
+def test_fused_dedup_matches_oracle(F, d, cfg):
+    """The decoder on the F*F distinct rows of pixel-duplicated features (dup = d) against the
+    oracle run on the reference's pooled (F d) x (F d) map: loss, predictions, alphas over all
+    positions and every gradient, under the rules of test_fused_train_step_matches_oracle."""
+    from capmi import decoder_fn as DF
+    dec, p = make_decoder(cfg["A"], cfg["D"], cfg["M"], cfg["V"], cfg["seed"], DEV)
+    dec.train()
+    B, L, V = cfg["B"], cfg["L"], cfg["V"]
+    g = torch.Generator().manual_seed(cfg["seed"])
+    distinct = torch.rand(B, F, F, 2048, generator=g)  # post-ReLU-like features
+    pooled = distinct.repeat_interleave(d, 1).repeat_interleave(d, 2)  # AdaptiveAvgPool2d(F d) of F x F
+    caps = gen.captions(cfg["seed"], B, L, V, None)
+    trainable = [n for n, q in dec.named_parameters() if q.requires_grad]
+    grads = {n: torch.zeros_like(q) for n, q in dec.named_parameters() if q.requires_grad}
+    loss, preds, alphas = DF.fused_loss_and_grads(dec, distinct.to(DEV), t(caps, DEV), [L] * B, 1.0, grads, dup=d)
+    torch.cuda.synchronize()
+    assert tuple(alphas.shape) == (B, L - 1, (F * d) ** 2)
+    rloss, rpreds, ralphas, rraw, _, _, _ = R.train_step(p, set(trainable), pooled.reshape(B, -1, 2048),
+                                                         t(caps), [L] * B)
+    assert_close(loss.view(()), rloss, 1e-5, 1e-6, "loss")
+    assert_close(preds, rpreds, LOGIT_RTOL, LOGIT_ATOL, "predictions")
+    assert_close(alphas, ralphas, 0.0, ALPHA_ATOL, "alphas")
+    excused = {n: _grad_check(grads[n].view_as(rraw[n]), rraw[n], "grad " + n) for n in trainable}
+    kinks = set().union(*(excused.get(n, set()) for n in KINK_ROWS))
+    assert len(kinks) <= 2, excused
+
+
+def test_dedup_kernels_exact():
+    """capmi_att_alpha_expand / capmi_att_dup_pick against torch indexing (exact)."""
+    from capmi import kernels as K
+    F, d, B, T = 7, 2, 3, 5
+    aq = torch.rand(B, T, F * F, device=DEV)
+    ap = torch.empty(B, T, (F * d) ** 2, device=DEV)
+    K.att_alpha_expand(aq, B * T, F, d, ap)
+    want = aq.view(B, T, F, F).repeat_interleave(d, 2).repeat_interleave(d, 3).reshape(B, T, -1) / (d * d)
+    torch.cuda.synchronize()
+    assert torch.equal(ap, want)
+    full = torch.rand(B, (F * d) ** 2, device=DEV)
+    out = torch.empty(B, F * F, device=DEV)
+    K.att_dup_pick(full, B, F, d, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, full.view(B, F * d, F * d)[:, ::d, ::d].reshape(B, -1))
+
+
 def test_autograd_path_reference_loss():
     """The reference's own loss code (pack_padded_sequence + CrossEntropyLoss + reg) on top of
     capmi's differentiable forward: gradients reach the parameters through AttentionDecoderFn."""
