@@ -377,7 +377,8 @@ class EncoderRunner:
             nbt = [m.num_batches_tracked for m in bns if m.num_batches_tracked is not None]
             if nbt:
                 torch._foreach_add_(nbt, 1)
-        OH, OW = out_hw
+        # out_hw None: the layer4 map itself, converted to fp32 (an identity "pool")
+        OH, OW = out_hw if out_hw is not None else (H, W)
         if out is None:
             out = torch.empty(N, OH, OW, Cx, device=imgs.device, dtype=torch.float32)
         K.adaptive_avgpool_bf16(x, N, H, W, Cx, OH, OW, out)

@@ -104,7 +104,7 @@ class AttentionTrainStep:
         enc = self.encoder
         out_hw = enc._out_hw() if hasattr(enc, "_out_hw") else (14, 14)
         d = 1
-        if self.dedup and not self.fine_tune and hasattr(enc, "_runner") and not enc._runner.bf16:
+        if self.dedup and not self.fine_tune and hasattr(enc, "_runner"):
             d = pool_dup(H, W, out_hw)
         if d > 1:
             fh, fw = feature_hw(H, W)

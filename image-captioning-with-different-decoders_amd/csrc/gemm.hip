@@ -556,6 +556,15 @@ bool sk_hybrid() {
   }();
   return on;
 }
+// CAPMI_SK_OFF=1: data-parallel grids everywhere (A/B measurement: a persistent stream-K grid
+// holds every CU until it ends, a data-parallel one frees CUs as its tiles retire)
+bool sk_off() {
+  static const bool off = [] {
+    const char* e = getenv("CAPMI_SK_OFF");
+    return e && e[0] == '1' && e[1] == 0;
+  }();
+  return off;
+}
 // the launch capmi_gemm_sk makes for a problem (shared by the launcher and the plan query)
 int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, bool bf16, GemmPlan& g, bool& sk) {
   CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
@@ -592,6 +601,7 @@ int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, bo
     const long long rounds = (tiles + slots - 1) / slots;
     sk = (double)tiles / (double)(rounds * slots) < 0.9;
   }
+  if (sk_off()) sk = false;
   return 0;
 }
 }  // namespace
@@ -678,7 +688,7 @@ int gemm_bf16_io(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
   const long long slots = (long long)cus * 2;
   const int nkt = p.K / 64;
   const long long rounds = (total + slots - 1) / slots;
-  const bool sk = workspace != nullptr && nkt >= 4 && (double)total / (double)(rounds * slots) < 0.9;
+  const bool sk = !sk_off() && workspace != nullptr && nkt >= 4 && (double)total / (double)(rounds * slots) < 0.9;
   if (!sk) return gemm_bf16_launch(a, amode, bm, bn, (int)total, s);
   CAPMI_REQUIRE(aligned16(workspace), CAPMI_EINVAL);
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
@@ -724,7 +734,7 @@ int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gemm
   const long long slots = cu_count();
   const int nkt = p.K / 32;
   const long long rounds = (total + slots - 1) / slots;
-  sk = total > 0 && nkt >= 8 && (double)total / (double)(rounds * slots) < 0.9;
+  sk = !sk_off() && total > 0 && nkt >= 8 && (double)total / (double)(rounds * slots) < 0.9;
   return 0;
 }
 
@@ -784,7 +794,7 @@ int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
   const long long slots = cu_count();
   const int nkt = p.K / 32;
   const long long rounds = (total + slots - 1) / slots;
-  sk = total > 0 && nkt >= 8 && (double)total / (double)(rounds * slots) < 0.9;
+  sk = !sk_off() && total > 0 && nkt >= 8 && (double)total / (double)(rounds * slots) < 0.9;
   return 0;
 }
 

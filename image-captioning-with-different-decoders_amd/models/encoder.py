@@ -207,8 +207,6 @@ class EncoderAttention(nn.Module):
         before adaptive_pool -- the distinct rows of the pooled features when the pool only
         repeats pixels (capmi.resnet.pool_dup; the training step's decoder runs on them)."""
         _check_frozen(self.resnet)
-        if not pooled and self._runner.bf16:
-            raise NotImplementedError("capmi: the unpooled map is an fp32-path output")
         return self._runner.forward(_ResNetView(self.resnet), imgs.contiguous(),
                                     self._out_hw() if pooled else None, train=self.training, out=out)
 

@@ -88,3 +88,23 @@ def test_bn_add_relu_elementwise(rows, C, rbn):
                   res_shift=d[5] if rbn else None)
     torch.cuda.synchronize()
     torch.testing.assert_close(out.cpu(), want, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp32-x3", "bf16"])
+def test_unpooled_map_is_the_distinct_rows(precision):
+    """forward_into(pooled=False) writes the layer4 map whose AdaptiveAvgPool2d(14) is a pure
+    repetition (224x224: 7x7 -> 14x14): the pooled features at (2i, 2j) equal it bit for bit, which
+    is what the training step's distinct-row decoder relies on. Eval mode, so both
+    forwards see the same BatchNorm statistics."""
+    from capmi.resnet import pool_dup
+    enc = _encoder(gen.resnet101_params(72)).eval()
+    enc.set_compute_precision(precision)
+    imgs = torch.rand(2, 3, 224, 224, generator=torch.Generator().manual_seed(3)).to(DEV)
+    assert pool_dup(224, 224, (14, 14)) == 2
+    with torch.no_grad():
+        pooled = torch.empty(2, 14, 14, 2048, device=DEV)
+        enc.forward_into(imgs, pooled)
+        raw = torch.empty(2, 7, 7, 2048, device=DEV)
+        enc.forward_into(imgs, raw, pooled=False)
+    torch.cuda.synchronize()
+    assert torch.equal(pooled, raw.repeat_interleave(2, 1).repeat_interleave(2, 2))
