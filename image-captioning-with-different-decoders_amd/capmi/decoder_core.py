@@ -245,10 +245,12 @@ class DecoderCore:
         all-reduce is issued there and runs beside the loop)."""
         dm, ws = st["dm"], st["ws"]
         B, T, L, P, A, D, M, V, E, X = dm.B, dm.T, dm.L, dm.P, dm.A, dm.D, dm.M, dm.V, dm.E, dm.X
-        if st.get("dup", 1) > 1 and (dalphas is not None or denc is not None):
+        if st.get("dup", 1) > 1 and dalphas is not None:
             # the fused path's regulariser gradient arrives on the distinct rows (decoder_fn); a
-            # per-position alphas gradient or d(encoder_out) needs the full (B, P) layout
-            raise ValueError("capmi decoder: dalphas / denc need the full (non-deduplicated) features")
+            # per-position alphas gradient needs the full (B, P) layout. (denc on the distinct rows
+            # is d(loss)/d(F x F map): the sum over each duplicate group, what the pool's backward
+            # would form.)
+            raise ValueError("capmi decoder: dalphas needs the full (non-deduplicated) features")
         enc, bt = st["enc"], st["bt"]
         need = set(grads) if need is None else set(need)
         W_ih = p["decode_step.weight_ih"]

@@ -135,7 +135,8 @@ def fused_loss_and_grads(dec, encoder_out, captions, caption_lengths, alpha_c, g
     Writes d(loss)/d(param) into ``grads`` (name -> tensor, e.g. the optimizer's flat
     views); returns (loss (1,) device tensor, predictions, alphas). ``seed_dev``: an int64
     device counter driving the dropout mask (graph-replayable); else a host seed is drawn.
-    ``denc``: optional (B,14,14,2048)-sized buffer receiving d(loss)/d(encoder_out) (fine-tune).
+    ``denc``: optional buffer shaped like ``encoder_out`` receiving d(loss)/d(encoder_out) (fine-tune;
+    with ``dup`` the gradient of the F x F map).
     ``on_fc_grads``: callback once the fc gradients are final (before the BPTT loop).
     ``dup`` > 1: ``encoder_out`` is the (B, F, F, E) map whose pooled (B, F dup, F dup, E) form the
     reference would decode (every pooled pixel repeated dup x dup times, DecoderCore.forward); the
@@ -170,7 +171,7 @@ def fused_loss_and_grads(dec, encoder_out, captions, caption_lengths, alpha_c, g
     if "attention.full_att.weight" in g:
         g["attention.full_att.weight"] = g["attention.full_att.weight"].view(-1)
     CORE.backward(p, st, g, fs.dlogits, dpred_time_major=True, dreg=dreg,
-                  denc=None if denc is None else denc.view(B, P, -1), on_fc_grads=on_fc_grads)
+                  denc=None if denc is None else denc.view(B, dm.P, -1), on_fc_grads=on_fc_grads)
     return fs.loss, preds, alphas
 
 

@@ -585,7 +585,8 @@ class FineTuneRunner:
         nbt = [m.num_batches_tracked for m in bns if m.num_batches_tracked is not None]
         if nbt:
             torch._foreach_add_(nbt, 1)
-        OH, OW = out_hw
+        # out_hw None: the layer4 map itself (identity pool: a copy; its backward a copy too)
+        OH, OW = out_hw if out_hw is not None else (H, W)
         if out is None:
             out = torch.empty(N, OH, OW, Cx, device=dev, dtype=torch.float32)
         K.adaptive_avgpool_nhwc(x, N, H, W, Cx, OH, OW, out)

@@ -104,7 +104,7 @@ class AttentionTrainStep:
         enc = self.encoder
         out_hw = enc._out_hw() if hasattr(enc, "_out_hw") else (14, 14)
         d = 1
-        if self.dedup and not self.fine_tune and hasattr(enc, "_runner"):
+        if self.dedup and hasattr(enc, "_runner") and not (self.fine_tune and enc._runner.bf16):
             d = pool_dup(H, W, out_hw)
         if d > 1:
             fh, fw = feature_hw(H, W)
@@ -155,12 +155,13 @@ class AttentionTrainStep:
         producing d(features), encoder backward into the encoder optimizer's gradients."""
         K.counter_add(self.seed_dev, 1)
         self._apply_pending()
-        feats = self.encoder.ft_forward(imgs)
+        _, dup = self._feat_layout(imgs)
+        feats = self.encoder.ft_forward(imgs, pooled=dup == 1)
         if self._denc is None or self._denc.shape != feats.shape:
             self._denc = torch.empty_like(feats)
         loss, _, _ = DF.fused_loss_and_grads(self.decoder, feats, captions, caption_lengths,
                                              self.alpha_c, self._grads(), need=self.need,
-                                             seed_dev=self.seed_dev, denc=self._denc)
+                                             seed_dev=self.seed_dev, denc=self._denc, dup=dup)
         works = []
         if self.ctx.distributed and not self.graph_mode:
             # the decoder's gradients are final: their all-reduce overlaps the encoder backward

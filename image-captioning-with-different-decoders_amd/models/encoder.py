@@ -190,11 +190,13 @@ class EncoderAttention(nn.Module):
             self._ft_runner = ft
         return ft
 
-    def ft_forward(self, imgs, out=None):
-        """Train-mode forward that keeps layer2-4's activations for ft_backward (fp32)."""
+    def ft_forward(self, imgs, out=None, pooled=True):
+        """Train-mode forward that keeps layer2-4's activations for ft_backward (fp32). pooled=False:
+        the layer4 map (see forward_into); ft_backward then takes its gradient."""
         if self._runner.bf16:
             raise NotImplementedError("capmi: the fine-tune path runs fp32 (set_compute_precision('fp32'))")
-        return self._ft().forward(_ResNetView(self.resnet), imgs.contiguous(), self._out_hw(), out=out)
+        return self._ft().forward(_ResNetView(self.resnet), imgs.contiguous(),
+                                  self._out_hw() if pooled else None, out=out)
 
     def ft_backward(self, dfeat, grads, hook=None):
         """d(loss)/d(features) (B,14,14,2048) -> parameter gradients of layer2-4 written into

@@ -214,7 +214,9 @@ def test_fused_dedup_matches_oracle(F, d, cfg):
     caps = gen.captions(cfg["seed"], B, L, V, None)
     trainable = [n for n, q in dec.named_parameters() if q.requires_grad]
     grads = {n: torch.zeros_like(q) for n, q in dec.named_parameters() if q.requires_grad}
-    loss, preds, alphas = DF.fused_loss_and_grads(dec, distinct.to(DEV), t(caps, DEV), [L] * B, 1.0, grads, dup=d)
+    denc = torch.empty(B, F, F, 2048, device=DEV)  # d(loss)/d(F x F map), as the fine-tune step uses it
+    loss, preds, alphas = DF.fused_loss_and_grads(dec, distinct.to(DEV), t(caps, DEV), [L] * B, 1.0, grads,
+                                                  dup=d, denc=denc)
     torch.cuda.synchronize()
     assert tuple(alphas.shape) == (B, L - 1, (F * d) ** 2)
     rloss, rpreds, ralphas, rraw, _, _, _ = R.train_step(p, set(trainable), pooled.reshape(B, -1, 2048),
@@ -225,6 +227,12 @@ def test_fused_dedup_matches_oracle(F, d, cfg):
     excused = {n: _grad_check(grads[n].view_as(rraw[n]), rraw[n], "grad " + n) for n in trainable}
     kinks = set().union(*(excused.get(n, set()) for n in KINK_ROWS))
     assert len(kinks) <= 2, excused
+    # d(map): the reference's d(pooled features) summed over each d x d duplicate group
+    pin = pooled.reshape(B, -1, 2048).clone().requires_grad_()
+    pr, cp, dl, al = R.decoder_forward(dict(p), pin, t(caps), [L] * B)
+    R.attention_loss(pr, cp, dl, al, 1.0).backward()
+    want = pin.grad.view(B, F, d, F, d, 2048).sum((2, 4))
+    assert_close(denc.cpu(), want, 2e-3, 1e-3 * float(want.abs().max()), "d map")
 
 
 def test_dedup_kernels_exact():
