@@ -26,11 +26,15 @@ class DistCtx:
 
     @property
     def distributed(self):
-        return self.world > 1
+        """True when collectives run: world > 1, or a one-rank process group forced with
+        CAPMI_DIST_FORCE=1 (runs the RCCL path, all-reduce over one rank, on a one-GPU box)."""
+        return self.world > 1 or self.backend != ""
 
 
 def init_from_env(device=None, backend=None):
-    """Reads RANK / WORLD_SIZE / LOCAL_RANK (torchrun); MASTER_ADDR defaults to 127.0.0.1."""
+    """Reads RANK / WORLD_SIZE / LOCAL_RANK (torchrun); MASTER_ADDR defaults to 127.0.0.1.
+    CAPMI_DIST_FORCE=1 initialises the process group at world size 1 too (the data-parallel path
+    with its collectives on one GPU: how the RCCL branch is exercised without a second device)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -39,7 +43,8 @@ def init_from_env(device=None, backend=None):
     device = torch.device(device)
     if device.type == "cuda":
         torch.cuda.set_device(device)
-    if world > 1 and not dist.is_initialized():
+    force = os.environ.get("CAPMI_DIST_FORCE", "0") == "1"
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         be = backend or ("nccl" if device.type == "cuda" else "gloo")

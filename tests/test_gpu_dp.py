@@ -55,21 +55,29 @@ def _setup(fine_tune, seed=3):
     return enc, dec, dopt, eopt
 
 
-def _worker(rank, world, port, fine_tune, q, graph=False):
+class _Probe:
+    """The attributes AttentionTrainStep._feat_layout reads, for a fine-tune step."""
+
+    def __init__(self, enc):
+        self.encoder, self.dedup, self.fine_tune = enc, os.environ.get("CAPMI_ATT_DEDUP", "1") != "0", True
+
+
+def _worker(rank, world, port, fine_tune, q, graph=False, backend="gloo"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.join(os.path.dirname(here), "image-captioning-with-different-decoders_amd"),
               os.path.dirname(here), os.path.join(here, "golden"), here):
         sys.path.insert(0, p)
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port))
+                      MASTER_PORT=str(port), CAPMI_DIST_FORCE="1")
     try:
         import gen
         from capmi import decoder_fn as DF
         from capmi import dist as cdist
         from capmi.train_step import AttentionTrainStep
         from helpers import t
-        ctx = cdist.init_from_env("cuda", backend="gloo")
+        ctx = cdist.init_from_env("cuda", backend=backend)
+        assert ctx.distributed and ctx.backend == backend, (ctx, backend)
         B, L, V = 2, 6, 50
         imgs = t(gen.images(11, B * world, 64, 64), "cuda")
         caps = t(gen.captions(11, B * world, L, V), "cuda")
@@ -80,9 +88,12 @@ def _worker(rank, world, port, fine_tune, q, graph=False):
             sl = slice(r * B, (r + 1) * B)
             g = {n: torch.zeros_like(q) for n, q in dec.named_parameters() if q.requires_grad}
             if fine_tune:
-                f = enc.ft_forward(imgs[sl])
+                # same feature layout as the step (the distinct-row map when the pool only repeats
+                # pixels), so the two differ only in the all-reduce
+                _, dup = AttentionTrainStep._feat_layout(_Probe(enc), imgs[sl])
+                f = enc.ft_forward(imgs[sl], pooled=dup == 1)
                 denc = torch.empty_like(f)
-                DF.fused_loss_and_grads(dec, f, caps[sl], [L] * B, 1.0, g, denc=denc)
+                DF.fused_loss_and_grads(dec, f, caps[sl], [L] * B, 1.0, g, denc=denc, dup=dup)
                 eg = {id(q): torch.zeros_like(q) for q in enc.parameters() if q.requires_grad}
                 enc.ft_backward(denc, eg)
                 ref_e.append(torch.cat([eg[id(q)].reshape(-1) for q in enc.parameters() if q.requires_grad]))
@@ -101,12 +112,12 @@ def _worker(rank, world, port, fine_tune, q, graph=False):
         step.flush()
         torch.cuda.synchronize()
         got_d = torch.cat([q.grad.reshape(-1) for q in dec.parameters() if q.requires_grad])
-        want_d = (ref_d[0] + ref_d[1]) / 2
+        want_d = sum(ref_d) / world
         err_d = float((got_d - want_d).abs().max() / want_d.abs().max())
         err_e = 0.0
         if fine_tune:
             got_e = torch.cat([q.grad.reshape(-1) for q in enc.parameters() if q.requires_grad])
-            want_e = (ref_e[0] + ref_e[1]) / 2
+            want_e = sum(ref_e) / world
             err_e = float((got_e - want_e).abs().max() / want_e.abs().max())
         p = torch.cat([q.detach().reshape(-1) for q in dec.parameters()]).cpu()
         q.put((rank, err_d, err_e, p))
@@ -140,3 +151,21 @@ def test_dp_two_ranks_one_gpu(fine_tune, graph):
         assert res[r][1] < 1e-6, ("decoder grads", res[r][1])
         assert res[r][2] < 1e-6, ("encoder grads", res[r][2])
     assert torch.equal(res[0][3], res[1][3])  # identical parameters after the update
+
+
+@pytest.mark.parametrize("fine_tune,graph", [(False, False), (False, True), (True, False)])
+def test_dp_rccl_one_rank(fine_tune, graph):
+    """The RCCL ("nccl" backend) branch of capmi.dist -- init_process_group(device_id=...), the
+    async ReduceOp.AVG all-reduce of the flat buffers (the fc bucket beside the BPTT loop, the rest
+    after; in fine-tune the decoder's beside the encoder backward) -- at world size 1
+    (CAPMI_DIST_FORCE=1; RCCL refuses two ranks on one GPU). AVG over one rank is the identity, so
+    the gradient buffers must equal the non-DP ones bit for bit."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), fine_tune, q, graph, "nccl"))
+    p.start()
+    r = q.get(timeout=180)
+    p.join(timeout=60)
+    assert r[1] != "error", r[2]
+    assert r[1] == 0.0, ("decoder grads", r[1])
+    assert r[2] == 0.0, ("encoder grads", r[2])
