@@ -23,7 +23,7 @@ CAPMI_B_NMAJOR_W, CAPMI_B_KROWS, CAPMI_B_CONV_NHWC = 0, 1, 2
 CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO, CAPMI_TILE_128_W8 = 0, 1, 2, 3, 4
 CAPMI_MAX_GROUP = 4
 CAPMI_COLSUM_GROUPS = 64
-ABI_VERSION = 11
+ABI_VERSION = 12
 CAPMI_BNB_RELU_Y, CAPMI_BNB_RELU_OUT = 0, 1
 CAPMI_BNB_MAX_SLABS = 256
 CAPMI_GEMM_BF16 = 1
@@ -47,6 +47,24 @@ class GemmProblem(ctypes.Structure):
         ("in_scale", c_vp), ("in_shift", c_vp),
     ]
 
+
+class DstepSeg(ctypes.Structure):
+    """Mirror of ``capmi_dstep_seg`` (include/capmi.h)."""
+    _fields_ = [("A", c_vp), ("lda", c_ll), ("W", c_vp), ("ldw", c_ll), ("K", c_int)]
+
+
+class DstepEpi(ctypes.Structure):
+    """Mirror of ``capmi_dstep_epi`` (include/capmi.h)."""
+    _fields_ = [
+        ("mode", c_int), ("out0", c_vp), ("ld0", c_ll), ("bias0", c_vp), ("nsplit", c_int),
+        ("out1", c_vp), ("ld1", c_ll), ("bias1", c_vp), ("act1", c_int), ("D", c_int),
+        ("xemb", c_vp), ("c_prev", c_vp), ("h_out", c_vp), ("c_out", c_vp), ("act_out", c_vp),
+        ("dhd", c_vp), ("dc_in", c_vp), ("act", c_vp), ("c_cur", c_vp), ("dgates", c_vp), ("dc_out", c_vp),
+        ("bt", c_int), ("gate", c_vp), ("awe", c_vp), ("dawe_out", c_vp), ("dgp", c_vp),
+    ]
+
+
+CAPMI_DSTEP_STORE2, CAPMI_DSTEP_LSTM_FWD, CAPMI_DSTEP_LSTM_BWD, CAPMI_DSTEP_GATE_BWD = 0, 1, 2, 3
 
 # name -> argtypes (restype is int unless listed in _RESTYPES)
 _SIGS = {
@@ -103,6 +121,12 @@ _SIGS = {
                             c_int, c_vp, c_vp, c_vp],
     "capmi_att_enc_grad": [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,
                            ctypes.POINTER(c_int), c_vp],
+    "capmi_dstep_gemm": [ctypes.POINTER(DstepSeg), c_int, c_int, c_int, c_int, c_int, c_int,
+                         ctypes.POINTER(DstepEpi), c_vp, c_ll, c_vp, c_int, c_vp],
+    "capmi_att_fwd_fused": [c_vp, c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp, c_vp,
+                            c_int, c_int, c_int, c_int, c_int, c_vp, c_ll, c_vp, c_vp, c_ll, c_vp],
+    "capmi_att_bwd_fused": [c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_ll, c_vp, c_vp,
+                            c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp],
     "capmi_adam_clamp": [c_vp, c_vp, c_vp, c_vp, c_ll, c_double, c_double, c_double, c_double, c_double,
                          c_double, c_double, c_vp, c_vp],
     "capmi_adam_clamp_f64": [c_vp, c_vp, c_vp, c_vp, c_ll, c_double, c_double, c_double, c_double,

@@ -21,12 +21,14 @@ Ragged captions follow the reference's ``batch_size_t = sum(l > t)`` rule
 (:261): rows b >= bt[t] produce zero predictions/alphas and no gradient.
 """
 import math
+import os
 
 import torch
 
 from . import kernels as K
 from ._lib import CAPMI_A_KMAJOR as AK, CAPMI_A_MMAJOR as AMM, CAPMI_B_KROWS as BKR
 from ._lib import CAPMI_B_NMAJOR_W as BW
+from ._lib import CAPMI_DSTEP_GATE_BWD, CAPMI_DSTEP_LSTM_BWD, CAPMI_DSTEP_LSTM_FWD, CAPMI_DSTEP_STORE2
 
 E_DIM = 2048
 PNAMES = ["attention.enc_att.weight", "attention.enc_att.bias", "attention.dec_att.weight",
@@ -34,6 +36,15 @@ PNAMES = ["attention.enc_att.weight", "attention.enc_att.bias", "attention.dec_a
           "decode_step.weight_ih", "decode_step.weight_hh", "decode_step.bias_ih",
           "decode_step.bias_hh", "h_lin.weight", "h_lin.bias", "c_lin.weight", "c_lin.bias",
           "f_beta.weight", "f_beta.bias", "fc.weight", "fc.bias", "embedding.weight"]
+
+
+def _dsplit(M, N, nt, K_, target=None):
+    """k-split of a capmi_dstep_gemm launch: tiles * S ~ target workgroups, each workgroup at most
+    16 k-tiles (4 k-groups x 4 loaded up front; the C side raises S to that too), >= 1 per split."""
+    target = target or int(os.environ.get("CAPMI_DSTEP_WGS", "256"))
+    tiles = -(-M // 64) * (N // nt)
+    kt = K_ // 32
+    return max(1, min(kt, max(-(-kt // 16), round(target / tiles))))
 
 
 def _split(M, N, K_, tile, target=256, min_k=128):
@@ -60,6 +71,24 @@ class DecoderDims:
         self.s_dx = _split(B, E, 4 * D, K.TILE_64)
         self.s_dh = (_split(B, D, 4 * D, K.TILE_64, 96), _split(B, D, E, K.TILE_64, 96),
                      _split(B, D, A, K.TILE_64, 64))
+        # decoder_step.hip (CAPMI_DEC_FUSED, opt-in): "1" the attention forward (score + softmax +
+        # context + gate) and backward (gate split + context + softmax + score) as one launch each,
+        # reading the split-K GEMM partials; "2" also the last-arriver GEMMs with the LSTM cell in
+        # their epilogue (three launches per timestep each way). "0" (default) the five-launch path:
+        # measured on one box "1" is 0.9 % faster run alone but 1.1 % slower in the
+        # pipelined step, "2" 3.5 % slower
+        mode = os.environ.get("CAPMI_DEC_FUSED", "0")
+        self.fused_att = mode != "0" and P <= 56 and E + P + 4100 <= 16384
+        self.fused = (mode == "2" and self.fused_att and A % 32 == 0 and D % 32 == 0 and E % 64 == 0
+                      and M % 4 == 0)
+        if self.fused:
+            self.f_s1 = _dsplit(B, A + E, 32, D)              # att_dec | f_beta from h
+            self.f_s3 = _dsplit(B, 4 * D, 64, E + D)          # [gate*awe | h] x [W_ih_awe | W_hh] + LSTM
+            self.f_sb1 = _dsplit(B, D, 16, 4 * D + E + A)     # dh of step t+1 + LSTM backward of step t
+            self.f_sb2 = _dsplit(B, E, 64, 4 * D)             # d(gate*awe) + gate / context split
+            self.f_part = max(-(-B // 64) * n * s * 64 * nt for n, s, nt in (
+                ((A + E) // 32, self.f_s1, 32), (D // 16, self.f_s3, 64), (D // 16, self.f_sb1, 16),
+                (E // 64, self.f_sb2, 64)))
 
     def key(self):
         return (self.B, self.T, self.L, self.P, self.A, self.D, self.M, self.V, self.E)
@@ -108,6 +137,11 @@ class Workspace:
         self.sk = K.gemm_workspace(device)  # stream-K workspace of the hoisted GEMMs
         self.work = e(max(K.colsum_work_size(T * B, V), K.colsum_work_size(B * P, A),
                           K.colsum_work_size(T * B, 4 * D), K.colsum_work_size(T * B, E), 64), **f)
+        if dm.fused:
+            self.f_part = e(dm.f_part, **f)
+            # last-arriver counters of the GEMM tiles; every launch leaves them zero
+            self.f_count = torch.zeros(4096, device=device, dtype=torch.int32)
+            self.DAWE1 = e(B, E, **f)
 
 
 class DecoderCore:
@@ -132,6 +166,79 @@ class DecoderCore:
         few output tiles (dW_enc_att: 128 tiles of 128x64 over K = B*P) still fills the chip."""
         K.gemm_sk(K.problem(M, N, Kd, A, lda, B, ldb, out, ld_out, bias=bias, **kw), amode, ws.sk,
                   K.TILE_AUTO, bmode)
+
+    # ------------------------------------------------------------------ fused recurrence
+    @staticmethod
+    def _fwd_loop_fused(p, dm, ws, enc, bt, alphas):
+        """The 24-step loop in three launches per step (decoder_step.hip):
+        1. [att_dec | f_beta pre-activation] = h [W_da ; W_fb]^T, last arriver: + bias -> AD[t], sigmoid -> GATE[t]
+        2. score + softmax + context + gate * awe -> alphas[:, t], AWE[t], X[t, :, M:]
+        3. [gate*awe | h] [W_ih_awe | W_hh]^T (gate-interleaved tiles), last arriver: + xemb, LSTMCell
+           -> H[t+1], C[t+1], ACT[t]   (models/attention.py:265-278)"""
+        B, T, P, A, D, M, E, X = dm.B, dm.T, dm.P, dm.A, dm.D, dm.M, dm.E, dm.X
+        W_ih = p["decode_step.weight_ih"]
+        wk1 = torch.cat([p["attention.dec_att.weight"], p["f_beta.weight"]], 0)  # (A + E, D)
+        part, cnt = ws.f_part, ws.f_count
+        for t in range(T):
+            h = ws.H[t]
+            K.dstep_gemm([(h, D, wk1, D, D)], B, A + E, 32, dm.f_s1,
+                         dict(mode=CAPMI_DSTEP_STORE2, out0=ws.AD[t], ld0=A, bias0=p["attention.dec_att.bias"],
+                              nsplit=A, out1=ws.GATE[t], ld1=E, bias1=p["f_beta.bias"], act1=1), part, cnt)
+            K.att_fwd_fused(ws.ATT_ENC, ws.AD[t], 0, 0, None, None, p["attention.full_att.weight"],
+                            p["attention.full_att.bias"], enc, ws.GATE[t], 0, 0, None, None, B, P, A, E, bt[t],
+                            alphas[:, t], T * P, ws.AWE[t], ws.X[t, :, M:], X)
+            K.dstep_gemm([(ws.X[t, :, M:], X, W_ih[:, M:], X, E), (h, D, p["decode_step.weight_hh"], D, D)],
+                         B, 4 * D, 64, dm.f_s3,
+                         dict(mode=CAPMI_DSTEP_LSTM_FWD, D=D, xemb=ws.XEMB[t], c_prev=ws.C[t], h_out=ws.H[t + 1],
+                              c_out=ws.C[t + 1], act_out=ws.ACT[t]), part, cnt, gate_D=D)
+
+    @staticmethod
+    def _bwd_loop_fused(p, st, dm, ws, enc, bt, dalphas, dreg, denc):
+        """Backward through time in three launches per step (decoder_step.hip):
+        1. dh_t = DHD[t] + [DG | DGP | DAD]_{t+1} [W_hh ; W_fb ; W_da] (transposed once per call),
+           last arriver: LSTMCell backward of step t -> DG[t], dc
+        2. d(gate*awe)_t = DG[t] W_ih_awe, last arriver: dawe = d * gate, DGP[t] = d * awe * gate'
+        3. dalpha = dawe . enc, last workgroup of each row: softmax + ReLU-score backward -> DE[t], DAD[t]
+        The final launch writes dh_0 (h_lin / c_lin backward). Returns the DC slot holding dc_0."""
+        B, T, P, A, D, M, E, X = dm.B, dm.T, dm.P, dm.A, dm.D, dm.M, dm.E, dm.X
+        W_ih = p["decode_step.weight_ih"]
+        wb1 = torch.cat([p["decode_step.weight_hh"].t(), p["f_beta.weight"].t(),
+                         p["attention.dec_att.weight"].t()], 1)       # (D, 4D + E + A)
+        wb2 = W_ih[:, M:].t().contiguous()                            # (E, 4D)
+        KB1 = 4 * D + E + A
+        part, cnt = ws.f_part, ws.f_count
+        wf = p["attention.full_att.weight"]
+
+        def dh_segs(t1):
+            return [(ws.DG[t1], 4 * D, wb1, KB1, 4 * D), (ws.DGP[t1], E, wb1[:, 4 * D:], KB1, E),
+                    (ws.DAD[t1], A, wb1[:, 4 * D + E:], KB1, A)]
+
+        cur = 0
+        for t in range(T - 1, -1, -1):
+            if t == T - 1:
+                K.lstm_cell_bwd(ws.DHD[t], None, 0, B * D, None, ws.ACT[t], ws.C[t], ws.C[t + 1], B, D, bt[t],
+                                ws.DG[t], ws.DC[cur ^ 1])
+            else:
+                K.dstep_gemm(dh_segs(t + 1), B, D, 16, dm.f_sb1,
+                             dict(mode=CAPMI_DSTEP_LSTM_BWD, D=D, dhd=ws.DHD[t], dc_in=ws.DC[cur], act=ws.ACT[t],
+                                  c_prev=ws.C[t], c_cur=ws.C[t + 1], dgates=ws.DG[t], dc_out=ws.DC[cur ^ 1],
+                                  bt=bt[t]), part, cnt)
+            cur ^= 1
+            dawe = ws.DAWE[t] if denc is not None else ws.DAWE1
+            K.dstep_gemm([(ws.DG[t], 4 * D, wb2, 4 * D, 4 * D)], B, E, 64, dm.f_sb2,
+                         dict(mode=CAPMI_DSTEP_GATE_BWD, gate=ws.GATE[t], awe=ws.AWE[t], dawe_out=dawe,
+                              dgp=ws.DGP[t]), part, cnt)
+            if dalphas is not None:
+                dr, dr_ld = dalphas[:, t], T * P
+            elif dreg is not None:
+                dr, dr_ld = dreg, P
+            else:
+                dr, dr_ld = None, 0
+            K.att_bwd_fused(dawe, 0, 0, None, None, None, None, enc, st["alphas"][:, t], T * P, dr, dr_ld, ws.ATT_ENC,
+                            ws.AD[t], wf, B, P, A, E, bt[t], ws.DE[t], ws.DAD[t])
+        K.dstep_gemm(dh_segs(0), B, D, 16, dm.f_sb1, dict(mode=CAPMI_DSTEP_STORE2, out0=ws.DH0, ld0=D, nsplit=D),
+                     part, cnt)
+        return cur
 
     # ------------------------------------------------------------------ forward
     def forward(self, p, enc, caps, decode_lengths, *, dropout_p=0.0, training=False, seed=0,
@@ -191,7 +298,9 @@ class DecoderCore:
         s_a, s_g, s_hh = dm.s_h
         W_ih_awe = W_ih[:, M:]
         wf = p["attention.full_att.weight"]
-        for t in range(T):
+        if dm.fused:
+            self._fwd_loop_fused(p, dm, ws, enc, bt, alphas)
+        for t in range(T if not dm.fused else 0):
             h = ws.H[t]
             # att_dec (:55), f_beta (:270) and W_hh h (:277) share the input h: one grouped launch
             K.gemm([K.problem(B, A, D, h, D, p["attention.dec_att.weight"], D, ws.P_ad, A, ksplit=s_a,
@@ -200,10 +309,15 @@ class DecoderCore:
                               c_split_stride=B * E),
                     K.problem(B, 4 * D, D, h, D, p["decode_step.weight_hh"], D, ws.P_hh, 4 * D, ksplit=s_hh,
                               c_split_stride=B * 4 * D)], AK, BW, K.TILE_64)
-            K.att_score_fwd(ws.ATT_ENC, ws.P_ad, s_a, B * A, p["attention.dec_att.bias"], wf,
-                            p["attention.full_att.bias"], B, P, A, ws.score, ws.AD[t])
-            K.att_softmax_ctx_fwd(ws.score, enc, B, P, E, bt[t], alphas[:, t], T * P, ws.AWE[t],
-                                  ws.P_gate, s_g, B * E, p["f_beta.bias"], ws.GATE[t], ws.X[t, :, M:], X)
+            if dm.fused_att:
+                K.att_fwd_fused(ws.ATT_ENC, ws.P_ad, s_a, B * A, p["attention.dec_att.bias"], ws.AD[t], wf,
+                                p["attention.full_att.bias"], enc, ws.P_gate, s_g, B * E, p["f_beta.bias"],
+                                ws.GATE[t], B, P, A, E, bt[t], alphas[:, t], T * P, ws.AWE[t], ws.X[t, :, M:], X)
+            else:
+                K.att_score_fwd(ws.ATT_ENC, ws.P_ad, s_a, B * A, p["attention.dec_att.bias"], wf,
+                                p["attention.full_att.bias"], B, P, A, ws.score, ws.AD[t])
+                K.att_softmax_ctx_fwd(ws.score, enc, B, P, E, bt[t], alphas[:, t], T * P, ws.AWE[t],
+                                      ws.P_gate, s_g, B * E, p["f_beta.bias"], ws.GATE[t], ws.X[t, :, M:], X)
             K.gemm(K.problem(B, 4 * D, E, ws.X[t, :, M:], X, W_ih_awe, X, ws.P_x, 4 * D, ksplit=dm.s_x,
                              c_split_stride=B * 4 * D), AK, BW, K.TILE_64)
             K.lstm_cell_fwd(ws.P_x, dm.s_x, B * 4 * D, ws.XEMB[t], ws.P_hh, s_hh, B * 4 * D, ws.C[t], B, D,
@@ -286,23 +400,30 @@ class DecoderCore:
             ws.DAWE = torch.empty(T, B, E, device=enc.device, dtype=torch.float32)
             ws.DMEAN = torch.empty(B, E, device=enc.device, dtype=torch.float32)
         cur = 0
-        for t in range(T - 1, -1, -1):
+        if dm.fused:
+            cur = self._bwd_loop_fused(p, st, dm, ws, enc, bt, dalphas, dreg, denc)
+        for t in range(T - 1, -1, -1) if not dm.fused else ():
             K.lstm_cell_bwd(ws.DHD[t], ws.P_dh, S_dh if t < T - 1 else 0, B * D,
                             ws.DC[cur] if t < T - 1 else None, ws.ACT[t], ws.C[t], ws.C[t + 1], B, D, bt[t],
                             ws.DG[t], ws.DC[cur ^ 1])
             cur ^= 1
             K.gemm(K.problem(B, E, 4 * D, ws.DG[t], 4 * D, W_ih_awe, X, ws.P_dx, E, ksplit=dm.s_dx,
                              c_split_stride=B * E), AK, BKR, K.TILE_64)
-            K.att_ctx_bwd(ws.P_dx, dm.s_dx, B * E, ws.GATE[t], ws.AWE[t], enc, B, P, E, ws.DGP[t], ws.DALPHA,
-                          dawe_out=ws.DAWE[t] if denc is not None else None)
             if dalphas is not None:
                 dr, dr_ld = dalphas[:, t], T * P
             elif dreg is not None:
                 dr, dr_ld = dreg, P
             else:
                 dr, dr_ld = None, 0
-            K.att_score_bwd(ws.DALPHA, dr, dr_ld, st["alphas"][:, t], T * P, ws.ATT_ENC, ws.AD[t], wf, B, P,
-                            A, bt[t], ws.DE[t], ws.DAD[t])
+            if dm.fused_att:
+                K.att_bwd_fused(ws.P_dx, dm.s_dx, B * E, ws.GATE[t], ws.AWE[t], ws.DGP[t],
+                                ws.DAWE[t] if denc is not None else None, enc, st["alphas"][:, t], T * P, dr, dr_ld,
+                                ws.ATT_ENC, ws.AD[t], wf, B, P, A, E, bt[t], ws.DE[t], ws.DAD[t])
+            else:
+                K.att_ctx_bwd(ws.P_dx, dm.s_dx, B * E, ws.GATE[t], ws.AWE[t], enc, B, P, E, ws.DGP[t], ws.DALPHA,
+                              dawe_out=ws.DAWE[t] if denc is not None else None)
+                K.att_score_bwd(ws.DALPHA, dr, dr_ld, st["alphas"][:, t], T * P, ws.ATT_ENC, ws.AD[t], wf, B, P,
+                                A, bt[t], ws.DE[t], ws.DAD[t])
             o1, o2 = s_dh[0] * B * D, (s_dh[0] + s_dh[1]) * B * D
             K.gemm([K.problem(B, D, 4 * D, ws.DG[t], 4 * D, p["decode_step.weight_hh"], D, ws.P_dh, D,
                               ksplit=s_dh[0], c_split_stride=B * D),
@@ -312,7 +433,8 @@ class DecoderCore:
                               ws.P_dh.view(-1)[o2:], D, ksplit=s_dh[2], c_split_stride=B * D)],
                    AK, BKR, K.TILE_64)
         # dh0 / dc0 -> h_lin / c_lin (:162-163)
-        K.splitk_reduce(ws.P_dh, S_dh, B * D, B, D, D, ws.DH0, D)
+        if not dm.fused:  # (the fused loop's last launch wrote DH0)
+            K.splitk_reduce(ws.P_dh, S_dh, B * D, B, D, D, ws.DH0, D)
         dc0 = ws.DC[cur]
         for nm, dd in (("h_lin", ws.DH0), ("c_lin", dc0)):
             if nm + ".weight" in need:

@@ -8,6 +8,7 @@ import weakref
 
 import torch
 
+from ._lib import DstepEpi, DstepSeg
 from ._lib import (CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_GEMM_BF16_IO, CAPMI_GEMM_X3, CAPMI_GEMM_X3P,
                    CAPMI_COLSUM_GROUPS, CAPMI_TILE_128, CAPMI_TILE_64,
                    CAPMI_TILE_128x64, CAPMI_TILE_AUTO, GemmProblem, call, lib)
@@ -541,6 +542,45 @@ def att_enc_grad(de, att_enc, att_dec, wf, T, B, P, A, datt_enc, wf_part, bf_par
 
 def att_enc_grad_blocks(B, P):
     return ((P + 27) // 28) * B
+
+
+# --------------------------------------------------------------------------------------
+# fused recurrence kernels (decoder_step.hip)
+# --------------------------------------------------------------------------------------
+def dstep_gemm(segs, M, N, nt, S, epi, part, counters, gate_D=0):
+    """segs: [(A, lda, W, ldw, K), ...] (1-3 K segments, fp32 views; A [M][K], W [N][K] row-major);
+    epi: dict of capmi_dstep_epi fields (tensors or ints; ``mode`` one of CAPMI_DSTEP_*)."""
+    arr = (DstepSeg * len(segs))()
+    for i, (A, lda, W, ldw, K) in enumerate(segs):
+        _cuda(A, W)
+        arr[i].A, arr[i].lda, arr[i].W, arr[i].ldw, arr[i].K = ptr(A), int(lda), ptr(W), int(ldw), int(K)
+    e = DstepEpi()
+    for k, v in epi.items():
+        if isinstance(v, torch.Tensor):
+            _cuda(v)
+            setattr(e, k, v.data_ptr())
+        else:
+            setattr(e, k, v)
+    _cuda(part)
+    _cuda(counters, dtype=torch.int32)
+    call("capmi_dstep_gemm", arr, len(segs), int(M), int(N), int(nt), int(S), int(gate_D), ctypes.byref(e),
+         ptr(part), part.numel(), ptr(counters), counters.numel(), stream())
+
+
+def att_fwd_fused(att_enc, ad, S_a, slab_a, bias_da, ad_out, wf, bf, enc, gate, S_g, slab_g, bias_fb, gate_out,
+                  B, P, A, E, bt, alpha_out, alpha_ld_b, awe_out, x_out, ld_x):
+    _cuda(att_enc, ad, bias_da, ad_out, wf, bf, enc, gate, bias_fb, gate_out, alpha_out, awe_out, x_out)
+    call("capmi_att_fwd_fused", ptr(att_enc), ptr(ad), S_a, slab_a, ptr(bias_da), ptr(ad_out), ptr(wf), ptr(bf),
+         ptr(enc), ptr(gate), S_g, slab_g, ptr(bias_fb), ptr(gate_out), B, P, A, E, bt, ptr(alpha_out), alpha_ld_b,
+         ptr(awe_out), ptr(x_out), ld_x, stream())
+
+
+def att_bwd_fused(dx, S, slab, gate, awe, dgp, dawe_out, enc, alpha, alpha_ld_b, dreg, dreg_ld_b, att_enc, att_dec,
+                  wf, B, P, A, E, bt, de, dad):
+    _cuda(dx, gate, awe, dgp, dawe_out, enc, alpha, dreg, att_enc, att_dec, wf, de, dad)
+    call("capmi_att_bwd_fused", ptr(dx), S, slab, ptr(gate), ptr(awe), ptr(dgp), ptr(dawe_out), ptr(enc), ptr(alpha),
+         alpha_ld_b, ptr(dreg), dreg_ld_b, ptr(att_enc), ptr(att_dec), ptr(wf), B, P, A, E, bt, ptr(de), ptr(dad),
+         stream())
 
 
 # --------------------------------------------------------------------------------------

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 11
+#define CAPMI_ABI_VERSION 12
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -353,6 +353,90 @@ int capmi_att_score_bwd(const float* dalpha, const float* dreg, long long dreg_l
 int capmi_att_enc_grad(const float* de, const float* att_enc, const float* att_dec,
                        const float* wf, int T, int B, int P, int A, float* datt_enc,
                        float* wf_part, float* bf_part, int* nblk_out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Fused recurrence kernels (decoder_step.hip): three launches per timestep forward and three
+ * backward instead of five each. Replace, per step t of models/attention.py:260-281:
+ *   capmi_dstep_gemm, STORE2   : att_dec = dec_att(h) (:55) and gate = sigmoid(f_beta(h)) (:270)
+ *   capmi_att_fwd_fused        : SoftAttention score, softmax, context (:56-60), gate * awe (:271)
+ *   capmi_dstep_gemm, LSTM_FWD : LSTMCell([emb, gate*awe], (h, c)) (:277-278), the embedding
+ *                                half of W_ih precomputed for all t (xemb, incl. both biases)
+ * and the autograd backward of the same ops (LSTM_BWD: dh GEMM of step t+1 + the cell backward of
+ * step t; GATE_BWD: d(gate*awe) GEMM + the gate/context split; capmi_att_bwd_fused: context,
+ * softmax and score backward).
+ *
+ * capmi_dstep_gemm: C[M, N] = sum over segments i of A_i[M, K_i] * W_i[N, K_i]^T (both row-major,
+ * k contiguous; every K_i % 32 == 0), fp32 MFMA (v_mfma_f32_16x16x4_f32), 64-row x nt-column tiles
+ * (nt in {16, 32, 64}, N % nt == 0), k split S ways over workgroups. The S partials of a tile are
+ * parked (write-through) and the LAST workgroup to arrive (one agent-scope counter per tile, reset
+ * by that workgroup) adds them in split order -- deterministic -- and runs the epilogue.
+ * gate_D > 0 (LSTM_FWD, nt = 64): tile tn's column c is W row (c/16)*gate_D + 16 tn + c%16, so a
+ * tile holds the four gates i, f, g, o of 16 hidden units.
+ * part: >= tiles*S*64*nt floats; counters: >= tiles ints, zero between launches.
+ * ---------------------------------------------------------------------- */
+typedef struct {
+  const float* A;
+  long long lda;
+  const float* W;
+  long long ldw;
+  int K;
+} capmi_dstep_seg;
+
+#define CAPMI_DSTEP_STORE2 0   /* col < nsplit: out0 = v + bias0; else out1 = act1(v + bias1), act1 1 = sigmoid */
+#define CAPMI_DSTEP_LSTM_FWD 1 /* gates = v + xemb -> h_out, c_out, act_out (i, f, g, o) */
+#define CAPMI_DSTEP_LSTM_BWD 2 /* dh = v + dhd -> dgates, dc_out (rows >= bt: zeros) */
+#define CAPMI_DSTEP_GATE_BWD 3 /* d = v: dawe_out = d * gate, dgp = d * awe * gate * (1 - gate) */
+
+typedef struct {
+  int mode;
+  float* out0;
+  long long ld0;
+  const float* bias0;
+  int nsplit;
+  float* out1;
+  long long ld1;
+  const float* bias1;
+  int act1;
+  int D;                /* LSTM hidden size */
+  const float* xemb;    /* LSTM_FWD: [M][4D] */
+  const float* c_prev;  /* LSTM_FWD / LSTM_BWD: c_{t} [M][D] */
+  float* h_out;
+  float* c_out;
+  float* act_out;       /* LSTM_FWD: [M][4D]; LSTM_BWD reads it (act) */
+  const float* dhd;     /* LSTM_BWD: [M][D] or NULL */
+  const float* dc_in;   /* LSTM_BWD: [M][D] or NULL */
+  const float* act;     /* LSTM_BWD: [M][4D] */
+  const float* c_cur;   /* LSTM_BWD: c_{t+1} */
+  float* dgates;        /* LSTM_BWD: [M][4D] */
+  float* dc_out;        /* LSTM_BWD: [M][D] */
+  int bt;               /* LSTM_BWD: active rows */
+  const float* gate;    /* GATE_BWD: [M][N] */
+  const float* awe;     /* GATE_BWD: [M][N] */
+  float* dawe_out;      /* GATE_BWD: [M][N] */
+  float* dgp;           /* GATE_BWD: [M][N] */
+} capmi_dstep_epi;
+
+int capmi_dstep_gemm(const capmi_dstep_seg* segs, int nseg, int M, int N, int nt, int S, int gate_D,
+                     const capmi_dstep_epi* epi, float* part, long long part_floats, int* counters,
+                     int ncounters, void* stream);
+/* capmi_att_score_fwd + capmi_att_softmax_ctx_fwd in one launch, on the distinct rows (P <= 56):
+ * grid (E/512, B), each workgroup recomputes the P scores of its row b and writes its 512 columns
+ * of awe and x = gate*awe; alphas of rows b >= bt are written as 0. att_dec: ad final [B][A]
+ * (S_a = 0) or bias_da + the S_a split-K partials ad[s*slab_a + b*A + a] (then also written to
+ * ad_out); gate: final sigmoid (S_g = 0) or sigmoid(bias_fb + partials), then written to gate_out.
+ * Same arithmetic and summation order as the two kernels it replaces. */
+int capmi_att_fwd_fused(const float* att_enc, const float* ad, int S_a, long long slab_a, const float* bias_da,
+                        float* ad_out, const float* wf, const float* bf, const float* enc, const float* gate,
+                        int S_g, long long slab_g, const float* bias_fb, float* gate_out, int B, int P, int A,
+                        int E, int bt, float* alpha_out, long long alpha_ld_b, float* awe_out, float* x_out,
+                        long long ld_x, void* stream);
+/* capmi_att_ctx_bwd + capmi_att_score_bwd in one launch, one workgroup per row b: d(gate*awe) final
+ * (S = 0: dx is dawe) or the S split-K partials (then dawe = d*gate -> dawe_out, dgp as
+ * capmi_att_ctx_bwd), dalpha, softmax and ReLU-score backward. Bit-identical to the two kernels. */
+int capmi_att_bwd_fused(const float* dx, int S, long long slab, const float* gate, const float* awe, float* dgp,
+                        float* dawe_out, const float* enc, const float* alpha, long long alpha_ld_b,
+                        const float* dreg, long long dreg_ld_b, const float* att_enc, const float* att_dec,
+                        const float* wf, int B, int P, int A, int E, int bt, float* de, float* dad, void* stream);
 
 /* ------------------------------------------------------------------------
  * Optimiser (train_utils.py:2-12 clamp + torch.optim.Adam, models/attention.py:352-355,423-430)

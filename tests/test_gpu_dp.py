@@ -56,10 +56,10 @@ def _setup(fine_tune, seed=3):
 
 
 class _Probe:
-    """The attributes AttentionTrainStep._feat_layout reads, for a fine-tune step."""
+    """The attributes AttentionTrainStep._feat_layout reads."""
 
-    def __init__(self, enc):
-        self.encoder, self.dedup, self.fine_tune = enc, os.environ.get("CAPMI_ATT_DEDUP", "1") != "0", True
+    def __init__(self, enc, fine_tune):
+        self.encoder, self.dedup, self.fine_tune = enc, os.environ.get("CAPMI_ATT_DEDUP", "1") != "0", fine_tune
 
 
 def _worker(rank, world, port, fine_tune, q, graph=False, backend="gloo"):
@@ -87,10 +87,10 @@ def _worker(rank, world, port, fine_tune, q, graph=False, backend="gloo"):
         for r in range(world):
             sl = slice(r * B, (r + 1) * B)
             g = {n: torch.zeros_like(q) for n, q in dec.named_parameters() if q.requires_grad}
+            # same feature layout as the step (the distinct-row map when the pool only repeats
+            # pixels), so the two differ only in the all-reduce
+            shape, dup = AttentionTrainStep._feat_layout(_Probe(enc, fine_tune), imgs[sl])
             if fine_tune:
-                # same feature layout as the step (the distinct-row map when the pool only repeats
-                # pixels), so the two differ only in the all-reduce
-                _, dup = AttentionTrainStep._feat_layout(_Probe(enc), imgs[sl])
                 f = enc.ft_forward(imgs[sl], pooled=dup == 1)
                 denc = torch.empty_like(f)
                 DF.fused_loss_and_grads(dec, f, caps[sl], [L] * B, 1.0, g, denc=denc, dup=dup)
@@ -98,9 +98,10 @@ def _worker(rank, world, port, fine_tune, q, graph=False, backend="gloo"):
                 enc.ft_backward(denc, eg)
                 ref_e.append(torch.cat([eg[id(q)].reshape(-1) for q in enc.parameters() if q.requires_grad]))
             else:
+                f = torch.empty(shape, device="cuda")
                 with torch.no_grad():
-                    f = enc(imgs[sl])
-                DF.fused_loss_and_grads(dec, f, caps[sl], [L] * B, 1.0, g)
+                    AttentionTrainStep._encode_into(_Probe(enc, fine_tune), imgs[sl], f, dup)
+                DF.fused_loss_and_grads(dec, f, caps[sl], [L] * B, 1.0, g, dup=dup)
             ref_d.append(torch.cat([g[n].reshape(-1) for n, q in dec.named_parameters() if q.requires_grad]))
         torch.cuda.synchronize()
         # the DP step on this rank's shard (fresh model: BN running stats / weights as above)
