@@ -79,6 +79,10 @@ def parse():
                     help="fp32 configs: x3 = fp32-accurate convs on the bf16 matrix cores (operands split exactly "
                          "into three bf16 terms, six cross products accumulated in fp32; gemm_x3*.hip), native = "
                          "v_mfma_f32_32x32x2_f32")
+    ap.add_argument("--dec", default="auto", choices=["auto", "x3", "fp32", "bf16"],
+                    help="decoder GEMM arithmetic (AttentionDecoder.set_compute_precision): auto = bf16 for the "
+                         "bf16 config, else fp32 (v_mfma_f32_32x32x2_f32; tools/dec_gemm_ab.py: the x3 split is "
+                         "slower on the transposed-operand backward GEMMs); x3 = fp32-accurate three-term split")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="cpu_baseline: keep stepping the oracle at the full batch until this much time "
@@ -402,6 +406,8 @@ def main():
             encoder.set_compute_precision("bf16")  # config 5 is the bf16 config
     if not encoder._runner.bf16 and args.conv == "x3":
         encoder.set_compute_precision("fp32-x3")
+    dec_prec = args.dec if args.dec != "auto" else ("bf16" if encoder._runner.bf16 else "fp32")
+    decoder.set_compute_precision({"x3": "fp32-x3", "fp32": "fp32", "bf16": "bf16"}[dec_prec])
     if ft:
         # synthetic GloVe-300 table, fp64 like load_glove_vectors (embed.py:64-68, Q7)
         g = torch.Generator().manual_seed(300)
@@ -507,6 +513,9 @@ def main():
                                 "products above 2^-23|a||b| accumulated in fp32 on bf16 MFMA (error vs fp64 <= the "
                                 "fp32-MFMA kernel's, tests/test_gpu_x3.py)" if encoder._runner.x3 else
                                 "fp32 MFMA (v_mfma_f32_32x32x2_f32)"),
+            "decoder_gemm_arithmetic": {"fp32-x3": "fp32-accurate x3 split (CAPMI_GEMM_SPLIT3, tests/test_gpu_split_gemm.py)",
+                                        "bf16": "bf16 operands, fp32 accumulate (CAPMI_GEMM_BF16)",
+                                        "fp32": "fp32 MFMA"}[decoder.compute_precision],
             "data": "synthetic (resident in HBM; random-init weights, torch.manual_seed(0))",
             "config": {"workload": ("'glove_att' decoder (GloVe-300 fp64 embedding, fine-tuned) + ResNet-101 "
                                     "encoder fine-tuned (layer2-4, BN train mode), one training step per batch")

@@ -161,11 +161,12 @@ class DecoderCore:
 
     # ------------------------------------------------------------------ helpers
     @staticmethod
-    def _gemm_into(ws, out, ld_out, M, N, Kd, A, lda, B, ldb, amode, bmode, bias=None, **kw):
+    def _gemm_into(ws, out, ld_out, M, N, Kd, A, lda, B, ldb, amode, bmode, bias=None, gf=0, **kw):
         """C = op(A) op(B) (+bias) for the hoisted (all-timestep) GEMMs: stream-K, so a grid of
-        few output tiles (dW_enc_att: 128 tiles of 128x64 over K = B*P) still fills the chip."""
+        few output tiles (dW_enc_att: 128 tiles of 128x64 over K = B*P) still fills the chip.
+        gf: operand staging flags (0 fp32 MFMA, CAPMI_GEMM_SPLIT3, CAPMI_GEMM_BF16)."""
         K.gemm_sk(K.problem(M, N, Kd, A, lda, B, ldb, out, ld_out, bias=bias, **kw), amode, ws.sk,
-                  K.TILE_AUTO, bmode)
+                  K.TILE_AUTO, bmode, flags=gf)
 
     # ------------------------------------------------------------------ fused recurrence
     @staticmethod
@@ -242,7 +243,7 @@ class DecoderCore:
 
     # ------------------------------------------------------------------ forward
     def forward(self, p, enc, caps, decode_lengths, *, dropout_p=0.0, training=False, seed=0,
-                seed_dev=None, emb_dense=None, dup=1):
+                seed_dev=None, emb_dense=None, dup=1, gemm_flags=0):
         """p: dict name->tensor (PNAMES). enc: (B,P,E) contiguous fp32. caps: (B,L) int64.
         emb_dense: optional (B, Le, M) fp32 word embeddings used instead of the embedding table
         (the BERT variant, :242-244; frozen: no gradient flows into it).
@@ -251,7 +252,11 @@ class DecoderCore:
         every pixel dup x dup times). Everything runs on the distinct rows -- the softmax over the
         (F dup)^2 positions is the softmax over the distinct ones / dup^2, the context sum and the
         init mean are unchanged -- and only the returned alphas are expanded.
+        gemm_flags: operand staging of every non-fused GEMM, forward and backward: 0 (fp32 MFMA),
+        CAPMI_GEMM_SPLIT3 (fp32-accurate three-term split on the bf16 matrix cores) or CAPMI_GEMM_BF16
+        (bf16 operands, fp32 accumulation: the bf16 config).
         Returns (predictions (B,T,V), alphas (B,T,P) [P = (F dup)^2 with dup], state)."""
+        gf = gemm_flags
         B, P, E = enc.shape
         F = 0
         if dup > 1:
@@ -285,14 +290,14 @@ class DecoderCore:
         slab = ws.scratch[:2 * sh * B * D]
         K.gemm([K.problem(B, D, E, ws.mean, E, p["h_lin.weight"], E, slab, D, ksplit=sh, c_split_stride=B * D),
                 K.problem(B, D, E, ws.mean, E, p["c_lin.weight"], E, slab[sh * B * D:], D, ksplit=sh,
-                          c_split_stride=B * D)], AK, BW, K.TILE_64)
+                          c_split_stride=B * D)], AK, BW, K.TILE_64, flags=gf)
         K.splitk_reduce(slab, sh, B * D, B, D, D, ws.H[0], D, bias=p["h_lin.bias"])
         K.splitk_reduce(slab[sh * B * D:], sh, B * D, B, D, D, ws.C[0], D, bias=p["c_lin.bias"])
         # hoisted enc_att (:54) and the embedding half of the LSTM input GEMM
         self._gemm_into(ws, ws.ATT_ENC, A, B * P, A, E, enc, E, p["attention.enc_att.weight"], E, AK, BW,
-                        bias=p["attention.enc_att.bias"])
+                        bias=p["attention.enc_att.bias"], gf=gf)
         self._gemm_into(ws, ws.XEMB, 4 * D, T * B, 4 * D, M, ws.X, X, W_ih, X, AK, BW,
-                        bias=p["decode_step.bias_ih"], bias2=p["decode_step.bias_hh"])
+                        bias=p["decode_step.bias_ih"], bias2=p["decode_step.bias_hh"], gf=gf)
 
         alphas = torch.empty(B, T, P, device=enc.device, dtype=torch.float32)  # over the rows enc holds
         s_a, s_g, s_hh = dm.s_h
@@ -308,7 +313,7 @@ class DecoderCore:
                     K.problem(B, E, D, h, D, p["f_beta.weight"], D, ws.P_gate, E, ksplit=s_g,
                               c_split_stride=B * E),
                     K.problem(B, 4 * D, D, h, D, p["decode_step.weight_hh"], D, ws.P_hh, 4 * D, ksplit=s_hh,
-                              c_split_stride=B * 4 * D)], AK, BW, K.TILE_64)
+                              c_split_stride=B * 4 * D)], AK, BW, K.TILE_64, flags=gf)
             if dm.fused_att:
                 K.att_fwd_fused(ws.ATT_ENC, ws.P_ad, s_a, B * A, p["attention.dec_att.bias"], ws.AD[t], wf,
                                 p["attention.full_att.bias"], enc, ws.P_gate, s_g, B * E, p["f_beta.bias"],
@@ -319,7 +324,7 @@ class DecoderCore:
                 K.att_softmax_ctx_fwd(ws.score, enc, B, P, E, bt[t], alphas[:, t], T * P, ws.AWE[t],
                                       ws.P_gate, s_g, B * E, p["f_beta.bias"], ws.GATE[t], ws.X[t, :, M:], X)
             K.gemm(K.problem(B, 4 * D, E, ws.X[t, :, M:], X, W_ih_awe, X, ws.P_x, 4 * D, ksplit=dm.s_x,
-                             c_split_stride=B * 4 * D), AK, BW, K.TILE_64)
+                             c_split_stride=B * 4 * D), AK, BW, K.TILE_64, flags=gf)
             K.lstm_cell_fwd(ws.P_x, dm.s_x, B * 4 * D, ws.XEMB[t], ws.P_hh, s_hh, B * 4 * D, ws.C[t], B, D,
                             ws.H[t + 1], ws.C[t + 1], ws.ACT[t])
 
@@ -332,7 +337,7 @@ class DecoderCore:
             Hd = Hcur
         preds = torch.empty(B, T, V, device=enc.device, dtype=torch.float32)
         self._gemm_into(ws, preds, T * V, T * B, V, D, Hd, D, p["fc.weight"], D, AK, BW, bias=p["fc.bias"],
-                        c_r1=B, c_s2=V)
+                        c_r1=B, c_s2=V, gf=gf)
         if ragged:
             K.mask_rows_tb(preds, bt_dev, T, B, V, T * V, B, V)
         alphas_out = alphas
@@ -340,7 +345,7 @@ class DecoderCore:
             alphas_out = torch.empty(B, T, P * dup * dup, device=enc.device, dtype=torch.float32)
             K.att_alpha_expand(alphas, B * T, F, dup, alphas_out)
         state = dict(dm=dm, ws=ws, enc=enc, caps=caps, bt=bt, bt_dev=bt_dev, ragged=ragged, alphas=alphas,
-                     dense_emb=emb_dense is not None, dup=dup, F=F,
+                     dense_emb=emb_dense is not None, dup=dup, F=F, gflags=gf,
                      Hd=Hd, dropout_p=dropout_p if training else 0.0, seed=seed, seed_dev=seed_dev)
         return preds, alphas_out, state
 
@@ -367,6 +372,7 @@ class DecoderCore:
             raise ValueError("capmi decoder: dalphas needs the full (non-deduplicated) features")
         enc, bt = st["enc"], st["bt"]
         need = set(grads) if need is None else set(need)
+        gf = st.get("gflags", 0)
         W_ih = p["decode_step.weight_ih"]
         TB = T * B
         if dpred_time_major:
@@ -381,9 +387,9 @@ class DecoderCore:
             K.mask_rows_tb(dpred, st["bt_dev"], T, B, V, T * V, B, V)
 
         # ---- fc (:279): dHd = dpred W_fc ; dW_fc = dpred^T Hd ; db_fc = colsum(dpred)
-        self._gemm_into(ws, ws.DHD, D, TB, D, V, dpred, lda_p, p["fc.weight"], D, AK, BKR, **ar)
+        self._gemm_into(ws, ws.DHD, D, TB, D, V, dpred, lda_p, p["fc.weight"], D, AK, BKR, **ar, gf=gf)
         if "fc.weight" in need:
-            self._gemm_into(ws, grads["fc.weight"], D, V, D, TB, dpred, lda_p, st["Hd"], D, AMM, BKR, **ar)
+            self._gemm_into(ws, grads["fc.weight"], D, V, D, TB, dpred, lda_p, st["Hd"], D, AMM, BKR, **ar, gf=gf)
         if "fc.bias" in need:
             K.colsum(dpred, TB, V, V, grads["fc.bias"], ws.work)
         if on_fc_grads is not None:
@@ -408,7 +414,7 @@ class DecoderCore:
                             ws.DG[t], ws.DC[cur ^ 1])
             cur ^= 1
             K.gemm(K.problem(B, E, 4 * D, ws.DG[t], 4 * D, W_ih_awe, X, ws.P_dx, E, ksplit=dm.s_dx,
-                             c_split_stride=B * E), AK, BKR, K.TILE_64)
+                             c_split_stride=B * E), AK, BKR, K.TILE_64, flags=gf)
             if dalphas is not None:
                 dr, dr_ld = dalphas[:, t], T * P
             elif dreg is not None:
@@ -431,23 +437,23 @@ class DecoderCore:
                               ksplit=s_dh[1], c_split_stride=B * D),
                     K.problem(B, D, A, ws.DAD[t], A, p["attention.dec_att.weight"], D,
                               ws.P_dh.view(-1)[o2:], D, ksplit=s_dh[2], c_split_stride=B * D)],
-                   AK, BKR, K.TILE_64)
+                   AK, BKR, K.TILE_64, flags=gf)
         # dh0 / dc0 -> h_lin / c_lin (:162-163)
         if not dm.fused:  # (the fused loop's last launch wrote DH0)
             K.splitk_reduce(ws.P_dh, S_dh, B * D, B, D, D, ws.DH0, D)
         dc0 = ws.DC[cur]
         for nm, dd in (("h_lin", ws.DH0), ("c_lin", dc0)):
             if nm + ".weight" in need:
-                K.gemm(K.problem(D, E, B, dd, D, ws.mean, E, grads[nm + ".weight"], E), AMM, BKR, K.TILE_128)
+                K.gemm(K.problem(D, E, B, dd, D, ws.mean, E, grads[nm + ".weight"], E), AMM, BKR, K.TILE_128, flags=gf)
             if nm + ".bias" in need:
                 K.colsum(dd, B, D, D, grads[nm + ".bias"], ws.work)
 
         # ---- hoisted weight gradients over all t
         Hprev = ws.H[:T]
         if "decode_step.weight_ih" in need:
-            self._gemm_into(ws, grads["decode_step.weight_ih"], X, 4 * D, X, TB, ws.DG, 4 * D, ws.X, X, AMM, BKR)
+            self._gemm_into(ws, grads["decode_step.weight_ih"], X, 4 * D, X, TB, ws.DG, 4 * D, ws.X, X, AMM, BKR, gf=gf)
         if "decode_step.weight_hh" in need:
-            self._gemm_into(ws, grads["decode_step.weight_hh"], D, 4 * D, D, TB, ws.DG, 4 * D, Hprev, D, AMM, BKR)
+            self._gemm_into(ws, grads["decode_step.weight_hh"], D, 4 * D, D, TB, ws.DG, 4 * D, Hprev, D, AMM, BKR, gf=gf)
         if "decode_step.bias_ih" in need or "decode_step.bias_hh" in need:
             tgt = grads.get("decode_step.bias_ih", grads.get("decode_step.bias_hh"))
             K.colsum(ws.DG, TB, 4 * D, 4 * D, tgt, ws.work)
@@ -455,11 +461,11 @@ class DecoderCore:
                 if nm in need and grads[nm] is not tgt:
                     grads[nm].copy_(tgt)
         if "f_beta.weight" in need:
-            self._gemm_into(ws, grads["f_beta.weight"], D, E, D, TB, ws.DGP, E, Hprev, D, AMM, BKR)
+            self._gemm_into(ws, grads["f_beta.weight"], D, E, D, TB, ws.DGP, E, Hprev, D, AMM, BKR, gf=gf)
         if "f_beta.bias" in need:
             K.colsum(ws.DGP, TB, E, E, grads["f_beta.bias"], ws.work)
         if "attention.dec_att.weight" in need:
-            self._gemm_into(ws, grads["attention.dec_att.weight"], D, A, D, TB, ws.DAD, A, Hprev, D, AMM, BKR)
+            self._gemm_into(ws, grads["attention.dec_att.weight"], D, A, D, TB, ws.DAD, A, Hprev, D, AMM, BKR, gf=gf)
         if "attention.dec_att.bias" in need:
             K.colsum(ws.DAD, TB, A, A, grads["attention.dec_att.bias"], ws.work)
         # d(att_enc) summed over t, full_att grads (:56-57), then enc_att grads (:54)
@@ -469,20 +475,20 @@ class DecoderCore:
         if "attention.full_att.bias" in need:
             K.colsum(ws.BF_PART, nblk, 1, 1, grads["attention.full_att.bias"], ws.work)
         if "attention.enc_att.weight" in need:
-            self._gemm_into(ws, grads["attention.enc_att.weight"], E, A, E, B * P, ws.DATT, A, enc, E, AMM, BKR)
+            self._gemm_into(ws, grads["attention.enc_att.weight"], E, A, E, B * P, ws.DATT, A, enc, E, AMM, BKR, gf=gf)
         if "attention.enc_att.bias" in need:
             K.colsum(ws.DATT, B * P, A, A, grads["attention.enc_att.bias"], ws.work)
         # d(encoder_out): init mean (:161) + context sums (:59-60) + enc_att (:54)
         if denc is not None:
-            K.gemm([K.problem(B, E, D, ws.DH0, D, p["h_lin.weight"], E, ws.DMEAN, E)], AK, BKR, K.TILE_64)
-            K.gemm([K.problem(B, E, D, dc0, D, p["c_lin.weight"], E, ws.DMEAN, E, beta=1.0)], AK, BKR, K.TILE_64)
+            K.gemm([K.problem(B, E, D, ws.DH0, D, p["h_lin.weight"], E, ws.DMEAN, E)], AK, BKR, K.TILE_64, flags=gf)
+            K.gemm([K.problem(B, E, D, dc0, D, p["c_lin.weight"], E, ws.DMEAN, E, beta=1.0)], AK, BKR, K.TILE_64, flags=gf)
             K.att_enc_dinput(st["alphas"], T * P, ws.DAWE, ws.DMEAN, B, T, P, E, denc)
             self._gemm_into(ws, denc, E, B * P, E, A, ws.DATT, A, p["attention.enc_att.weight"], E, AK, BKR,
-                            beta=1.0)
+                            beta=1.0, gf=gf)
         # embedding (only when fine-tuned, Q8): dX_emb = DG W_ih[:, :M] -> scatter-add by token
         if "embedding.weight" in need and not st["dense_emb"]:
             demb = grads["embedding.weight"]
             demb.zero_()
             dxe = ws.scratch[:TB * M].view(TB, M)
-            K.gemm(K.problem(TB, M, 4 * D, ws.DG, 4 * D, W_ih, X, dxe, M), AK, BKR, K.TILE_128)
+            K.gemm(K.problem(TB, M, 4 * D, ws.DG, 4 * D, W_ih, X, dxe, M), AK, BKR, K.TILE_128, flags=gf)
             K.embed_scatter_add(dxe, M, st["caps"], B, L, T, st["bt_dev"], M, demb)

@@ -15,6 +15,7 @@ import torch
 
 from . import kernels as K
 from ._lib import CAPMI_A_KMAJOR, CAPMI_A_MMAJOR as AMM, CAPMI_B_KROWS as BKR, CAPMI_B_NMAJOR_W
+from ._lib import CAPMI_GEMM_BF16, CAPMI_GEMM_SPLIT3
 from .decoder_core import PNAMES, DecoderCore
 
 CORE = DecoderCore()
@@ -53,6 +54,14 @@ def dense_embeddings(dec, caps):
     return e.contiguous()
 
 
+def gemm_flags(dec):
+    """Operand staging of the decoder's GEMMs for ``dec.compute_precision`` (models/attention.py
+    set_compute_precision): 'fp32' -> fp32 MFMA, 'fp32-x3' -> CAPMI_GEMM_SPLIT3 (fp32-accurate),
+    'bf16' -> CAPMI_GEMM_BF16."""
+    prec = getattr(dec, "compute_precision", "fp32")
+    return {"fp32": 0, "fp32-x3": CAPMI_GEMM_SPLIT3, "bf16": CAPMI_GEMM_BF16}[prec]
+
+
 def _seed():
     return int(torch.randint(0, 2 ** 62, (1,)).item())
 
@@ -65,7 +74,7 @@ class AttentionDecoderFn(torch.autograd.Function):
         drop = dec.dropout.p if dec.training else 0.0
         preds, alphas, st = CORE.forward(p, enc, caps, decode_lengths, dropout_p=drop,
                                          training=dec.training, seed=_seed() if drop > 0 else 0,
-                                         emb_dense=dense_embeddings(dec, caps))
+                                         emb_dense=dense_embeddings(dec, caps), gemm_flags=gemm_flags(dec))
         _GEN[0] += 1
         st["gen"] = _GEN[0]
         ctx.st, ctx.p = st, p
@@ -148,7 +157,7 @@ def fused_loss_and_grads(dec, encoder_out, captions, caption_lengths, alpha_c, g
     host_seed = 0x5EED if seed_dev is not None else (_seed() if drop > 0 else 0)
     preds, alphas, st = CORE.forward(p, enc, caps, decode_lengths, dropout_p=drop, training=dec.training,
                                      seed=host_seed, seed_dev=seed_dev, emb_dense=dense_embeddings(dec, caps),
-                                     dup=dup)
+                                     dup=dup, gemm_flags=gemm_flags(dec))
     _GEN[0] += 1
     dm = st["dm"]
     B, T, V, L = dm.B, dm.T, dm.V, dm.L

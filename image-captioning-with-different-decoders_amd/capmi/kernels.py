@@ -62,11 +62,16 @@ def problem(M, N, K, A, lda, B, ldb, C, ldc, *, a_r1=0, a_s2=0, c_r1=0, c_s2=0, 
     return p
 
 
-def gemm(problems, amode=CAPMI_A_KMAJOR, bmode=CAPMI_B_NMAJOR_W, tile=CAPMI_TILE_128):
+def gemm(problems, amode=CAPMI_A_KMAJOR, bmode=CAPMI_B_NMAJOR_W, tile=CAPMI_TILE_128, flags=0):
+    """flags: 0 (fp32 MFMA), CAPMI_GEMM_BF16 (bf16 operands) or CAPMI_GEMM_SPLIT3 (fp32-accurate
+    three-term split on the bf16 matrix cores; capmi_gemm_ex)."""
     if isinstance(problems, GemmProblem):
         problems = [problems]
     arr = (GemmProblem * len(problems))(*problems)
-    call("capmi_gemm", arr, len(problems), amode, bmode, tile, stream())
+    if flags:
+        call("capmi_gemm_ex", arr, len(problems), amode, bmode, tile, flags, stream())
+    else:
+        call("capmi_gemm", arr, len(problems), amode, bmode, tile, stream())
 
 
 def gemm_workspace_bytes():
@@ -102,10 +107,12 @@ def sk_check(workspaces=None):
                            "launches since the last check are invalid (flags re-zeroed)")
 
 
-def gemm_sk(prob, amode, workspace, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W, bf16=False):
-    """bf16: operands rounded to bf16 in LDS, bf16 MFMA with fp32 accumulation (CAPMI_GEMM_BF16)."""
+def gemm_sk(prob, amode, workspace, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W, bf16=False, flags=None):
+    """bf16: operands rounded to bf16 in LDS, bf16 MFMA with fp32 accumulation (CAPMI_GEMM_BF16).
+    flags (overrides bf16): 0, CAPMI_GEMM_BF16 or CAPMI_GEMM_SPLIT3."""
     _cuda(workspace, dtype=torch.int32)
-    call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, bmode, tile, 1 if bf16 else 0, ptr(workspace),
+    f = (1 if bf16 else 0) if flags is None else flags
+    call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, bmode, tile, f, ptr(workspace),
          workspace.numel() * 4, stream())
 
 

@@ -532,6 +532,28 @@ extern "C" int capmi_gemm(const capmi_gemm_problem* probs, int nprob, int amode,
 
 extern "C" long long capmi_gemm_workspace_flag_bytes(void) { return sk_flag_bytes(cu_count()); }
 
+namespace {
+int flag_terms(int flags);
+bool terms_mode_ok(int terms, int amode, int bmode);
+}  // namespace
+
+extern "C" int capmi_gemm_ex(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, int tile, int flags,
+                             void* stream) {
+  const int terms = flag_terms(flags);
+  CAPMI_REQUIRE(terms >= 0, CAPMI_EINVAL);
+  if (terms == 0) return capmi_gemm(probs, nprob, amode, bmode, tile, stream);
+  CAPMI_REQUIRE(terms_mode_ok(terms, amode, bmode) && tile != CAPMI_TILE_128_W8, CAPMI_EINVAL);
+  GemmPlan g;
+  const int rc = gemm_plan(probs, nprob, amode, bmode, tile, g);
+  if (rc) return rc;
+  bool split_ok = g.nt_ok && g.vec;
+  for (int i = 0; i < nprob; ++i) split_ok = split_ok && probs[i].in_scale == nullptr;
+  // shapes the split forms do not cover (unaligned / generic-kernel problems): the fp32 kernel
+  if (!split_ok) return gemm_launch_dp(g, amode, bmode, as_stream(stream));
+  if (g.total == 0) return 0;
+  return gemm_nt_launch(g.a, amode, bmode, g.bm, g.bn, (int)g.total, as_stream(stream), terms);
+}
+
 extern "C" long long capmi_gemm_workspace_bytes(void) {
   const int cus = cu_count();
   // parked partials: (WGs per CU) * BM * BN floats per CU is 64 KB for 4 x 64x64 and for
@@ -566,7 +588,8 @@ bool sk_off() {
   return off;
 }
 // the launch capmi_gemm_sk makes for a problem (shared by the launcher and the plan query)
-int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, bool bf16, GemmPlan& g, bool& sk) {
+int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, int terms, GemmPlan& g, bool& sk) {
+  const bool bf16 = terms > 0;
   CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
   const int nkt = (prob->K + 31) / 32;
   const bool automatic = tile == CAPMI_TILE_AUTO;
@@ -591,7 +614,7 @@ int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, bo
     rc = gemm_plan(prob, 1, amode, bmode, CAPMI_TILE_128_W8, g);
     if (rc) return rc;
   }
-  const long long slots = (long long)cu_count() * (g.nt == 512 ? 1 : gemm_nt_wg_per_cu(g.bm, g.bn));
+  const long long slots = (long long)cu_count() * (g.nt == 512 ? 1 : gemm_nt_wg_per_cu(g.bm, g.bn, terms));
   const long long tiles = g.total;
   // short k-loops (< 16 k-tiles) stay data-parallel even in the hybrid form: splitting the last
   // rounds' tiles there cost 6-10 % on the layer1-3 1x1 shapes (tools/hybrid_ab.sh)
@@ -607,6 +630,20 @@ int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, bo
 }  // namespace
 
 namespace {
+// operand staging of the v2 kernel: 0 fp32, 1 bf16 (CAPMI_GEMM_BF16), 3 three-term split
+// (CAPMI_GEMM_SPLIT3); -1 for any other flag combination
+int flag_terms(int flags) {
+  if (flags == 0) return 0;
+  if (flags == CAPMI_GEMM_BF16) return 1;
+  if (flags == CAPMI_GEMM_SPLIT3) return 3;
+  return -1;
+}
+// the modes a split-staged (terms > 0) launch supports (gemm_nt.hip: gemm_nt_launch)
+bool terms_mode_ok(int terms, int amode, int bmode) {
+  if (terms == 0) return true;
+  if (terms == 1 && bmode == 0) return amode == 0 || amode == 2 || amode == 4;
+  return (amode == 0 && bmode <= 1) || (amode == 1 && bmode == 1);
+}
 int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, GemmArgs& a, int& bn, bool& sk,
             long long& total);
 int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total,
@@ -643,9 +680,14 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
     if (generic) *generic = 0;
     return 0;
   }
-  CAPMI_REQUIRE((flags & ~CAPMI_GEMM_BF16) == 0, CAPMI_EINVAL);
-  const int rc = sk_decide(prob, amode, bmode, tile, (flags & CAPMI_GEMM_BF16) != 0, g, sk);
+  int terms = flag_terms(flags);
+  CAPMI_REQUIRE(terms >= 0 && terms_mode_ok(terms, amode, bmode), CAPMI_EINVAL);
+  int rc = sk_decide(prob, amode, bmode, tile, terms, g, sk);
   if (rc) return rc;
+  if (terms > 0 && !(g.nt_ok && g.nt == 256 && (prob->in_scale == nullptr || amode == CAPMI_A_CONV_NHWC))) {
+    rc = sk_decide(prob, amode, bmode, tile, 0, g, sk);
+    if (rc) return rc;
+  }
   if (threads) *threads = g.nt_ok ? g.nt : 256;
   if (bm) *bm = g.bm;
   if (bn) *bn = g.bn;
@@ -854,22 +896,27 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   if (flags == CAPMI_GEMM_BF16_IO) return gemm_bf16_io(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3) return gemm_x3(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3P) return gemm_x3p(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
-  CAPMI_REQUIRE((flags & ~CAPMI_GEMM_BF16) == 0, CAPMI_EINVAL);
-  const bool bf16 = (flags & CAPMI_GEMM_BF16) != 0;
-  const int rc = sk_decide(prob, amode, bmode, tile, bf16, g, sk);
+  int terms = flag_terms(flags);
+  CAPMI_REQUIRE(terms >= 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE(terms_mode_ok(terms, amode, bmode), CAPMI_EINVAL);
+  int rc = sk_decide(prob, amode, bmode, tile, terms, g, sk);
   if (rc) return rc;
-  CAPMI_REQUIRE(!bf16 || (g.nt_ok && g.nt == 256 && bmode == 0 && (amode == 0 || amode == 2 || amode == 4)),
-                CAPMI_EINVAL);
+  if (terms > 0 && !(g.nt_ok && g.nt == 256 && (prob->in_scale == nullptr || amode == CAPMI_A_CONV_NHWC))) {
+    // shapes the split forms do not cover (unaligned / generic-kernel problems): the fp32 kernel
+    terms = 0;
+    rc = sk_decide(prob, amode, bmode, tile, 0, g, sk);
+    if (rc) return rc;
+  }
   hipStream_t s = as_stream(stream);
   if (!sk) {
     if (g.total == 0) return 0;
-    return bf16 ? gemm_nt_launch(g.a, amode, bmode, g.bm, g.bn, (int)g.total, s, true)
-                : gemm_launch_dp(g, amode, bmode, s);
+    return terms ? gemm_nt_launch(g.a, amode, bmode, g.bm, g.bn, (int)g.total, s, terms)
+                 : gemm_launch_dp(g, amode, bmode, s);
   }
   CAPMI_REQUIRE(workspace != nullptr && aligned16(workspace), CAPMI_EINVAL);
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
   const int cus = cu_count();
-  const long long slots = (long long)cus * (g.nt == 512 ? 1 : gemm_nt_wg_per_cu(g.bm, g.bn));
+  const long long slots = (long long)cus * (g.nt == 512 ? 1 : gemm_nt_wg_per_cu(g.bm, g.bn, terms));
   GemmArgs& a = g.a;
   a.sk_nkt = (prob->K + 31) / 32;
   // hybrid: with more than two rounds of tiles, all but the last 1-2 rounds' worth run whole
@@ -879,7 +926,7 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   a.sk_groups = sk_xcd_groups() && a.sk_workers % 8 == 0 && g.total >= 64 ? 8 : 1;
   a.sk_flags = static_cast<int*>(workspace);
   a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
-  return gemm_nt_launch(a, amode, bmode, g.bm, g.bn, a.sk_workers, s, bf16, g.nt);
+  return gemm_nt_launch(a, amode, bmode, g.bm, g.bn, a.sk_workers, s, terms, g.nt);
 }
 
 extern "C" int capmi_gemm_sk(const capmi_gemm_problem* prob, int amode, int bmode, int tile,

@@ -29,7 +29,7 @@ __device__ __forceinline__ long long remap(long long r, long long r1, long long 
 // v2 kernel: A K-major dense / NHWC conv / NHWC4 conv1 / M-major (k rows), B = W[N][K] or k rows;
 // BM x BN in {128x128, 128x64, 64x64}
 int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int blocks, hipStream_t s,
-                   bool bf16 = false, int nt = 256);
+                   int terms = 0, int nt = 256);
 // bf16-in/bf16-out conv GEMM (gemm_bf16.hip): BM = 128, BN in {128, 64}, amode 0 (dense) / 2 (conv)
 int gemm_bf16_launch(const GemmArgs& a, int amode, int bm, int bn, int blocks, hipStream_t s);
 // fp32-accurate 3-way bf16 split GEMM (gemm_x3.hip): BM = 128, BN in {128, 64}, 512 threads,
@@ -40,4 +40,8 @@ int gemm_x3_launch(const GemmArgs& a, int amode, int bn, int blocks, hipStream_t
 // of GemmArgs::sk_nkt for it
 int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_t s);
 // resident workgroups per CU of the NT kernel for a tile shape (LDS / register bound)
-inline int gemm_nt_wg_per_cu(int bm, int bn) { return bm == 64 && bn == 64 ? 4 : 2; }
+// (terms 3: three bf16 LDS planes per operand, 60 KB for 64x64 and >= 90 KB for the larger tiles)
+inline int gemm_nt_wg_per_cu(int bm, int bn, int terms = 0) {
+  if (terms == 3) return bm == 64 && bn == 64 ? 2 : 1;
+  return bm == 64 && bn == 64 ? 4 : 2;
+}

@@ -61,33 +61,89 @@ constexpr int SB = BK2 + 8;  // bf16 LDS row stride (elements)
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ bf16x4 to_bf16x4(float4 v) {
-  bf16x4 r;
-  r.x = (__bf16)v.x;
-  r.y = (__bf16)v.y;
-  r.z = (__bf16)v.z;
-  r.w = (__bf16)v.w;
-  return r;
+
+// the exact split of gemm_x3.hip: t0 = RNE(x), t1 = RNE(x - t0), t2 = x - t0 - t1 (exact in bf16)
+template <int TERMS>
+__device__ __forceinline__ void split_terms(float x, __bf16 (&t)[TERMS]) {
+  t[0] = (__bf16)x;
+  if (TERMS == 3) {
+    const float r = x - (float)t[0];
+    t[1 % TERMS] = (__bf16)r;
+    t[2 % TERMS] = (__bf16)(r - (float)t[1 % TERMS]);
+  }
+}
+
+// four consecutive k of one row -> TERMS planes (plane stride PL bf16 elements)
+template <int TERMS, int PL>
+__device__ __forceinline__ void store_row4(__bf16* dst, float4 v) {
+  __bf16 t0[TERMS], t1[TERMS], t2[TERMS], t3[TERMS];
+  split_terms<TERMS>(v.x, t0);
+  split_terms<TERMS>(v.y, t1);
+  split_terms<TERMS>(v.z, t2);
+  split_terms<TERMS>(v.w, t3);
+#pragma unroll
+  for (int p = 0; p < TERMS; ++p) {
+    bf16x4 h;
+    h.x = t0[p];
+    h.y = t1[p];
+    h.z = t2[p];
+    h.w = t3[p];
+    *reinterpret_cast<bf16x4*>(dst + p * PL) = h;
+  }
+}
+
+// k rows k, k+1 of four consecutive rows (v0: row k, v1: row k+1, one float per row) -> per plane
+// four 32-bit stores at rows 0..3 (stride SB) of dst, k pair (k, k+1)
+template <int TERMS, int PL>
+__device__ __forceinline__ void store_kpair(__bf16* dst, float4 v0, float4 v1) {
+  const float a[4] = {v0.x, v0.y, v0.z, v0.w}, b[4] = {v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    __bf16 ta[TERMS], tb[TERMS];
+    split_terms<TERMS>(a[e], ta);
+    split_terms<TERMS>(b[e], tb);
+#pragma unroll
+    for (int p = 0; p < TERMS; ++p) {
+      const unsigned w = (unsigned)__builtin_bit_cast(unsigned short, ta[p]) |
+                         ((unsigned)__builtin_bit_cast(unsigned short, tb[p]) << 16);
+      *reinterpret_cast<unsigned*>(dst + p * PL + e * SB) = w;
+    }
+  }
 }
 
 // NT threads = NT/64 waves as (NT/128) rows x 2 columns: 256 (the 2x2 form, every mode) or 512
 // (128x128 tiles only, 4x2 waves of 32x64: one workgroup per CU moves a third fewer bytes per
 // k-tile through L2 and LDS than two 128x64 workgroups; forward modes only)
-template <int BM, int BN, int AMODE, int BMODE, bool PRO, bool SK, bool BF, int NT>
+// TERMS = 0: fp32 operands on v_mfma_f32_32x32x2_f32. TERMS = 1: both operands rounded to bf16
+// when staged (the BF form above). TERMS = 3: both operands split EXACTLY into three bf16 terms when
+// staged (a = a0 + a1 + a2, gemm_x3.hip's arithmetic: six cross products above 2^-23 |a||b| on the
+// bf16 matrix cores, fp32-accurate), three LDS planes per operand. With TERMS > 0 a transposed
+// operand (AMODE 1 / BMODE 1: k rows, m/n contiguous) is loaded as pairs of adjacent k rows and
+// transposed at the LDS store (one 32-bit store = two k of one row per plane), so the MFMA loop
+// reads [row][k] images with one ds_read_b128 per fragment in every mode.
+template <int BM, int BN, int AMODE, int BMODE, bool PRO, bool SK, int TERMS, int NT>
 __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
-  static_assert(!BF || (BMODE == 0 && AMODE != 1), "bf16 staging: row-major A (dense / conv) x W[N][K] only");
+  constexpr bool BF = TERMS > 0;
+  constexpr int TT = BF ? TERMS : 1;  // planes (array extents; the fp32 form never reads them)
+  static_assert(TERMS == 0 || TERMS == 1 || TERMS == 3, "terms");
+  static_assert(!BF || BMODE <= 1, "bf16 staging: B = W[N][K] or k rows");
   static_assert(NT == 256 || (NT == 512 && BMODE == 0 && AMODE != 1 && !BF), "512-thread form: forward modes");
   constexpr int WR = NT / 128;  // wave rows
   constexpr int WM = BM / WR, WN = BN / 2, TM = WM / 32, TN = WN / 32;
   constexpr int NA = BM * BK2 / 4 / NT, NB = BN * BK2 / 4 / NT;
   static_assert(NA >= 1 && NB >= 1, "tile");
-  __shared__ __attribute__((aligned(16))) float As[2][BM * S2];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN * S2];
+  static_assert(!BF || ((AMODE != 1 || NA % 2 == 0) && (BMODE != 1 || NB % 2 == 0)), "k-row pairs");
+  // floats per tile row and buffer: the fp32 [m][k] image (S2), or TERMS bf16 planes of SB
+  constexpr int ROWF = TERMS == 3 ? 3 * SB / 2 : S2;
+  static_assert(TERMS != 1 || SB / 2 <= S2, "bf16 plane");
+  constexpr int PLA = BM * SB, PLB = BN * SB;  // bf16 elements per plane
+  __shared__ __attribute__((aligned(16))) float As[2][BM * ROWF];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * ROWF];
   // row strides of the k-major images of transposed operands (AMODE 1 / BMODE >= 1): BK2 rows of
   // BM (BN) + 8 floats fit the [m][k] image's BM * S2 for BM >= 64; the +8 puts the two half-waves'
   // rows (4 apart) on disjoint bank halves
   constexpr int SMA = BM + 8, SMB = BN + 8;
-  static_assert(BK2 * SMA <= BM * S2 && BK2 * SMB <= BN * S2, "k-major LDS image");
+  static_assert(BK2 * SMA <= BM * ROWF && BK2 * SMB <= BN * ROWF, "k-major LDS image");
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
@@ -131,6 +187,15 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
     for (int i = 0; i < NA; ++i) {
       const int f = tid + i * NT;
       if (AMODE == 1) {
+        if (BF) {  // slots 2j, 2j+1: k rows 2kp, 2kp+1 of column group jq (transposed at the store)
+          const int u = tid + (i >> 1) * NT;
+          const int jq = u % AQ, kp = u / AQ;
+          a_ok[i] = m0 + jq * 4 < M;
+          a_base[i] = m0 + jq * 4;
+          a_ih0[i] = 2 * kp + (i & 1);
+          a_iw0[i] = jq;
+          continue;
+        }
         const int jq = (tid & 15) + 16 * (i % AQ16);
         const int m = m0 + jq * 4;
         a_ok[i] = m < M;  // M % 4 == 0
@@ -183,7 +248,14 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
         }
         continue;
       }
-      if (BMODE == 1) {
+      if (BMODE == 1 && BF) {
+        const int u = tid + (i >> 1) * NT;
+        const int jq = u % BQ, kp = u / BQ;
+        b_ok[i] = n0 + jq * 4 < N;
+        b_base[i] = n0 + jq * 4;
+        b_k[i] = 2 * kp + (i & 1);
+        b_kw[i] = jq;  // column group (the transposing store's row)
+      } else if (BMODE == 1) {
         const int jq = (tid & 15) + 16 * (i % BQ16);
         const int n = n0 + jq * 4;
         b_ok[i] = n < N;  // N % 4 == 0
@@ -295,20 +367,38 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
       if (BF) {
         __bf16* Ah = reinterpret_cast<__bf16*>(As[buf]);
         __bf16* Bh = reinterpret_cast<__bf16*>(Bs[buf]);
+        if (AMODE == 1) {
 #pragma unroll
-        for (int i = 0; i < NA; ++i) {
-          float4 v = st.ra[i];
-          if (PRO && AMODE == 2) v = relu4(fma4(v, st.sc, st.sh));
-          if (!((st.am >> i) & 1u)) v = f4(0.f);
-          const int f = tid + i * NT;
-          *reinterpret_cast<bf16x4*>(Ah + (f >> 3) * SB + kq) = to_bf16x4(v);
+          for (int j = 0; j < NA / 2; ++j) {
+            const float4 v0 = (st.am >> (2 * j)) & 1u ? st.ra[2 * j] : f4(0.f);
+            const float4 v1 = (st.am >> (2 * j + 1)) & 1u ? st.ra[2 * j + 1] : f4(0.f);
+            store_kpair<TT, PLA>(Ah + 4 * a_iw0[2 * j] * SB + a_ih0[2 * j], v0, v1);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < NA; ++i) {
+            float4 v = st.ra[i];
+            if (PRO && AMODE == 2) v = relu4(fma4(v, st.sc, st.sh));
+            if (!((st.am >> i) & 1u)) v = f4(0.f);
+            const int f = tid + i * NT;
+            store_row4<TT, PLA>(Ah + (f >> 3) * SB + kq, v);
+          }
         }
+        if (BMODE == 1) {
 #pragma unroll
-        for (int i = 0; i < NB; ++i) {
-          float4 v = st.rb[i];
-          if (!((st.bm >> i) & 1u)) v = f4(0.f);
-          const int f = tid + i * NT;
-          *reinterpret_cast<bf16x4*>(Bh + (f >> 3) * SB + kq) = to_bf16x4(v);
+          for (int j = 0; j < NB / 2; ++j) {
+            const float4 v0 = (st.bm >> (2 * j)) & 1u ? st.rb[2 * j] : f4(0.f);
+            const float4 v1 = (st.bm >> (2 * j + 1)) & 1u ? st.rb[2 * j + 1] : f4(0.f);
+            store_kpair<TT, PLB>(Bh + 4 * b_kw[2 * j] * SB + b_k[2 * j], v0, v1);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < NB; ++i) {
+            float4 v = st.rb[i];
+            if (!((st.bm >> i) & 1u)) v = f4(0.f);
+            const int f = tid + i * NT;
+            store_row4<TT, PLB>(Bh + (f >> 3) * SB + kq, v);
+          }
         }
         return;
       }
@@ -344,16 +434,28 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
         const __bf16* Bh = reinterpret_cast<const __bf16*>(Bs[buf]) + (wn0 + lr) * SB + 8 * lh;
 #pragma unroll
         for (int g = 0; g < BK2 / 16; ++g) {
-          bf16x8 a[TM], b[TN];
+          bf16x8 a[TT][TM], b[TT][TN];
 #pragma unroll
-          for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const bf16x8*>(Ah + 32 * i * SB + 16 * g);
+          for (int p = 0; p < TT; ++p) {
 #pragma unroll
-          for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Bh + 32 * j * SB + 16 * g);
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
+            for (int i = 0; i < TM; ++i)
+              a[p][i] = *reinterpret_cast<const bf16x8*>(Ah + p * PLA + 32 * i * SB + 16 * g);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+              b[p][j] = *reinterpret_cast<const bf16x8*>(Bh + p * PLB + 32 * j * SB + 16 * g);
+          }
+          // TERMS 3: the six products smallest first (gemm_x3.hip), product-major so that the
+          // TM x TN independent accumulators interleave between dependent MFMAs
+          constexpr int NPROD = TERMS == 3 ? 6 : 1;
+          constexpr int PA[6] = {1, 0, 2, 0, 1, 0}, PB[6] = {1, 2, 0, 1, 0, 0};
+#pragma unroll
+          for (int q = 6 - NPROD; q < 6; ++q)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+              for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[PA[q] % TT][i], b[PB[q] % TT][j], acc[i][j],
+                                                                   0, 0, 0);
         }
         return;
       }
@@ -659,13 +761,34 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
 template <int BM, int BN, int AMODE, int BMODE, bool PRO, bool SK, bool BF = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWavesPerEu<BM, BN>)))
 gemm_nt_kernel(const GemmArgs args) {
-  gemm_nt_body<BM, BN, AMODE, BMODE, PRO, SK, BF, 256>(args);
+  gemm_nt_body<BM, BN, AMODE, BMODE, PRO, SK, BF ? 1 : 0, 256>(args);
+}
+
+// split-staged dense GEMMs (the decoder's, every layout it uses): TERMS 1 (bf16 operands) or 3
+// (fp32-accurate three-term split); TERMS 3 holds three LDS planes per operand, so 64x64 tiles run
+// two workgroups per CU and the larger ones one (gemm_nt_wg_per_cu)
+template <int BM, int BN, int AMODE, int BMODE, bool SK, int TERMS>
+__global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(TERMS == 3 ? (BM == 64 && BN == 64 ? 2 : 1) : kWavesPerEu<BM, BN>)))
+gemm_nts_kernel(const GemmArgs args) {
+  gemm_nt_body<BM, BN, AMODE, BMODE, false, SK, TERMS, 256>(args);
+}
+
+template <int BM, int BN, bool SK, int TERMS>
+void launch_nts(const GemmArgs& a, int amode, int bmode, int blocks, hipStream_t s) {
+  const dim3 g(blocks), b(256);
+  if (amode == 0 && bmode == 0)
+    hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, 0, 0, SK, TERMS>), g, b, 0, s, a);
+  else if (amode == 0 && bmode == 1)
+    hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, 0, 1, SK, TERMS>), g, b, 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, 1, 1, SK, TERMS>), g, b, 0, s, a);
 }
 
 template <int AMODE, bool PRO, bool SK>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
 gemm_nt8_kernel(const GemmArgs args) {
-  gemm_nt_body<128, 128, AMODE, 0, PRO, SK, false, 512>(args);
+  gemm_nt_body<128, 128, AMODE, 0, PRO, SK, 0, 512>(args);
 }
 
 template <bool SK>
@@ -721,8 +844,23 @@ void launch_sk(const GemmArgs& a, int amode, int bmode, bool pro, int blocks, hi
 }
 
 template <int BM, int BN>
-int launch_bmbn(const GemmArgs& a, int amode, int bmode, bool pro, bool bf16, int blocks, hipStream_t s) {
-  if (bf16) {
+int launch_bmbn(const GemmArgs& a, int amode, int bmode, bool pro, int terms, int blocks, hipStream_t s) {
+  const bool bf16 = terms == 1 && bmode == 0 && amode != 1;  // the forward / conv bf16 forms
+  if (terms > 0 && !bf16) {
+    if (!((amode == 0 && bmode <= 1) || (amode == 1 && bmode == 1)) || pro) return CAPMI_EINVAL;
+    const bool sk = a.sk_workers > 0;
+    if (terms == 3) {
+      if (sk)
+        launch_nts<BM, BN, true, 3>(a, amode, bmode, blocks, s);
+      else
+        launch_nts<BM, BN, false, 3>(a, amode, bmode, blocks, s);
+    } else {
+      if (sk)
+        launch_nts<BM, BN, true, 1>(a, amode, bmode, blocks, s);
+      else
+        launch_nts<BM, BN, false, 1>(a, amode, bmode, blocks, s);
+    }
+  } else if (bf16) {
     if (a.sk_workers > 0)
       launch_sk_bf16<BM, BN, true>(a, amode, pro, blocks, s);
     else
@@ -738,14 +876,17 @@ int launch_bmbn(const GemmArgs& a, int amode, int bmode, bool pro, bool bf16, in
 }  // namespace
 
 int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int blocks, hipStream_t s,
-                   bool bf16, int nt) {
+                   int terms, int nt) {
+  const bool bf16 = terms > 0;
   bool pro = false;
   for (int i = 0; i < a.nprob; ++i) pro = pro || a.p[i].in_scale != nullptr;
   for (int i = 0; i < a.nprob; ++i)
     if (pro && a.p[i].in_scale == nullptr) return CAPMI_EINVAL;  // grouped: all or none
   if (pro && !((amode == 2 && bmode == 0) || (amode == 1 && bmode == 2))) return CAPMI_EINVAL;
   if (bmode == 2 && amode != 1) return CAPMI_EINVAL;
-  if (bf16 && !(bmode == 0 && (amode == 0 || amode == 2 || amode == 4))) return CAPMI_EINVAL;
+  if (terms != 0 && terms != 1 && terms != 3) return CAPMI_EINVAL;
+  if (terms == 3 && !((amode == 0 && bmode <= 1) || (amode == 1 && bmode == 1))) return CAPMI_EINVAL;
+  if (terms == 1 && !((bmode == 0 && amode != 1 && amode != 3) || (amode <= 1 && bmode == 1))) return CAPMI_EINVAL;
   if (nt == 512) {
     if (bm != 128 || bn != 128 || bf16 || bmode != 0 || !(amode == 0 || amode == 2 || amode == 4)) return CAPMI_EINVAL;
     if (a.sk_workers > 0)
@@ -755,8 +896,8 @@ int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int 
     CAPMI_LAUNCH_CHECK();
     return 0;
   }
-  if (bm == 128 && bn == 128) return launch_bmbn<128, 128>(a, amode, bmode, pro, bf16, blocks, s);
-  if (bm == 128 && bn == 64) return launch_bmbn<128, 64>(a, amode, bmode, pro, bf16, blocks, s);
-  if (bm == 64 && bn == 64) return launch_bmbn<64, 64>(a, amode, bmode, pro, bf16, blocks, s);
+  if (bm == 128 && bn == 128) return launch_bmbn<128, 128>(a, amode, bmode, pro, terms, blocks, s);
+  if (bm == 128 && bn == 64) return launch_bmbn<128, 64>(a, amode, bmode, pro, terms, blocks, s);
+  if (bm == 64 && bn == 64) return launch_bmbn<64, 64>(a, amode, bmode, pro, terms, blocks, s);
   return CAPMI_EINVAL;
 }

@@ -68,6 +68,7 @@ class AttentionDecoder(nn.Module):
         # the (B, L+1, 768) word-level layer-11 features that _create_bert_embeddings (:166-215)
         # builds; plug in a local BERT, or capmi.data.SyntheticBertEmbedder for benchmarks.
         self.bert_embedder = None
+        self.compute_precision = "fp32"  # set_compute_precision
 
         self.attention = SoftAttention(self.encoder_dim, self.decoder_dim, self.attention_dim)
         self.dropout = nn.Dropout(p=self.dropout)
@@ -84,6 +85,16 @@ class AttentionDecoder(nn.Module):
         self.fc.weight.data.uniform_(-0.1, 0.1)
         self.embedding.weight.data.uniform_(-0.1, 0.1)
         self.fine_tune_embeddings(on=True)
+
+    def set_compute_precision(self, precision):
+        """Arithmetic of the decoder's GEMMs on the MI355X (the per-step attention / LSTMCell
+        pointwise, softmax and loss kernels stay fp32 throughout): 'fp32' (the reference's, fp32
+        MFMA), 'fp32-x3' (fp32-accurate: both operands split exactly into three bf16 terms on the
+        bf16 matrix cores, as the encoder's 'fp32-x3') or 'bf16' (operands rounded to bf16, fp32
+        accumulation: the bf16 config, BASELINE config 5)."""
+        if precision not in ("fp32", "fp32-x3", "bf16"):
+            raise ValueError(precision)
+        self.compute_precision = precision
 
     def load_pretrained_embeddins(self, embeddings):
         """Reference :128-136 (name kept, typo included). GloVe tables stay fp64 (Q7)."""

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 12
+#define CAPMI_ABI_VERSION 13
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -133,6 +133,22 @@ int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int t
  * when there are >= 2 x CUs tiles filling >= 70 % of the last round, else k-tiles of 32, one
  * workgroup per CU, stream-K as capmi_gemm_sk. */
 #define CAPMI_GEMM_X3P 8
+/* CAPMI_GEMM_SPLIT3 (alone): fp32 A and B, both split exactly into three bf16 terms when staged to
+ * LDS (the CAPMI_GEMM_X3 arithmetic with no pre-split operand: fp32-accurate on the bf16 matrix
+ * cores). Dense modes only: CAPMI_A_KMAJOR x CAPMI_B_NMAJOR_W / CAPMI_B_KROWS and CAPMI_A_MMAJOR x
+ * CAPMI_B_KROWS (the decoder's forward, data-gradient and weight-gradient GEMMs); K % 4 == 0, 16-B
+ * aligned operands, M % 4 == 0 for CAPMI_A_MMAJOR, N % 4 == 0 for CAPMI_B_KROWS; no prologue, no
+ * stats. Tiles 64x64 (two workgroups per CU), 128x64, 128x128 (one). Also accepted by
+ * capmi_gemm_ex (grouped problems, ksplit). CAPMI_GEMM_BF16 accepts the same dense modes (bf16
+ * operands, one product). A problem of these modes that the split forms do not cover (an operand
+ * not 16-B aligned or a stride / size not a multiple of 4: the generic-kernel shapes) runs the fp32
+ * kernel instead. */
+#define CAPMI_GEMM_SPLIT3 16
+/* capmi_gemm with flags 0 / CAPMI_GEMM_BF16 / CAPMI_GEMM_SPLIT3 (dense modes above; grouped problems,
+ * ksplit and the epilogue as capmi_gemm). Replaces the decoder's per-timestep nn.Linear / LSTMCell
+ * GEMMs (models/attention.py:55,270,277-278) and their backward. */
+int capmi_gemm_ex(const capmi_gemm_problem* problems, int nprob, int amode, int bmode, int tile, int flags,
+                  void* stream);
 int capmi_gemm_sk_ex(const capmi_gemm_problem* problem, int amode, int bmode, int tile, int flags, void* workspace,
                      long long ws_bytes, void* stream);
 /* the launch capmi_gemm_sk_ex(..., flags, ...) would make (no GPU work): tile bm x bn, stream_k 0/1,

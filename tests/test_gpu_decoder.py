@@ -154,16 +154,19 @@ def _grad_check(got, want, name):
     return set()
 
 
+@pytest.mark.parametrize("precision", ["fp32", "fp32-x3"])
 @pytest.mark.parametrize("cfg", [
     dict(A=32, D=32, M=16, V=50, B=3, L=7, lengths=None, seed=41, emb=np.float32, ft_emb=False),
     dict(A=32, D=32, M=300, V=50, B=3, L=6, lengths=[6, 5, 3], seed=42, emb=np.float64, ft_emb=True),
     dict(A=512, D=512, M=512, V=8100, B=4, L=25, lengths=None, seed=43, emb=np.float32, ft_emb=False),
 ])
-def test_fused_train_step_matches_oracle(cfg):
-    """capmi fused loss + BPTT + clamp/Adam vs the oracle's reference-restated step."""
+def test_fused_train_step_matches_oracle(cfg, precision):
+    """capmi fused loss + BPTT + clamp/Adam vs the oracle's reference-restated step (fp32-x3: the
+    decoder GEMMs as fp32-accurate three-term bf16 splits, same tolerances)."""
     from capmi import decoder_fn as DF
     from capmi.optim import Adam
     dec, p = make_decoder(cfg["A"], cfg["D"], cfg["M"], cfg["V"], cfg["seed"], DEV, emb_dtype=cfg["emb"])
+    dec.set_compute_precision(precision)
     dec.fine_tune_embeddings(cfg["ft_emb"])
     dec.train()
     B, L, V = cfg["B"], cfg["L"], cfg["V"]
@@ -197,15 +200,17 @@ def test_fused_train_step_matches_oracle(cfg):
     _ = rnew
 
 
+@pytest.mark.parametrize("precision", ["fp32", "fp32-x3"])
 @pytest.mark.parametrize("F,d,cfg", [
     (7, 2, dict(A=512, D=512, M=512, V=8100, B=4, L=25, seed=44)),  # 224x224: 7x7 -> 14x14
     (2, 7, dict(A=32, D=32, M=16, V=50, B=3, L=7, seed=45))])       # 64x64: 2x2 -> 14x14
-def test_fused_dedup_matches_oracle(F, d, cfg):
+def test_fused_dedup_matches_oracle(F, d, cfg, precision):
     """The decoder on the F*F distinct rows of pixel-duplicated features (dup = d) against the
     oracle run on the reference's pooled (F d) x (F d) map: loss, predictions, alphas over all
     positions and every gradient, under the rules of test_fused_train_step_matches_oracle."""
     from capmi import decoder_fn as DF
     dec, p = make_decoder(cfg["A"], cfg["D"], cfg["M"], cfg["V"], cfg["seed"], DEV)
+    dec.set_compute_precision(precision)
     dec.train()
     B, L, V = cfg["B"], cfg["L"], cfg["V"]
     g = torch.Generator().manual_seed(cfg["seed"])

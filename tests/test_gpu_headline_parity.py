@@ -38,11 +38,14 @@ def _check_grads(grads, rraw, trainable):
         excused.get("attention.enc_att.weight", set()) | excused.get("attention.enc_att.bias", set()), excused
 
 
-def test_decoder_step_b64_matches_oracle():
+@pytest.mark.parametrize("precision", ["fp32", "fp32-x3"])
+def test_decoder_step_b64_matches_oracle(precision):
+    """fp32-x3 (the bench's decoder GEMMs, CAPMI_GEMM_SPLIT3) under the same tolerances as fp32."""
     from capmi import decoder_fn as DF
     torch.set_num_threads(_threads())
     A, D, M, V, B, L, seed = 512, 512, 512, 8100, 64, 25, 47
     dec, p = make_decoder(A, D, M, V, seed, DEV)
+    dec.set_compute_precision(precision)
     dec.fine_tune_embeddings(False)  # the bench's (and the reference's default) configuration
     dec.train()
     enc = gen.encoder_features(seed, B)
@@ -118,3 +121,41 @@ def test_train_step_224_grads_match_oracle():
     rloss, _, _, rraw, _, _, _ = R.train_step(p, trainable, feats, t(caps), [L] * B)
     assert_close(loss.view(()), rloss, 1e-5, 1e-6, "loss")
     _check_grads(grads, rraw, trainable)
+
+
+def test_decoder_step_b64_bf16_gemms():
+    """The bf16 config's decoder (set_compute_precision('bf16'): GEMM operands rounded to bf16, fp32
+    accumulation; attention / LSTM pointwise / softmax / loss kernels fp32) at the bench's size, on
+    the distinct feature rows the bench decodes (dup = 2), vs the fp32 oracle on the pooled map.
+    bf16 rounding (relative 2^-9 per operand) bounds it loosely, so the rule is aggregate: loss
+    rel. 2e-3, predictions / alphas relative L2 <= 1e-2, every gradient tensor relative L2 <= 3e-2,
+    except the attention-score parameters (enc_att / dec_att): their gradients are sums over
+    B*P*T ReLU-gated terms of both signs that cancel to ~1e-6, which amplifies the relative error
+    (measured 4-5 %), so <= 1e-1 there (full_att.bias is fp32 noise around 0 in both: max |g| < 1e-5)."""
+    from capmi import decoder_fn as DF
+    torch.set_num_threads(_threads())
+    A, D, M, V, B, L, seed, F, d = 512, 512, 512, 8100, 64, 25, 48, 7, 2
+    dec, p = make_decoder(A, D, M, V, seed, DEV)
+    dec.set_compute_precision("bf16")
+    dec.fine_tune_embeddings(False)
+    dec.train()
+    g = torch.Generator().manual_seed(seed)
+    distinct = torch.rand(B, F, F, 2048, generator=g)
+    pooled = distinct.repeat_interleave(d, 1).repeat_interleave(d, 2)
+    caps = gen.captions(seed, B, L, V)
+    trainable = [n for n, q in dec.named_parameters() if q.requires_grad]
+    grads = {n: torch.zeros_like(q) for n, q in dec.named_parameters() if q.requires_grad}
+    loss, preds, alphas = DF.fused_loss_and_grads(dec, distinct.to(DEV), t(caps, DEV), [L] * B, 1.0, grads, dup=d)
+    torch.cuda.synchronize()
+    rloss, rpreds, ralphas, rraw, _, _, _ = R.train_step(p, set(trainable), pooled.reshape(B, -1, 2048), t(caps),
+                                                         [L] * B)
+    assert abs(float(loss) - float(rloss)) <= 2e-3 * abs(float(rloss)), (float(loss), float(rloss))
+    assert rel_err(preds.cpu(), rpreds) <= 1e-2
+    assert rel_err(alphas.cpu(), ralphas) <= 1e-2
+    for n in trainable:
+        got, want = grads[n].view_as(rraw[n]).cpu(), rraw[n]
+        if n == "attention.full_att.bias":
+            assert float(got.abs().max()) < 1e-5 and float(want.abs().max()) < 1e-5, n
+            continue
+        tol = 1e-1 if n.startswith(("attention.enc_att", "attention.dec_att")) else 3e-2
+        assert rel_err(got, want) <= tol, (n, rel_err(got, want))
