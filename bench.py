@@ -521,8 +521,9 @@ def main():
                                     "encoder fine-tuned (layer2-4, BN train mode), one training step per batch")
                        if ft else ("'bert_attention' decoder (768-d synthetic BERT word features) + frozen "
                                    "ResNet-101 encoder (BN train mode), one training step per batch" +
-                                   ("; encoder convs bf16 MFMA (fp32 accumulate), decoder fp32 (the reference "
-                                    "forces fp32 at the LSTM input)" if encoder._runner.bf16 else "")) if bert else
+                                   ("; encoder convs bf16 MFMA (fp32 accumulate), decoder GEMMs "
+                                    f"{decoder.compute_precision} (attention / LSTM pointwise / softmax / loss fp32)"
+                                    if encoder._runner.bf16 else "")) if bert else
                        ("'attention' decoder + frozen ResNet-101 encoder (BN train mode), "
                         "one training step per batch"),
                        "per_gpu_batch": B, "global_batch": B * N, "image_size": args.image_size,
