@@ -47,8 +47,14 @@ def _dsplit(M, N, nt, K_, target=None):
     return max(1, min(kt, max(-(-kt // 16), round(target / tiles))))
 
 
-def _split(M, N, K_, tile, target=256, min_k=128):
+# workgroups a per-timestep GEMM launch aims for (CAPMI_DEC_WGS, A/B measurement: fewer, longer
+# workgroups leave more CUs to the encoder stream running beside the decoder)
+DEC_WGS = int(os.environ.get("CAPMI_DEC_WGS", "256"))
+
+
+def _split(M, N, K_, tile, target=None, min_k=128):
     """K-split so that tiles*split ~ target workgroups (each split keeps >= min_k of K)."""
+    target = DEC_WGS if target is None else target
     t = K.tiles_for(M, N, tile)
     if t >= target:
         return 1
@@ -69,8 +75,8 @@ class DecoderDims:
         self.s_h = (_split(B, A, D, K.TILE_64), _split(B, E, D, K.TILE_64), _split(B, 4 * D, D, K.TILE_64))
         self.s_x = _split(B, 4 * D, E, K.TILE_64)
         self.s_dx = _split(B, E, 4 * D, K.TILE_64)
-        self.s_dh = (_split(B, D, 4 * D, K.TILE_64, 96), _split(B, D, E, K.TILE_64, 96),
-                     _split(B, D, A, K.TILE_64, 64))
+        self.s_dh = (_split(B, D, 4 * D, K.TILE_64, DEC_WGS * 3 // 8), _split(B, D, E, K.TILE_64, DEC_WGS * 3 // 8),
+                     _split(B, D, A, K.TILE_64, DEC_WGS // 4))
         # decoder_step.hip (CAPMI_DEC_FUSED, opt-in): "1" the attention forward (score + softmax +
         # context + gate) and backward (gate split + context + softmax + score) as one launch each,
         # reading the split-K GEMM partials; "2" also the last-arriver GEMMs with the LSTM cell in

@@ -10,6 +10,7 @@ import torch
 
 from ._lib import DstepEpi, DstepSeg
 from ._lib import (CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_GEMM_BF16_IO, CAPMI_GEMM_X3, CAPMI_GEMM_X3P,
+                   CAPMI_GEMM_SPLIT3,
                    CAPMI_COLSUM_GROUPS, CAPMI_TILE_128, CAPMI_TILE_64,
                    CAPMI_TILE_128x64, CAPMI_TILE_AUTO, GemmProblem, call, lib)
 
@@ -199,24 +200,29 @@ def gemm_x3_kernel_name(prob, amode, tile=CAPMI_TILE_AUTO):
     return f"gemm_x3_kernel<{v[1].value}, {amode}, {b(bool(prob.in_scale))}, {b(v[2].value)}>"
 
 
-def gemm_sk_plan(prob, amode, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W, bf16=False, threads=False):
+def gemm_sk_plan(prob, amode, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W, bf16=False, threads=False,
+                 flags=None):
     """(bm, bn, stream_k, generic[, threads]) of the launch gemm_sk would make for ``prob``."""
+    f = (1 if bf16 else 0) if flags is None else flags
     v = [ctypes.c_int(0) for _ in range(5)]
-    call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, bmode, tile, 1 if bf16 else 0,
-         *[ctypes.byref(x) for x in v])
+    call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, bmode, tile, f, *[ctypes.byref(x) for x in v])
     return tuple(x.value for x in v[:5 if threads else 4])
 
 
-def gemm_sk_kernel_name(prob, amode, bmode=CAPMI_B_NMAJOR_W, bf16=False, tile=CAPMI_TILE_AUTO):
+def gemm_sk_kernel_name(prob, amode, bmode=CAPMI_B_NMAJOR_W, bf16=False, tile=CAPMI_TILE_AUTO, flags=None):
     """The kernel symbol (as rocprofv3 prints it) of the launch gemm_sk(..., tile) makes."""
-    bm, bn, sk, generic, nt = gemm_sk_plan(prob, amode, tile, bmode, bf16, threads=True)
+    f = (1 if bf16 else 0) if flags is None else flags
+    bm, bn, sk, generic, nt = gemm_sk_plan(prob, amode, tile, bmode, threads=True, flags=f)
     b = lambda v: "true" if v else "false"  # noqa: E731
     pro = b(bool(prob.in_scale))
     if generic:
         return "gemm_kernel (generic)"
     if nt == 512:
         return f"gemm_nt8_kernel<{amode}, {pro}, {b(sk)}>"
-    return f"gemm_nt_kernel<{bm}, {bn}, {amode}, {bmode}, {pro}, {b(sk)}, {b(bf16)}>"
+    split = f == CAPMI_GEMM_SPLIT3 or (f == 1 and (amode == 1 or bmode == 1))
+    if split and not (f == 1 and bmode == 0 and amode != 1):
+        return f"gemm_nts_kernel<{bm}, {bn}, {amode}, {bmode}, {b(sk)}, {3 if f == CAPMI_GEMM_SPLIT3 else 1}>"
+    return f"gemm_nt_kernel<{bm}, {bn}, {amode}, {bmode}, {pro}, {b(sk)}, {b(f == 1)}>"
 
 
 def stat_tiles(M, tile=CAPMI_TILE_128):

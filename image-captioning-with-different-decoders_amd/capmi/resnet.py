@@ -13,12 +13,14 @@ running-stat update in train mode) and (c) the apply+ReLU, fused into the next
 conv's A-tile load or into the bottleneck tail kernel (BN + residual + ReLU).
 On CPU tensors the modules run their ordinary nn forward (config 1 plumbing).
 """
+import os
+
 import torch
 import torch.nn as nn
 
 from . import kernels as K
 from ._lib import CAPMI_A_CONV_NHWC, CAPMI_A_CONV_NHWC4, CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_B_CONV_NHWC
-from ._lib import CAPMI_B_KROWS, CAPMI_B_NMAJOR_W
+from ._lib import CAPMI_B_KROWS, CAPMI_B_NMAJOR_W, CAPMI_GEMM_BF16, CAPMI_GEMM_SPLIT3
 
 AK, AMM, AC = CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_A_CONV_NHWC
 BW, BKR, BCONV = CAPMI_B_NMAJOR_W, CAPMI_B_KROWS, CAPMI_B_CONV_NHWC
@@ -257,10 +259,12 @@ class EncoderRunner:
             else:
                 launch()
             return Ho, Wo, rows
-        bf = self.bf16
-        launch = lambda: K.gemm_sk(prob, mode, self._ws["sk"], K.TILE_AUTO, bf16=bf)  # noqa: E731
+        # conv1 in the x3 mode: both operands split in-kernel (CAPMI_GEMM_SPLIT3; its K = 7*7*4 is
+        # not the gemm_x3 kernel's multiple of 32)
+        flags = CAPMI_GEMM_BF16 if self.bf16 else (CAPMI_GEMM_SPLIT3 if self.x3 and nchw else 0)
+        launch = lambda: K.gemm_sk(prob, mode, self._ws["sk"], K.TILE_AUTO, flags=flags)  # noqa: E731
         if self.conv_hook is not None:
-            key = K.gemm_sk_kernel_name(prob, mode, bf16=bf)
+            key = K.gemm_sk_kernel_name(prob, mode, flags=flags)
             self.conv_hook(tag, 2.0 * rows * co * Kd, launch, key)
         else:
             launch()
@@ -483,6 +487,9 @@ class _Pool:
         return t[:n]
 
 
+_FT_DGRAD_X3 = os.environ.get("CAPMI_FT_DGRAD_X3", "1") != "0"
+
+
 class FineTuneRunner:
     """EncoderAttention.fine_tune(True) (models/encoder.py:112-121): layer2, layer3 and layer4
     (children()[5:]) are trainable, BatchNorm stays in train mode (batch statistics).
@@ -594,8 +601,18 @@ class FineTuneRunner:
         return out
 
     # ------------------------------------------------------------------ backward
+    def _flags(self, prob, amode, bmode):
+        """Data gradients (convs of dY / 1x1 GEMMs on the transposed weight: A row-major, B = W[N][K],
+        no prologue) run the fp32-accurate three-term split when the encoder is in the x3 mode
+        (CAPMI_GEMM_SPLIT3); weight gradients (k-row operands) stay on the fp32 MFMA kernel, where
+        the split's transposing store is slower (tools/dec_gemm_ab.py). CAPMI_FT_DGRAD_X3=0: all fp32."""
+        if (self.r.x3 and _FT_DGRAD_X3 and bmode == CAPMI_B_NMAJOR_W and amode in (CAPMI_A_KMAJOR, CAPMI_A_CONV_NHWC)
+                and not prob.in_scale):
+            return CAPMI_GEMM_SPLIT3
+        return 0
+
     def _gemm(self, prob, amode, bmode, tile=K.TILE_AUTO):
-        K.gemm_sk(prob, amode, self.r._ws["sk"], tile, bmode)
+        K.gemm_sk(prob, amode, self.r._ws["sk"], tile, bmode, flags=self._flags(prob, amode, bmode))
 
     @torch.no_grad()
     def backward(self, dfeat, grads, hook=None):
@@ -635,7 +652,7 @@ class FineTuneRunner:
                 self._gemm(prob, amode, bmode, tile)
             else:
                 hook(tag, flops, lambda: self._gemm(prob, amode, bmode, tile),
-                     K.gemm_sk_kernel_name(prob, amode, bmode, tile=tile))
+                     K.gemm_sk_kernel_name(prob, amode, bmode, tile=tile, flags=self._flags(prob, amode, bmode)))
 
         K.adaptive_avgpool_bwd_nhwc(dfeat.contiguous(), N, stt["H"], stt["W"], stt["C"], stt["OH"], stt["OW"],
                                     dA[0])

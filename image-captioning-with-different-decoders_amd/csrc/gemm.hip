@@ -518,6 +518,17 @@ int cu_count() {
   return cache[dev];
 }
 
+// CUs the stream-K grids are sized for: cu_count(), or CAPMI_SK_CUS (A/B measurement: fewer
+// persistent workers than CUs leave CUs free for the concurrently running decoder stream)
+int sk_cus() {
+  static const int n = [] {
+    const char* e = getenv("CAPMI_SK_CUS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 && v < cu_count() ? v : cu_count();
+  }();
+  return n;
+}
+
 constexpr int kSkMaxWgPerCu = 4;
 long long sk_flag_bytes(int cus) { return ((long long)(cus * kSkMaxWgPerCu + 1) * 4 + 255) / 256 * 256; }
 }  // namespace
@@ -614,7 +625,7 @@ int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, in
     rc = gemm_plan(prob, 1, amode, bmode, CAPMI_TILE_128_W8, g);
     if (rc) return rc;
   }
-  const long long slots = (long long)cu_count() * (g.nt == 512 ? 1 : gemm_nt_wg_per_cu(g.bm, g.bn, terms));
+  const long long slots = (long long)sk_cus() * (g.nt == 512 ? 1 : gemm_nt_wg_per_cu(g.bm, g.bn, terms));
   const long long tiles = g.total;
   // short k-loops (< 16 k-tiles) stay data-parallel even in the hybrid form: splitting the last
   // rounds' tiles there cost 6-10 % on the layer1-3 1x1 shapes (tools/hybrid_ab.sh)
@@ -641,7 +652,8 @@ int flag_terms(int flags) {
 // the modes a split-staged (terms > 0) launch supports (gemm_nt.hip: gemm_nt_launch)
 bool terms_mode_ok(int terms, int amode, int bmode) {
   if (terms == 0) return true;
-  if (terms == 1 && bmode == 0) return amode == 0 || amode == 2 || amode == 4;
+  if (bmode == 0 && (amode == 2 || amode == 4)) return true;  // convs (terms 3: no BN prologue)
+  if (terms == 1 && bmode == 0) return amode == 0;
   return (amode == 0 && bmode <= 1) || (amode == 1 && bmode == 1);
 }
 int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, GemmArgs& a, int& bn, bool& sk,
@@ -684,7 +696,7 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
   CAPMI_REQUIRE(terms >= 0 && terms_mode_ok(terms, amode, bmode), CAPMI_EINVAL);
   int rc = sk_decide(prob, amode, bmode, tile, terms, g, sk);
   if (rc) return rc;
-  if (terms > 0 && !(g.nt_ok && g.nt == 256 && (prob->in_scale == nullptr || amode == CAPMI_A_CONV_NHWC))) {
+  if (terms > 0 && !(g.nt_ok && g.nt == 256 && (prob->in_scale == nullptr || (terms == 1 && amode == CAPMI_A_CONV_NHWC)))) {
     rc = sk_decide(prob, amode, bmode, tile, 0, g, sk);
     if (rc) return rc;
   }
@@ -727,7 +739,7 @@ int gemm_bf16_io(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
   const long long total = (long long)a.tiles_m[0] * a.tiles_n[0];
   a.tiles_begin[1] = (int)total;
   const int cus = cu_count();
-  const long long slots = (long long)cus * 2;
+  const long long slots = (long long)sk_cus() * 2;
   const int nkt = p.K / 64;
   const long long rounds = (total + slots - 1) / slots;
   const bool sk = !sk_off() && workspace != nullptr && nkt >= 4 && (double)total / (double)(rounds * slots) < 0.9;
@@ -773,7 +785,7 @@ int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gemm
   a.tiles_n[0] = (int)cdiv(p.N, bn);
   total = (long long)a.tiles_m[0] * a.tiles_n[0];
   a.tiles_begin[1] = (int)total;
-  const long long slots = cu_count();
+  const long long slots = sk_cus();
   const int nkt = p.K / 32;
   const long long rounds = (total + slots - 1) / slots;
   sk = !sk_off() && total > 0 && nkt >= 8 && (double)total / (double)(rounds * slots) < 0.9;
@@ -825,7 +837,7 @@ int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
   }
   total = (long long)a.tiles_m[0] * a.tiles_n[0];
   a.tiles_begin[1] = (int)total;
-  const long long slots2 = 2LL * cu_count();
+  const long long slots2 = 2LL * sk_cus();
   const long long rounds2 = (total + slots2 - 1) / slots2;
   if (!x3p_force32() && total >= slots2 && (double)total / (double)(rounds2 * slots2) >= 0.7) {
     bk = 16;
@@ -833,7 +845,7 @@ int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
     return 0;
   }
   bk = 32;
-  const long long slots = cu_count();
+  const long long slots = sk_cus();
   const int nkt = p.K / 32;
   const long long rounds = (total + slots - 1) / slots;
   sk = !sk_off() && total > 0 && nkt >= 8 && (double)total / (double)(rounds * slots) < 0.9;
@@ -853,7 +865,7 @@ int gemm_x3p(const capmi_gemm_problem* prob, int amode, int bmode, void* workspa
   CAPMI_REQUIRE(aligned16(workspace), CAPMI_EINVAL);
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
   const int cus = cu_count();
-  const long long slots = cus;
+  const long long slots = sk_cus();
   a.sk_nkt = prob->K / bk;  // k-tiles of the x3p kernel
   a.sk_dp_tiles = sk_hybrid() && total >= 2 * slots ? (int)((total / slots - 1) * slots) : 0;
   a.sk_units = (total - a.sk_dp_tiles) * a.sk_nkt;
@@ -877,7 +889,7 @@ int gemm_x3(const capmi_gemm_problem* prob, int amode, int bmode, int tile, void
   CAPMI_REQUIRE(aligned16(workspace), CAPMI_EINVAL);
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
   const int cus = cu_count();
-  const long long slots = cus;
+  const long long slots = sk_cus();
   a.sk_nkt = prob->K / 32;
   a.sk_dp_tiles = sk_hybrid() && total >= 2 * slots ? (int)((total / slots - 1) * slots) : 0;
   a.sk_units = (total - a.sk_dp_tiles) * a.sk_nkt;
@@ -901,8 +913,9 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   CAPMI_REQUIRE(terms_mode_ok(terms, amode, bmode), CAPMI_EINVAL);
   int rc = sk_decide(prob, amode, bmode, tile, terms, g, sk);
   if (rc) return rc;
-  if (terms > 0 && !(g.nt_ok && g.nt == 256 && (prob->in_scale == nullptr || amode == CAPMI_A_CONV_NHWC))) {
-    // shapes the split forms do not cover (unaligned / generic-kernel problems): the fp32 kernel
+  if (terms > 0 && !(g.nt_ok && g.nt == 256 && (prob->in_scale == nullptr || (terms == 1 && amode == CAPMI_A_CONV_NHWC)))) {
+    // shapes the split forms do not cover (unaligned / generic-kernel problems, the three-term
+    // split with a BN prologue): the fp32 kernel
     terms = 0;
     rc = sk_decide(prob, amode, bmode, tile, 0, g, sk);
     if (rc) return rc;
@@ -916,7 +929,7 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   CAPMI_REQUIRE(workspace != nullptr && aligned16(workspace), CAPMI_EINVAL);
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
   const int cus = cu_count();
-  const long long slots = (long long)cus * (g.nt == 512 ? 1 : gemm_nt_wg_per_cu(g.bm, g.bn, terms));
+  const long long slots = (long long)sk_cus() * (g.nt == 512 ? 1 : gemm_nt_wg_per_cu(g.bm, g.bn, terms));
   GemmArgs& a = g.a;
   a.sk_nkt = (prob->K + 31) / 32;
   // hybrid: with more than two rounds of tiles, all but the last 1-2 rounds' worth run whole

@@ -777,7 +777,11 @@ gemm_nts_kernel(const GemmArgs args) {
 template <int BM, int BN, bool SK, int TERMS>
 void launch_nts(const GemmArgs& a, int amode, int bmode, int blocks, hipStream_t s) {
   const dim3 g(blocks), b(256);
-  if (amode == 0 && bmode == 0)
+  if (TERMS == 3 && amode == 2)  // conv (no prologue: the data gradients' dY)
+    hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, TERMS == 3 ? 2 : 0, 0, SK, TERMS>), g, b, 0, s, a);
+  else if (TERMS == 3 && amode == 4)  // conv1 on the NHWC4 images
+    hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, TERMS == 3 ? 4 : 0, 0, SK, TERMS>), g, b, 0, s, a);
+  else if (amode == 0 && bmode == 0)
     hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, 0, 0, SK, TERMS>), g, b, 0, s, a);
   else if (amode == 0 && bmode == 1)
     hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, 0, 1, SK, TERMS>), g, b, 0, s, a);
@@ -847,7 +851,8 @@ template <int BM, int BN>
 int launch_bmbn(const GemmArgs& a, int amode, int bmode, bool pro, int terms, int blocks, hipStream_t s) {
   const bool bf16 = terms == 1 && bmode == 0 && amode != 1;  // the forward / conv bf16 forms
   if (terms > 0 && !bf16) {
-    if (!((amode == 0 && bmode <= 1) || (amode == 1 && bmode == 1)) || pro) return CAPMI_EINVAL;
+    const bool conv3 = terms == 3 && bmode == 0 && (amode == 2 || amode == 4);
+    if (!((amode == 0 && bmode <= 1) || (amode == 1 && bmode == 1) || conv3) || pro) return CAPMI_EINVAL;
     const bool sk = a.sk_workers > 0;
     if (terms == 3) {
       if (sk)
@@ -885,7 +890,9 @@ int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int 
   if (pro && !((amode == 2 && bmode == 0) || (amode == 1 && bmode == 2))) return CAPMI_EINVAL;
   if (bmode == 2 && amode != 1) return CAPMI_EINVAL;
   if (terms != 0 && terms != 1 && terms != 3) return CAPMI_EINVAL;
-  if (terms == 3 && !((amode == 0 && bmode <= 1) || (amode == 1 && bmode == 1))) return CAPMI_EINVAL;
+  if (terms == 3 && !((amode == 0 && bmode <= 1) || (amode == 1 && bmode == 1) ||
+                      (bmode == 0 && (amode == 2 || amode == 4) && !pro)))
+    return CAPMI_EINVAL;
   if (terms == 1 && !((bmode == 0 && amode != 1 && amode != 3) || (amode <= 1 && bmode == 1))) return CAPMI_EINVAL;
   if (nt == 512) {
     if (bm != 128 || bn != 128 || bf16 || bmode != 0 || !(amode == 0 || amode == 2 || amode == 4)) return CAPMI_EINVAL;

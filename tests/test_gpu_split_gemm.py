@@ -141,3 +141,58 @@ def test_split3_error_not_above_fp32_kernel():
         K.gemm(K.problem(M, N, Kd, X.float().to(DEV), Kd, W.float().to(DEV), Kd, C, N), 0, 0, 1, flags=flags)
         errs.append(float((C.double().cpu() - ref).norm() / ref.norm()))
     assert errs[1] <= 2 * errs[0] + 1e-9, errs
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3])
+def test_split3_conv1_nhwc4_stats(tile):
+    """conv1 as the x3 encoder runs it (CAPMI_GEMM_SPLIT3 on the NHWC4 images, K = 196) with the BN
+    statistics epilogue: fp32 tolerance vs fp64, statistics = sums of the stored output."""
+    import torch.nn.functional as F
+    from capmi._lib import CAPMI_GEMM_SPLIT3
+    K = _K()
+    N, H = 3, 46
+    x = rnd(N, 3, H, H, seed=21)
+    w = rnd(64, 3, 7, 7, seed=22) * 0.1
+    ref = F.conv2d(x, w, stride=2, padding=3)
+    ref_abs = F.conv2d(x.abs(), w.abs(), stride=2, padding=3)
+    Ho = ref.shape[2]
+    img4 = torch.empty(N * H * H * 4, device=DEV)
+    K.image_nhwc4(x.float().to(DEV).contiguous(), img4)
+    wp = torch.empty(64 * 49 * 4, device=DEV)
+    K.conv_weight_pack_pad(w.float().to(DEV).contiguous(), 4, wp)
+    M = N * Ho * Ho
+    out = torch.empty(M, 64, device=DEV)
+    stats = torch.empty(K.stat_tiles(M), 64, 2, device=DEV)
+    geo = dict(N=N, H=H, W=H, Cin=4, KH=7, KW=7, stride=2, pad=3, Ho=Ho, Wo=Ho)
+    ws = K.gemm_workspace(DEV)
+    K.gemm_sk(K.problem(M, 64, 196, img4, 0, wp, 196, out, 64, conv=geo, stats=stats), 4, ws, tile,
+              flags=CAPMI_GEMM_SPLIT3)
+    check(out.view(N, Ho, Ho, 64).permute(0, 3, 1, 2), ref, ref_abs, CAPMI_GEMM_SPLIT3, "conv1 NHWC4 x3")
+    s = stats.double().cpu().sum(0)
+    torch.testing.assert_close(s[:, 0], out.double().cpu().sum(0), rtol=1e-5, atol=1e-3)
+    assert "gemm_nts_kernel" in K.gemm_sk_kernel_name(
+        K.problem(M, 64, 196, img4, 0, wp, 196, out, 64, conv=geo, stats=stats), 4, tile=tile, flags=CAPMI_GEMM_SPLIT3)
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3])
+@pytest.mark.parametrize("k,stride,cin,cout,hw", [(3, 1, 64, 64, 14), (3, 2, 128, 128, 15), (1, 1, 64, 256, 9)])
+def test_split3_conv_nhwc(k, stride, cin, cout, hw, tile):
+    """The conv mode without prologue (the fine-tune data gradients' form) under CAPMI_GEMM_SPLIT3."""
+    import torch.nn.functional as F
+    from capmi._lib import CAPMI_GEMM_SPLIT3
+    K = _K()
+    N = 3
+    x = rnd(N, cin, hw, hw, seed=15)
+    w = rnd(cout, cin, k, k, seed=16) * 0.1
+    pad = k // 2
+    ref = F.conv2d(x, w, stride=stride, padding=pad)
+    ref_abs = F.conv2d(x.abs(), w.abs(), stride=stride, padding=pad)
+    Ho = ref.shape[2]
+    wp = torch.empty(cout, k, k, cin, device=DEV)
+    K.conv_weight_pack(w.float().to(DEV).contiguous(), wp)
+    out = torch.empty(N * Ho * Ho, cout, device=DEV)
+    geo = dict(N=N, H=hw, W=hw, Cin=cin, KH=k, KW=k, stride=stride, pad=pad, Ho=Ho, Wo=Ho)
+    ws = K.gemm_workspace(DEV)
+    K.gemm_sk(K.problem(N * Ho * Ho, cout, k * k * cin, x.permute(0, 2, 3, 1).contiguous().float().to(DEV), 0,
+                        wp, k * k * cin, out, cout, conv=geo), 2, ws, tile, flags=CAPMI_GEMM_SPLIT3)
+    check(out.view(N, Ho, Ho, cout).permute(0, 3, 1, 2), ref, ref_abs, CAPMI_GEMM_SPLIT3, f"conv{k} x3")

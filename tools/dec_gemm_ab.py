@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--B", type=int, default=64)
     ap.add_argument("--P", type=int, default=49)
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--tile", type=int, default=None, help="force this tile on the hoisted (stream-K) GEMMs")
     a = ap.parse_args()
     B, T, P, A, D, M, V, E = a.B, 24, a.P, 512, 512, 512, 8100, 2048
     dm = DecoderDims(B, T, 25, P, A, D, M, V, E)
@@ -72,7 +73,7 @@ def main():
                 if kind == "dp":
                     K.gemm(p, am, bm, tile, flags=f)
                 else:
-                    K.gemm_sk(p, am, ws, tile, bm, flags=f)
+                    K.gemm_sk(p, am, ws, tile if a.tile is None else a.tile, bm, flags=f)
             for _ in range(3):
                 launch()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
