@@ -141,6 +141,10 @@ def pool_dup(H, W, out_hw):
     return oh // fh
 
 
+# x3 mode: convs with K <= this run both operands split in-kernel (CAPMI_GEMM_SPLIT3) instead of gemm_x3
+_X3_SMALLK = int(os.environ.get("CAPMI_X3_SMALLK", "0"))
+
+
 class EncoderRunner:
     """Launch plan for the frozen ResNet-101 conv stack (children()[:-2] of torchvision's
     resnet101) on NHWC fp32 activations. Buffers are cached per input shape."""
@@ -213,6 +217,7 @@ class EncoderRunner:
         geo = dict(N=N, H=H, W=W, Cin=ci, KH=kh, KW=kw, stride=st, pad=pd, Ho=Ho, Wo=Wo)
         stats = ws_stats = self._ws["stats"] if train else None
         kw_ = dict(stats=ws_stats)
+        split3 = nchw and self.x3  # conv1 (K = 7*7*4) in the x3 mode
         if nchw:
             # conv1: the NCHW images are re-laid out once as NHWC with 4 channels (one float4 per
             # pixel); the implicit GEMM then runs over k = (kh, kw, c4), the 4th channel zero
@@ -222,6 +227,16 @@ class EncoderRunner:
             geo["Cin"] = 4
             prob = K.problem(rows, co, K4, img4, 0, w, K4, out, co, conv=geo, **kw_)
             mode = CAPMI_A_CONV_NHWC4
+        elif self.x3 and Kd <= _X3_SMALLK:
+            # short-k convs (layer1's K = 64): both operands split in-kernel on the 256-thread kernel
+            # (CAPMI_GEMM_SPLIT3, two workgroups per CU overlap one's epilogue with the other's loads)
+            sc, sh = in_ss if in_ss is not None else (None, None)
+            if kh == 1 and st == 1 and in_ss is None:
+                prob, mode = K.problem(rows, co, Kd, x, ci, w, Kd, out, co, **kw_), CAPMI_A_KMAJOR
+            else:
+                prob = K.problem(rows, co, Kd, x, 0, w, Kd, out, co, conv=geo, in_scale=sc, in_shift=sh, **kw_)
+                mode = CAPMI_A_CONV_NHWC
+            split3 = True
         elif self.x3 and in_ss is not None and co >= 128 and ci % 32 == 0 and Kd >= 128 and rows >= 12544:
             # x3p: the conv input relu(bn(y)) split once into three bf16 planes, then the GEMM with
             # both operands pre-split (gemm_x3p.hip). Where it pays (tools/x3_ab.py, batch 64): the
@@ -261,7 +276,7 @@ class EncoderRunner:
             return Ho, Wo, rows
         # conv1 in the x3 mode: both operands split in-kernel (CAPMI_GEMM_SPLIT3; its K = 7*7*4 is
         # not the gemm_x3 kernel's multiple of 32)
-        flags = CAPMI_GEMM_BF16 if self.bf16 else (CAPMI_GEMM_SPLIT3 if self.x3 and nchw else 0)
+        flags = CAPMI_GEMM_BF16 if self.bf16 else (CAPMI_GEMM_SPLIT3 if split3 else 0)
         launch = lambda: K.gemm_sk(prob, mode, self._ws["sk"], K.TILE_AUTO, flags=flags)  # noqa: E731
         if self.conv_hook is not None:
             key = K.gemm_sk_kernel_name(prob, mode, flags=flags)

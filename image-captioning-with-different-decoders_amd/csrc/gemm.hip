@@ -696,7 +696,7 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
   CAPMI_REQUIRE(terms >= 0 && terms_mode_ok(terms, amode, bmode), CAPMI_EINVAL);
   int rc = sk_decide(prob, amode, bmode, tile, terms, g, sk);
   if (rc) return rc;
-  if (terms > 0 && !(g.nt_ok && g.nt == 256 && (prob->in_scale == nullptr || (terms == 1 && amode == CAPMI_A_CONV_NHWC)))) {
+  if (terms > 0 && !(g.nt_ok && g.nt == 256 && (prob->in_scale == nullptr || amode == CAPMI_A_CONV_NHWC))) {
     rc = sk_decide(prob, amode, bmode, tile, 0, g, sk);
     if (rc) return rc;
   }
@@ -913,9 +913,8 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   CAPMI_REQUIRE(terms_mode_ok(terms, amode, bmode), CAPMI_EINVAL);
   int rc = sk_decide(prob, amode, bmode, tile, terms, g, sk);
   if (rc) return rc;
-  if (terms > 0 && !(g.nt_ok && g.nt == 256 && (prob->in_scale == nullptr || (terms == 1 && amode == CAPMI_A_CONV_NHWC)))) {
-    // shapes the split forms do not cover (unaligned / generic-kernel problems, the three-term
-    // split with a BN prologue): the fp32 kernel
+  if (terms > 0 && !(g.nt_ok && g.nt == 256 && (prob->in_scale == nullptr || amode == CAPMI_A_CONV_NHWC))) {
+    // shapes the split forms do not cover (unaligned / generic-kernel problems): the fp32 kernel
     terms = 0;
     rc = sk_decide(prob, amode, bmode, tile, 0, g, sk);
     if (rc) return rc;

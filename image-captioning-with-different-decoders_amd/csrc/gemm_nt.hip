@@ -767,17 +767,19 @@ gemm_nt_kernel(const GemmArgs args) {
 // split-staged dense GEMMs (the decoder's, every layout it uses): TERMS 1 (bf16 operands) or 3
 // (fp32-accurate three-term split); TERMS 3 holds three LDS planes per operand, so 64x64 tiles run
 // two workgroups per CU and the larger ones one (gemm_nt_wg_per_cu)
-template <int BM, int BN, int AMODE, int BMODE, bool SK, int TERMS>
+template <int BM, int BN, int AMODE, int BMODE, bool SK, int TERMS, bool PRO = false>
 __global__ void __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(TERMS == 3 ? (BM == 64 && BN == 64 ? 2 : 1) : kWavesPerEu<BM, BN>)))
 gemm_nts_kernel(const GemmArgs args) {
-  gemm_nt_body<BM, BN, AMODE, BMODE, false, SK, TERMS, 256>(args);
+  gemm_nt_body<BM, BN, AMODE, BMODE, PRO, SK, TERMS, 256>(args);
 }
 
 template <int BM, int BN, bool SK, int TERMS>
-void launch_nts(const GemmArgs& a, int amode, int bmode, int blocks, hipStream_t s) {
+void launch_nts(const GemmArgs& a, int amode, int bmode, bool pro, int blocks, hipStream_t s) {
   const dim3 g(blocks), b(256);
-  if (TERMS == 3 && amode == 2)  // conv (no prologue: the data gradients' dY)
+  if (TERMS == 3 && amode == 2 && pro)  // conv with the BN-apply + ReLU prologue
+    hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, TERMS == 3 ? 2 : 0, 0, SK, TERMS, TERMS == 3>), g, b, 0, s, a);
+  else if (TERMS == 3 && amode == 2)  // conv (no prologue: the data gradients' dY)
     hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, TERMS == 3 ? 2 : 0, 0, SK, TERMS>), g, b, 0, s, a);
   else if (TERMS == 3 && amode == 4)  // conv1 on the NHWC4 images
     hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, TERMS == 3 ? 4 : 0, 0, SK, TERMS>), g, b, 0, s, a);
@@ -852,18 +854,19 @@ int launch_bmbn(const GemmArgs& a, int amode, int bmode, bool pro, int terms, in
   const bool bf16 = terms == 1 && bmode == 0 && amode != 1;  // the forward / conv bf16 forms
   if (terms > 0 && !bf16) {
     const bool conv3 = terms == 3 && bmode == 0 && (amode == 2 || amode == 4);
-    if (!((amode == 0 && bmode <= 1) || (amode == 1 && bmode == 1) || conv3) || pro) return CAPMI_EINVAL;
+    if (!((amode == 0 && bmode <= 1) || (amode == 1 && bmode == 1) || conv3)) return CAPMI_EINVAL;
+    if (pro && !(conv3 && amode == 2)) return CAPMI_EINVAL;
     const bool sk = a.sk_workers > 0;
     if (terms == 3) {
       if (sk)
-        launch_nts<BM, BN, true, 3>(a, amode, bmode, blocks, s);
+        launch_nts<BM, BN, true, 3>(a, amode, bmode, pro, blocks, s);
       else
-        launch_nts<BM, BN, false, 3>(a, amode, bmode, blocks, s);
+        launch_nts<BM, BN, false, 3>(a, amode, bmode, pro, blocks, s);
     } else {
       if (sk)
-        launch_nts<BM, BN, true, 1>(a, amode, bmode, blocks, s);
+        launch_nts<BM, BN, true, 1>(a, amode, bmode, pro, blocks, s);
       else
-        launch_nts<BM, BN, false, 1>(a, amode, bmode, blocks, s);
+        launch_nts<BM, BN, false, 1>(a, amode, bmode, pro, blocks, s);
     }
   } else if (bf16) {
     if (a.sk_workers > 0)
@@ -891,7 +894,7 @@ int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int 
   if (bmode == 2 && amode != 1) return CAPMI_EINVAL;
   if (terms != 0 && terms != 1 && terms != 3) return CAPMI_EINVAL;
   if (terms == 3 && !((amode == 0 && bmode <= 1) || (amode == 1 && bmode == 1) ||
-                      (bmode == 0 && (amode == 2 || amode == 4) && !pro)))
+                      (bmode == 0 && (amode == 2 || (amode == 4 && !pro)))))
     return CAPMI_EINVAL;
   if (terms == 1 && !((bmode == 0 && amode != 1 && amode != 3) || (amode <= 1 && bmode == 1))) return CAPMI_EINVAL;
   if (nt == 512) {
