@@ -503,6 +503,7 @@ class _Pool:
 
 
 _FT_DGRAD_X3 = os.environ.get("CAPMI_FT_DGRAD_X3", "1") != "0"
+_FT_WGRAD_X3 = os.environ.get("CAPMI_FT_WGRAD_X3", "1") != "0"
 
 
 class FineTuneRunner:
@@ -621,9 +622,12 @@ class FineTuneRunner:
         no prologue) run the fp32-accurate three-term split when the encoder is in the x3 mode
         (CAPMI_GEMM_SPLIT3); weight gradients (k-row operands) stay on the fp32 MFMA kernel, where
         the split's transposing store is slower (tools/dec_gemm_ab.py). CAPMI_FT_DGRAD_X3=0: all fp32."""
-        if (self.r.x3 and _FT_DGRAD_X3 and bmode == CAPMI_B_NMAJOR_W and amode in (CAPMI_A_KMAJOR, CAPMI_A_CONV_NHWC)
-                and not prob.in_scale):
+        if not (self.r.x3 and _FT_DGRAD_X3) or prob.in_scale:
+            return 0
+        if bmode == CAPMI_B_NMAJOR_W and amode in (CAPMI_A_KMAJOR, CAPMI_A_CONV_NHWC):
             return CAPMI_GEMM_SPLIT3
+        if bmode == CAPMI_B_KROWS and amode == CAPMI_A_MMAJOR and _FT_WGRAD_X3:
+            return CAPMI_GEMM_SPLIT3  # 1x1 weight gradients on materialised inputs (dY^T X)
         return 0
 
     def _gemm(self, prob, amode, bmode, tile=K.TILE_AUTO):

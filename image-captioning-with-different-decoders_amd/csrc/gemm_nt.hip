@@ -187,9 +187,11 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
     for (int i = 0; i < NA; ++i) {
       const int f = tid + i * NT;
       if (AMODE == 1) {
-        if (BF) {  // slots 2j, 2j+1: k rows 2kp, 2kp+1 of column group jq (transposed at the store)
+        if (BF) {  // slots 2j, 2j+1: k rows 2kp, 2kp+1 of column group jq (transposed at the store).
+          // Lanes walk the 16 k pairs first: a wave's 32-bit LDS stores (row 4 jq + e, word kp) then
+          // hit 64 distinct banks; its loads read 16 k rows x 64 contiguous bytes
           const int u = tid + (i >> 1) * NT;
-          const int jq = u % AQ, kp = u / AQ;
+          const int jq = u / (BK2 / 2), kp = u % (BK2 / 2);
           a_ok[i] = m0 + jq * 4 < M;
           a_base[i] = m0 + jq * 4;
           a_ih0[i] = 2 * kp + (i & 1);
@@ -250,7 +252,7 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
       }
       if (BMODE == 1 && BF) {
         const int u = tid + (i >> 1) * NT;
-        const int jq = u % BQ, kp = u / BQ;
+        const int jq = u / (BK2 / 2), kp = u % (BK2 / 2);
         b_ok[i] = n0 + jq * 4 < N;
         b_base[i] = n0 + jq * 4;
         b_k[i] = 2 * kp + (i & 1);
