@@ -291,6 +291,21 @@ def bn_finalize(stats, tiles, C, count, gamma, beta, running_mean, running_var, 
          ptr(work), stream())
 
 
+def bn_finalize_apply(op, stats, tiles, C, count, gamma, beta, running_mean, running_var, momentum, eps,
+                      scale, shift, y, out, rows, res=None):
+    """capmi_bn_finalize_apply: the train-mode BN finalize fused into its consumer pass (op =
+    CAPMI_BNFA_SPLIT3 / ADD_RELU / RELU_BF16 / ADD_RELU_BF16)."""
+    _cuda(stats, gamma, beta, running_mean, running_var, scale, shift)
+    bf = op in (2, 3)
+    _cuda(y, res, dtype=torch.bfloat16 if bf else F32)
+    _cuda(out, dtype=torch.bfloat16 if op != 1 else F32)
+    if op == 0 and out.numel() < 3 * rows * C:
+        raise ValueError("bn_finalize_apply: the split planes need 3 * rows * C elements")
+    call("capmi_bn_finalize_apply", int(op), ptr(stats), int(tiles), int(C), int(count), ptr(gamma), ptr(beta),
+         ptr(running_mean), ptr(running_var), float(momentum), float(eps), ptr(scale), ptr(shift), ptr(y), ptr(res),
+         ptr(out), int(rows), stream())
+
+
 def bn_eval_params(gamma, beta, rm, rv, C, eps, scale, shift):
     _cuda(gamma, beta, rm, rv, scale, shift)
     call("capmi_bn_eval_params", ptr(gamma), ptr(beta), ptr(rm), ptr(rv), C, eps, ptr(scale), ptr(shift),

@@ -21,6 +21,8 @@ import torch.nn as nn
 from . import kernels as K
 from ._lib import CAPMI_A_CONV_NHWC, CAPMI_A_CONV_NHWC4, CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_B_CONV_NHWC
 from ._lib import CAPMI_B_KROWS, CAPMI_B_NMAJOR_W, CAPMI_GEMM_BF16, CAPMI_GEMM_SPLIT3
+from ._lib import CAPMI_BNFA_ADD_RELU, CAPMI_BNFA_ADD_RELU_BF16, CAPMI_BNFA_MAX_TILES, CAPMI_BNFA_RELU_BF16
+from ._lib import CAPMI_BNFA_SPLIT3
 
 AK, AMM, AC = CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_A_CONV_NHWC
 BW, BKR, BCONV = CAPMI_B_NMAJOR_W, CAPMI_B_KROWS, CAPMI_B_CONV_NHWC
@@ -143,6 +145,32 @@ def pool_dup(H, W, out_hw):
 
 # x3 mode: convs with K <= this run both operands split in-kernel (CAPMI_GEMM_SPLIT3) instead of gemm_x3
 _X3_SMALLK = int(os.environ.get("CAPMI_X3_SMALLK", "0"))
+# train-mode BN finalize fused into the consumer pass where it fits (capmi_bn_finalize_apply), opt-in
+# with CAPMI_BN_FUSE=1: measured slower than the separate finalize launch (headline 5558 -> 5458,
+# bf16 config 10559 -> 9732 img/s)
+_BN_FUSE = os.environ.get("CAPMI_BN_FUSE", "0") == "1"
+
+
+class _DeferredBN:
+    """A train-mode BatchNorm whose finalize is left to the pass that consumes the conv output
+    (capmi_bn_finalize_apply); ``now()`` runs the plain finalize instead and returns (scale, shift)."""
+
+    def __init__(self, runner, ws, bn, rows):
+        self.r, self.ws, self.bn, self.rows = runner, ws, bn, rows
+
+    def args(self):
+        bn, ws = self.bn, self.ws
+        s, b = self.r._ss(ws, bn)
+        mom = 0.1 if bn.momentum is None else bn.momentum
+        track = bn.track_running_stats
+        return (ws["stats"], K.stat_tiles(self.rows), bn.num_features, self.rows, bn.weight, bn.bias,
+                bn.running_mean if track else None, bn.running_var if track else None, mom, bn.eps, s, b)
+
+    def apply(self, op, y, out, res=None):
+        K.bn_finalize_apply(op, *self.args(), y, out, self.rows, res=res)
+
+    def now(self):
+        return self.r._bn(self.ws, self.bn, self.rows, True)
 
 
 class EncoderRunner:
@@ -207,6 +235,14 @@ class EncoderRunner:
             K.bn_eval_params(bn.weight, bn.bias, bn.running_mean, bn.running_var, C, bn.eps, s, b)
         return s, b
 
+    def _bn_defer(self, ws, bn, rows, train):
+        """As _bn, but a train-mode BN small enough for capmi_bn_finalize_apply (layer3/4) comes back
+        as a _DeferredBN for its consumer to finalize."""
+        if (train and _BN_FUSE and K.stat_tiles(rows) <= CAPMI_BNFA_MAX_TILES and bn.num_features % 32 == 0
+                and bn.weight is not None):
+            return _DeferredBN(self, ws, bn, rows)
+        return self._bn(ws, bn, rows, train)
+
     def _conv(self, tag, x, conv, out, N, H, W, train, in_ss=None, nchw=False):
         co, ci, kh, kw = conv.weight.shape
         st, pd = conv.stride[0], conv.padding[0]
@@ -218,6 +254,11 @@ class EncoderRunner:
         stats = ws_stats = self._ws["stats"] if train else None
         kw_ = dict(stats=ws_stats)
         split3 = nchw and self.x3  # conv1 (K = 7*7*4) in the x3 mode
+        smallk = not nchw and self.x3 and Kd <= _X3_SMALLK
+        x3p = (not nchw and not smallk and self.x3 and in_ss is not None and co >= 128 and ci % 32 == 0
+               and Kd >= 128 and rows >= 12544)
+        if isinstance(in_ss, _DeferredBN) and not x3p:
+            in_ss = in_ss.now()  # only the x3p split pass takes the finalize fused
         if nchw:
             # conv1: the NCHW images are re-laid out once as NHWC with 4 channels (one float4 per
             # pixel); the implicit GEMM then runs over k = (kh, kw, c4), the 4th channel zero
@@ -227,7 +268,7 @@ class EncoderRunner:
             geo["Cin"] = 4
             prob = K.problem(rows, co, K4, img4, 0, w, K4, out, co, conv=geo, **kw_)
             mode = CAPMI_A_CONV_NHWC4
-        elif self.x3 and Kd <= _X3_SMALLK:
+        elif smallk:
             # short-k convs (layer1's K = 64): both operands split in-kernel on the 256-thread kernel
             # (CAPMI_GEMM_SPLIT3, two workgroups per CU overlap one's epilogue with the other's loads)
             sc, sh = in_ss if in_ss is not None else (None, None)
@@ -237,14 +278,17 @@ class EncoderRunner:
                 prob = K.problem(rows, co, Kd, x, 0, w, Kd, out, co, conv=geo, in_scale=sc, in_shift=sh, **kw_)
                 mode = CAPMI_A_CONV_NHWC
             split3 = True
-        elif self.x3 and in_ss is not None and co >= 128 and ci % 32 == 0 and Kd >= 128 and rows >= 12544:
+        elif x3p:
             # x3p: the conv input relu(bn(y)) split once into three bf16 planes, then the GEMM with
             # both operands pre-split (gemm_x3p.hip). Where it pays (tools/x3_ab.py, batch 64): the
             # 3x3 convs of layer2/3 and the c3 convs of layer2/3 (their A tiles are re-staged 9x /
             # 4-8x); layer1's K = 64 c3 (no gain once the split pass is counted) and layer4's
             # 3136-row grids keep the in-kernel split (gemm_x3.hip)
             xp = self._x3p_buffer(self._ws)
-            K.bn_relu_split3(x, in_ss[0], in_ss[1], N * H * W, ci, xp)
+            if isinstance(in_ss, _DeferredBN):
+                in_ss.apply(CAPMI_BNFA_SPLIT3, x, xp)  # finalize of the input's BN + split, one pass
+            else:
+                K.bn_relu_split3(x, in_ss[0], in_ss[1], N * H * W, ci, xp)
             w3 = self._packed_x3(conv, tap_inner=True)
             if kh == 1 and st == 1:
                 prob, mode = K.problem(rows, co, Kd, xp, ci, w3, Kd, out, co, **kw_), CAPMI_A_KMAJOR
@@ -348,6 +392,15 @@ class EncoderRunner:
             launch()
         return Ho, Wo, rows
 
+    def _bn_relu_bf16(self, ws, bn, rows, train, y):
+        """relu(bn(y)) in place on a bf16 conv output (the next conv's input), the BN finalize fused in
+        where it fits."""
+        d = self._bn_defer(ws, bn, rows, train)
+        if isinstance(d, _DeferredBN):
+            d.apply(CAPMI_BNFA_RELU_BF16, y, y)
+        else:
+            K.bn_relu_bf16(y, d[0], d[1], rows, bn.num_features, y)
+
     def _forward_bf16(self, net, imgs, out_hw, train, out):
         """The conv stack on bf16 NHWC activations: every conv but conv1 on CAPMI_GEMM_BF16_IO (bf16
         operands, fp32 accumulation, bf16 output, fp32 BN statistics of the stored values), the BN
@@ -373,21 +426,23 @@ class EncoderRunner:
             for bi, blk in enumerate(getattr(net, f"layer{li}")):
                 tag = f"layer{li}.{bi}"
                 _, _, r1 = self._conv_bf16(tag + ".conv1", x, blk.conv1, bf["y1"], N, H, W, train)
-                s1, b1 = self._bn(ws, blk.bn1, r1, train)
-                K.bn_relu_bf16(bf["y1"], s1, b1, r1, blk.conv1.out_channels, bf["y1"])
+                self._bn_relu_bf16(ws, blk.bn1, r1, train, bf["y1"])
                 H2, W2, r2 = self._conv_bf16(tag + ".conv2", bf["y1"], blk.conv2, bf["y2"], N, H, W, train)
-                s2, b2 = self._bn(ws, blk.bn2, r2, train)
-                K.bn_relu_bf16(bf["y2"], s2, b2, r2, blk.conv2.out_channels, bf["y2"])
+                self._bn_relu_bf16(ws, blk.bn2, r2, train, bf["y2"])
                 _, _, r3 = self._conv_bf16(tag + ".conv3", bf["y2"], blk.conv3, bf["y3"], N, H2, W2, train)
-                s3, b3 = self._bn(ws, blk.bn3, r3, train)
                 Cout = blk.conv3.out_channels
                 if blk.downsample is not None:
+                    s3, b3 = self._bn(ws, blk.bn3, r3, train)  # (the downsample conv reuses the stats buffer)
                     self._conv_bf16(tag + ".downsample", x, blk.downsample[0], bf["yd"], N, H, W, train)
                     sd, bd = self._bn(ws, blk.downsample[1], r3, train)
                     K.bn_add_relu_bf16(bf["y3"], s3, b3, bf["yd"], xo, r3, Cout, res_scale=sd, res_shift=bd)
                     bns.append(blk.downsample[1])
                 else:
-                    K.bn_add_relu_bf16(bf["y3"], s3, b3, x, xo, r3, Cout)
+                    d3 = self._bn_defer(ws, blk.bn3, r3, train)
+                    if isinstance(d3, _DeferredBN):
+                        d3.apply(CAPMI_BNFA_ADD_RELU_BF16, bf["y3"], xo, res=x)
+                    else:
+                        K.bn_add_relu_bf16(bf["y3"], d3[0], d3[1], x, xo, r3, Cout)
                 bns += [blk.bn1, blk.bn2, blk.bn3]
                 x, xo = xo, x
                 H, W, Cx = H2, W2, Cout
@@ -431,19 +486,24 @@ class EncoderRunner:
                     xo = out  # the last block's output is the result
                 tag = f"layer{li}.{bi}"
                 _, _, r1 = self._conv(tag + ".conv1", x, blk.conv1, ws["y1"], N, H, W, train)
-                ss1 = self._bn(ws, blk.bn1, r1, train)
+                # (layer3/4: the finalize of bn1 / bn2 rides in the consumer's pass, _bn_defer)
+                ss1 = self._bn_defer(ws, blk.bn1, r1, train)
                 H2, W2, r2 = self._conv(tag + ".conv2", ws["y1"], blk.conv2, ws["y2"], N, H, W, train, in_ss=ss1)
-                ss2 = self._bn(ws, blk.bn2, r2, train)
+                ss2 = self._bn_defer(ws, blk.bn2, r2, train)
                 _, _, r3 = self._conv(tag + ".conv3", ws["y2"], blk.conv3, ws["y3"], N, H2, W2, train, in_ss=ss2)
-                s3, b3 = self._bn(ws, blk.bn3, r3, train)
                 Cout = blk.conv3.out_channels
                 if blk.downsample is not None:
+                    s3, b3 = self._bn(ws, blk.bn3, r3, train)  # (the downsample conv reuses the stats buffer)
                     self._conv(tag + ".downsample", x, blk.downsample[0], ws["yd"], N, H, W, train)
                     sd, bd = self._bn(ws, blk.downsample[1], r3, train)
                     K.bn_add_relu(ws["y3"], s3, b3, ws["yd"], xo, r3, Cout, res_scale=sd, res_shift=bd)
                     bns.append(blk.downsample[1])
                 else:
-                    K.bn_add_relu(ws["y3"], s3, b3, x, xo, r3, Cout)
+                    d3 = self._bn_defer(ws, blk.bn3, r3, train)
+                    if isinstance(d3, _DeferredBN):
+                        d3.apply(CAPMI_BNFA_ADD_RELU, ws["y3"], xo, res=x)
+                    else:
+                        K.bn_add_relu(ws["y3"], d3[0], d3[1], x, xo, r3, Cout)
                 bns += [blk.bn1, blk.bn2, blk.bn3]
                 x, xo = xo, x
                 H, W, Cx = H2, W2, Cout

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 13
+#define CAPMI_ABI_VERSION 14
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -474,6 +474,27 @@ int capmi_embed_scatter_add(const float* dx, long long ld_dx, const long long* c
  * term the RNE bf16 rounding of the remainder (B operand of CAPMI_GEMM_X3). */
 int capmi_split3_bf16(const float* in, long long n, void* out, void* stream);
 
+/* Train-mode BatchNorm finalize fused into the pass that consumes it (replaces capmi_bn_finalize +
+ * the apply pass for layer3/4-sized tensors: tiles <= CAPMI_BNFA_MAX_TILES slices). Every workgroup
+ * finalizes its 32 channels from `stats` (fp64, fixed order; bn_finalize's formulas), then applies
+ * them to its rows; scale / shift are written and the running statistics updated once (gamma,
+ * beta, running_*: models/encoder.py:88-91 nn.BatchNorm2d, train mode). rows = count = the conv's
+ * output rows; C % 32 == 0.
+ *   CAPMI_BNFA_SPLIT3        y fp32 [rows][C] -> out = relu(bn(y)) split into three bf16 planes
+ *                            [3][rows*C] (the capmi_bn_relu_split3 output; x3p conv input)
+ *   CAPMI_BNFA_ADD_RELU      y, res fp32 -> out fp32 = relu(bn(y) + res)   (bottleneck tail)
+ *   CAPMI_BNFA_RELU_BF16     y bf16 -> out bf16 = relu(bn(y)) (out may alias y)
+ *   CAPMI_BNFA_ADD_RELU_BF16 y, res bf16 -> out bf16 = relu(bn(y) + res)
+ * res must be NULL for the ops without a residual. */
+#define CAPMI_BNFA_SPLIT3 0
+#define CAPMI_BNFA_ADD_RELU 1
+#define CAPMI_BNFA_RELU_BF16 2
+#define CAPMI_BNFA_ADD_RELU_BF16 3
+#define CAPMI_BNFA_MAX_TILES 256
+int capmi_bn_finalize_apply(int op, const float* stats, int tiles, int C, long long count, const float* gamma,
+                            const float* beta, float* running_mean, float* running_var, float momentum, float eps,
+                            float* scale, float* shift, const void* y, const void* res, void* out, long long rows,
+                            void* stream);
 /* x = relu(y * scale[c] + shift[c]) of y [rows][C] fp32 (scale = shift = NULL: x = y), written as
  * the three bf16 split planes out[3][rows * C] (the CAPMI_GEMM_X3P A operand); C % 4 == 0. */
 int capmi_bn_relu_split3(const float* y, const float* scale, const float* shift, long long rows, int C, void* out,
