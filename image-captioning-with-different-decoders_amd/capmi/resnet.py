@@ -678,16 +678,17 @@ class FineTuneRunner:
 
     # ------------------------------------------------------------------ backward
     def _flags(self, prob, amode, bmode):
-        """Data gradients (convs of dY / 1x1 GEMMs on the transposed weight: A row-major, B = W[N][K],
-        no prologue) run the fp32-accurate three-term split when the encoder is in the x3 mode
-        (CAPMI_GEMM_SPLIT3); weight gradients (k-row operands) stay on the fp32 MFMA kernel, where
-        the split's transposing store is slower (tools/dec_gemm_ab.py). CAPMI_FT_DGRAD_X3=0: all fp32."""
-        if not (self.r.x3 and _FT_DGRAD_X3) or prob.in_scale:
+        """In the x3 mode the backward GEMMs run the fp32-accurate three-term split (CAPMI_GEMM_SPLIT3):
+        the data gradients (convs of dY / 1x1 GEMMs on the transposed weight) and the weight gradients
+        (CAPMI_FT_WGRAD_X3=0: those fp32). CAPMI_FT_DGRAD_X3=0: all fp32."""
+        if not (self.r.x3 and _FT_DGRAD_X3):
             return 0
-        if bmode == CAPMI_B_NMAJOR_W and amode in (CAPMI_A_KMAJOR, CAPMI_A_CONV_NHWC):
+        if bmode == CAPMI_B_NMAJOR_W and amode in (CAPMI_A_KMAJOR, CAPMI_A_CONV_NHWC) and not prob.in_scale:
             return CAPMI_GEMM_SPLIT3
-        if bmode == CAPMI_B_KROWS and amode == CAPMI_A_MMAJOR and _FT_WGRAD_X3:
-            return CAPMI_GEMM_SPLIT3  # 1x1 weight gradients on materialised inputs (dY^T X)
+        if amode == CAPMI_A_MMAJOR and bmode in (CAPMI_B_KROWS, CAPMI_B_CONV_NHWC) and _FT_WGRAD_X3:
+            # weight gradients dY^T X: on a materialised input (k rows) or the implicit im2col of the
+            # saved pre-BN output with the BN-apply + ReLU prologue
+            return CAPMI_GEMM_SPLIT3
         return 0
 
     def _gemm(self, prob, amode, bmode, tile=K.TILE_AUTO):

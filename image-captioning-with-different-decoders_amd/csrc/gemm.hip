@@ -608,15 +608,15 @@ int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, in
   // output tile, stream-K over 128x64 tiles is the fastest form; below that the per-segment
   // pipeline fill outweighs the balance gain and 64x64 data-parallel wins
   if (automatic) tile = nkt >= 16 ? CAPMI_TILE_128x64 : CAPMI_TILE_64;
-  // three-term split staging: 64x64 everywhere (two workgroups per CU; the larger tiles hold one:
-  // tools/dec_gemm_ab.py --tile, 5-20 % faster on every decoder GEMM at 64x64)
-  if (automatic && terms == 3) tile = CAPMI_TILE_64;
   // conv weight gradients (k = output pixels, always >= 16 k-tiles; tools/wgrad_tile_ab.py, with
   // the k-major LDS images): 128x128 for the wide 3x3 ones (Cout >= 256, N = 9*Cin >= 2048:
   // layer3/4, 1-7 % faster than 128x64), 128x64 for the rest (layer2 3x3 and the 1x1 ones: 128x128
   // is up to 2x slower there, 64x64 5-12 % slower)
   if (automatic && amode == CAPMI_A_MMAJOR && bmode == CAPMI_B_CONV_NHWC)
     tile = (prob->M >= 256 && prob->N >= 2048) ? CAPMI_TILE_128 : CAPMI_TILE_128x64;
+  // three-term split staging: 64x64 everywhere (two workgroups per CU; the larger tiles hold one:
+  // tools/dec_gemm_ab.py --tile, 5-20 % faster on every decoder GEMM at 64x64)
+  if (automatic && terms == 3) tile = CAPMI_TILE_64;
   int rc = gemm_plan(prob, 1, amode, bmode, tile, g);
   if (rc) return rc;
   // the 512-thread 128x128 form (tools/w8_ab.sh over all 19 encoder conv shapes, batch 64):
@@ -655,7 +655,8 @@ int flag_terms(int flags) {
 // the modes a split-staged (terms > 0) launch supports (gemm_nt.hip: gemm_nt_launch)
 bool terms_mode_ok(int terms, int amode, int bmode) {
   if (terms == 0) return true;
-  if (bmode == 0 && (amode == 2 || amode == 4)) return true;  // convs (terms 3: no BN prologue)
+  if (bmode == 0 && (amode == 2 || amode == 4)) return true;  // convs
+  if (bmode == 2) return terms == 3 && amode == 1;             // conv weight gradients (three-term split)
   if (terms == 1 && bmode == 0) return amode == 0;
   return (amode == 0 && bmode <= 1) || (amode == 1 && bmode == 1);
 }
@@ -699,7 +700,7 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
   CAPMI_REQUIRE(terms >= 0 && terms_mode_ok(terms, amode, bmode), CAPMI_EINVAL);
   int rc = sk_decide(prob, amode, bmode, tile, terms, g, sk);
   if (rc) return rc;
-  if (terms > 0 && !(g.nt_ok && g.nt == 256 && (prob->in_scale == nullptr || amode == CAPMI_A_CONV_NHWC))) {
+  if (terms > 0 && !(g.nt_ok && g.nt == 256 && (prob->in_scale == nullptr || amode == CAPMI_A_CONV_NHWC || bmode == CAPMI_B_CONV_NHWC))) {
     rc = sk_decide(prob, amode, bmode, tile, 0, g, sk);
     if (rc) return rc;
   }
@@ -916,7 +917,7 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   CAPMI_REQUIRE(terms_mode_ok(terms, amode, bmode), CAPMI_EINVAL);
   int rc = sk_decide(prob, amode, bmode, tile, terms, g, sk);
   if (rc) return rc;
-  if (terms > 0 && !(g.nt_ok && g.nt == 256 && (prob->in_scale == nullptr || amode == CAPMI_A_CONV_NHWC))) {
+  if (terms > 0 && !(g.nt_ok && g.nt == 256 && (prob->in_scale == nullptr || amode == CAPMI_A_CONV_NHWC || bmode == CAPMI_B_CONV_NHWC))) {
     // shapes the split forms do not cover (unaligned / generic-kernel problems): the fp32 kernel
     terms = 0;
     rc = sk_decide(prob, amode, bmode, tile, 0, g, sk);

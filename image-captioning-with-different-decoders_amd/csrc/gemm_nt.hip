@@ -126,13 +126,13 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
   constexpr bool BF = TERMS > 0;
   constexpr int TT = BF ? TERMS : 1;  // planes (array extents; the fp32 form never reads them)
   static_assert(TERMS == 0 || TERMS == 1 || TERMS == 3, "terms");
-  static_assert(!BF || BMODE <= 1, "bf16 staging: B = W[N][K] or k rows");
+  static_assert(!BF || BMODE <= 2, "split staging: B = W[N][K], k rows or the wgrad im2col");
   static_assert(NT == 256 || (NT == 512 && BMODE == 0 && AMODE != 1 && !BF), "512-thread form: forward modes");
   constexpr int WR = NT / 128;  // wave rows
   constexpr int WM = BM / WR, WN = BN / 2, TM = WM / 32, TN = WN / 32;
   constexpr int NA = BM * BK2 / 4 / NT, NB = BN * BK2 / 4 / NT;
   static_assert(NA >= 1 && NB >= 1, "tile");
-  static_assert(!BF || ((AMODE != 1 || NA % 2 == 0) && (BMODE != 1 || NB % 2 == 0)), "k-row pairs");
+  static_assert(!BF || ((AMODE != 1 || NA % 2 == 0) && (BMODE == 0 || NB % 2 == 0)), "k-row pairs");
   // floats per tile row and buffer: the fp32 [m][k] image (S2), or TERMS bf16 planes of SB
   constexpr int ROWF = TERMS == 3 ? 3 * SB / 2 : S2;
   static_assert(TERMS != 1 || SB / 2 <= S2, "bf16 plane");
@@ -224,7 +224,7 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
     int b_k[NB];
     bool b_ok[NB];
     // BMODE 2 (wgrad): the n column (kh, kw, ci..ci+3) of a slot is fixed for the whole k loop
-    int b_kh[NB], b_kw[NB];
+    int b_kh[NB], b_kw[NB], b_jq[NB];  // b_jq: column group of a k-row pair slot (split staging)
     float4 b_sc[NB], b_sh[NB];
     const int cWo = P.cWo, cHW = P.cHo * P.cWo, cStr = P.cStride, cPd = P.cPad;
     const float inv_hw = 1.f / (float)cHW, inv_wo = 1.f / (float)cWo;
@@ -234,8 +234,12 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
       b_kh[i] = b_kw[i] = 0;
       b_sc[i] = f4(1.f);
       b_sh[i] = f4(0.f);
+      b_jq[i] = 0;
       if (BMODE == 2) {
-        const int jq = (tid & 15) + 16 * (i % BQ16);
+        // split staging: slots 2j, 2j+1 = k rows 2kp, 2kp+1 of column group jq (lanes along the k pairs)
+        const int u = tid + (i >> 1) * NT;
+        const int jq = BF ? u / (BK2 / 2) : (tid & 15) + 16 * (i % BQ16);
+        b_jq[i] = jq;
         const int n = n0 + jq * 4;
         b_ok[i] = n < N;  // N % 4 == 0, Cin % 4 == 0: a float4 never straddles (kh, kw)
         const int nn = b_ok[i] ? n : 0;
@@ -243,7 +247,7 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
         b_kh[i] = kpos / cKW;
         b_kw[i] = kpos - b_kh[i] * cKW;
         b_base[i] = ci;
-        b_k[i] = (tid >> 4) + 16 * (i / BQ16);
+        b_k[i] = BF ? 2 * (u % (BK2 / 2)) + (i & 1) : (tid >> 4) + 16 * (i / BQ16);
         if (PRO) {
           b_sc[i] = *reinterpret_cast<const float4*>(isc + ci);
           b_sh[i] = *reinterpret_cast<const float4*>(ish + ci);
@@ -256,7 +260,7 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
         b_ok[i] = n0 + jq * 4 < N;
         b_base[i] = n0 + jq * 4;
         b_k[i] = 2 * kp + (i & 1);
-        b_kw[i] = jq;  // column group (the transposing store's row)
+        b_jq[i] = jq;  // column group (the transposing store's row)
       } else if (BMODE == 1) {
         const int jq = (tid & 15) + 16 * (i % BQ16);
         const int n = n0 + jq * 4;
@@ -386,12 +390,17 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
             store_row4<TT, PLA>(Ah + (f >> 3) * SB + kq, v);
           }
         }
-        if (BMODE == 1) {
+        if (BMODE >= 1) {
 #pragma unroll
           for (int j = 0; j < NB / 2; ++j) {
-            const float4 v0 = (st.bm >> (2 * j)) & 1u ? st.rb[2 * j] : f4(0.f);
-            const float4 v1 = (st.bm >> (2 * j + 1)) & 1u ? st.rb[2 * j + 1] : f4(0.f);
-            store_kpair<TT, PLB>(Bh + 4 * b_kw[2 * j] * SB + b_k[2 * j], v0, v1);
+            float4 v0 = st.rb[2 * j], v1 = st.rb[2 * j + 1];
+            if (PRO && BMODE == 2) {  // the wgrad's BN-apply + ReLU prologue, then the padding zeros
+              v0 = relu4(fma4(v0, b_sc[2 * j], b_sh[2 * j]));
+              v1 = relu4(fma4(v1, b_sc[2 * j + 1], b_sh[2 * j + 1]));
+            }
+            if (!((st.bm >> (2 * j)) & 1u)) v0 = f4(0.f);
+            if (!((st.bm >> (2 * j + 1)) & 1u)) v1 = f4(0.f);
+            store_kpair<TT, PLB>(Bh + 4 * b_jq[2 * j] * SB + b_k[2 * j], v0, v1);
           }
         } else {
 #pragma unroll
@@ -785,6 +794,10 @@ void launch_nts(const GemmArgs& a, int amode, int bmode, bool pro, int blocks, h
     hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, TERMS == 3 ? 2 : 0, 0, SK, TERMS>), g, b, 0, s, a);
   else if (TERMS == 3 && amode == 4)  // conv1 on the NHWC4 images
     hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, TERMS == 3 ? 4 : 0, 0, SK, TERMS>), g, b, 0, s, a);
+  else if (TERMS == 3 && bmode == 2 && pro)  // conv weight gradient, BN prologue on the im2col B
+    hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, 1, TERMS == 3 ? 2 : 1, SK, TERMS, TERMS == 3>), g, b, 0, s, a);
+  else if (TERMS == 3 && bmode == 2)
+    hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, 1, TERMS == 3 ? 2 : 1, SK, TERMS>), g, b, 0, s, a);
   else if (amode == 0 && bmode == 0)
     hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, 0, 0, SK, TERMS>), g, b, 0, s, a);
   else if (amode == 0 && bmode == 1)
@@ -856,8 +869,9 @@ int launch_bmbn(const GemmArgs& a, int amode, int bmode, bool pro, int terms, in
   const bool bf16 = terms == 1 && bmode == 0 && amode != 1;  // the forward / conv bf16 forms
   if (terms > 0 && !bf16) {
     const bool conv3 = terms == 3 && bmode == 0 && (amode == 2 || amode == 4);
-    if (!((amode == 0 && bmode <= 1) || (amode == 1 && bmode == 1) || conv3)) return CAPMI_EINVAL;
-    if (pro && !(conv3 && amode == 2)) return CAPMI_EINVAL;
+    const bool wgrad3 = terms == 3 && amode == 1 && bmode == 2;
+    if (!((amode == 0 && bmode <= 1) || (amode == 1 && bmode == 1) || conv3 || wgrad3)) return CAPMI_EINVAL;
+    if (pro && !((conv3 && amode == 2) || wgrad3)) return CAPMI_EINVAL;
     const bool sk = a.sk_workers > 0;
     if (terms == 3) {
       if (sk)
@@ -895,7 +909,7 @@ int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int 
   if (pro && !((amode == 2 && bmode == 0) || (amode == 1 && bmode == 2))) return CAPMI_EINVAL;
   if (bmode == 2 && amode != 1) return CAPMI_EINVAL;
   if (terms != 0 && terms != 1 && terms != 3) return CAPMI_EINVAL;
-  if (terms == 3 && !((amode == 0 && bmode <= 1) || (amode == 1 && bmode == 1) ||
+  if (terms == 3 && !((amode == 0 && bmode <= 1) || (amode == 1 && bmode >= 1) ||
                       (bmode == 0 && (amode == 2 || (amode == 4 && !pro)))))
     return CAPMI_EINVAL;
   if (terms == 1 && !((bmode == 0 && amode != 1 && amode != 3) || (amode <= 1 && bmode == 1))) return CAPMI_EINVAL;
