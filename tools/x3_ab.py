@@ -11,6 +11,7 @@ sys.path.insert(0, os.path.join(REPO, "tools"))
 import torch  # noqa: E402
 
 from capmi import kernels as K  # noqa: E402
+from capmi._lib import CAPMI_GEMM_SPLIT3  # noqa: E402
 
 
 def conv_shapes(B=64):
@@ -63,7 +64,9 @@ def main():
         pn = K.problem(rows, Cout, Kd, x, Cin if dense else 0, w, Kd, out, Cout, **kw)
         p3 = K.problem(rows, Cout, Kd, x, Cin if dense else 0, w3, Kd, out, Cout, **kw)
         res = {}
-        arms = [("native", lambda: K.gemm_sk(pn, mode, ws)), ("x3", lambda: K.gemm_x3(p3, mode, ws))]
+        arms = [("native", lambda: K.gemm_sk(pn, mode, ws)), ("x3", lambda: K.gemm_x3(p3, mode, ws)),
+                ("nts", lambda: K.gemm_sk(pn, mode, ws, flags=CAPMI_GEMM_SPLIT3)),
+                ("nts128", lambda: K.gemm_sk(pn, mode, ws, K.TILE_128x64, flags=CAPMI_GEMM_SPLIT3))]
         if pro and Cout >= 128 and Cin % 32 == 0:  # x3p candidates: split pass + pre-split GEMM
             xp = torch.empty(3 * x.numel(), device=dev, dtype=torch.bfloat16)
             w3p = torch.empty_like(w3)
@@ -94,7 +97,8 @@ def main():
                if "x3p" in res else "")
         print(f"| {tag} | {cnt} | {rows} | {Cout} | {Kd} | {res['native']:.1f} | {f / res['native'] / 1e6:.1f} | "
               f"{res['x3']:.1f} | {f / res['x3'] / 1e6:.1f} | {res['native'] / best:.2f} | "
-              f"{K.gemm_x3_kernel_name(p3, mode)}{x3p} |")
+              f"{K.gemm_x3_kernel_name(p3, mode)}{x3p} | split-staged 64x64 {res['nts']:.1f} us, 128x64 "
+              f"{res['nts128']:.1f} us |")
     print(f"\nlayer1-4 convs per forward: native {tot['native'] / 1e3:.3f} ms, best x3 form {tot['x3'] / 1e3:.3f} ms")
 
 
