@@ -253,7 +253,9 @@ class EncoderRunner:
         geo = dict(N=N, H=H, W=W, Cin=ci, KH=kh, KW=kw, stride=st, pad=pd, Ho=Ho, Wo=Wo)
         stats = ws_stats = self._ws["stats"] if train else None
         kw_ = dict(stats=ws_stats)
-        split3 = nchw and self.x3  # conv1 (K = 7*7*4) in the x3 mode
+        # conv1 stays on the fp32 MFMA kernel in the x3 mode: SPLIT3 measured 264 vs 261 us there (the
+        # 7x7/2 im2col gather over the NHWC4 images bounds it, not the MFMA)
+        split3 = False
         smallk = not nchw and self.x3 and Kd <= _X3_SMALLK
         x3p = (not nchw and not smallk and self.x3 and in_ss is not None and co >= 128 and ci % 32 == 0
                and Kd >= 128 and rows >= 12544)
