@@ -31,6 +31,7 @@ CAPMI_GEMM_BF16_IO = 2
 CAPMI_GEMM_X3 = 4
 CAPMI_GEMM_X3P = 8
 CAPMI_GEMM_SPLIT3 = 16
+CAPMI_GEMM_X3D = 32
 CAPMI_BNFA_SPLIT3, CAPMI_BNFA_ADD_RELU, CAPMI_BNFA_RELU_BF16, CAPMI_BNFA_ADD_RELU_BF16 = 0, 1, 2, 3
 CAPMI_BNFA_MAX_TILES = 256
 

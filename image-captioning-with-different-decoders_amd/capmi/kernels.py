@@ -10,7 +10,7 @@ import torch
 
 from ._lib import DstepEpi, DstepSeg
 from ._lib import (CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_GEMM_BF16_IO, CAPMI_GEMM_X3, CAPMI_GEMM_X3P,
-                   CAPMI_GEMM_SPLIT3,
+                   CAPMI_GEMM_SPLIT3, CAPMI_GEMM_X3D,
                    CAPMI_COLSUM_GROUPS, CAPMI_TILE_128, CAPMI_TILE_64,
                    CAPMI_TILE_128x64, CAPMI_TILE_AUTO, GemmProblem, call, lib)
 
@@ -183,6 +183,22 @@ def gemm_x3p(prob, amode, workspace):
     _cuda(workspace, dtype=torch.int32)
     call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3P,
          ptr(workspace), workspace.numel() * 4, stream())
+
+
+def gemm_x3d(prob, amode, workspace):
+    """CAPMI_GEMM_X3D: A fp32 (dense, or the NHWC conv input with the optional BN prologue) split
+    in-kernel x B = three bf16 planes in the x3p k order (conv_weight_order_x3p + split3_bf16)."""
+    _cuda(workspace, dtype=torch.int32)
+    call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3D,
+         ptr(workspace), workspace.numel() * 4, stream())
+
+
+def gemm_x3d_kernel_name(prob, amode):
+    v = [ctypes.c_int(0) for _ in range(5)]
+    call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3D,
+         *[ctypes.byref(x) for x in v])
+    b = lambda x: "true" if x else "false"  # noqa: E731
+    return f"gemm_x3p_kernel<{amode}, {b(v[2].value)}, 32, true, {b(bool(prob.in_scale))}>"
 
 
 def gemm_x3p_kernel_name(prob, amode):

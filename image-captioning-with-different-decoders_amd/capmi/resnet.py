@@ -145,6 +145,9 @@ def pool_dup(H, W, out_hw):
 
 # x3 mode: convs with K <= this run both operands split in-kernel (CAPMI_GEMM_SPLIT3) instead of gemm_x3
 _X3_SMALLK = int(os.environ.get("CAPMI_X3_SMALLK", "0"))
+# x3 mode: route the shapes where it measured fastest to the x3d kernel (CAPMI_X3D=1; off by default
+# until the encoder-level fault seen with it at batch 2 is found)
+_X3D = os.environ.get("CAPMI_X3D", "0") == "1"
 # train-mode BN finalize fused into the consumer pass where it fits (capmi_bn_finalize_apply), opt-in
 # with CAPMI_BN_FUSE=1: measured slower than the separate finalize launch (headline 5558 -> 5458,
 # bf16 config 10559 -> 9732 img/s)
@@ -257,8 +260,17 @@ class EncoderRunner:
         # 7x7/2 im2col gather over the NHWC4 images bounds it, not the MFMA)
         split3 = False
         smallk = not nchw and self.x3 and Kd <= _X3_SMALLK
-        x3p = (not nchw and not smallk and self.x3 and in_ss is not None and co >= 128 and ci % 32 == 0
-               and Kd >= 128 and rows >= 12544)
+        # x3d (A fp32 split in-kernel, B planes by LDS-DMA, 256x128 tiles; tools/x3_ab.py at batch 64,
+        # profiles/r02_x3_ab_x3d.md): the stride-2 convs, the first c1 of a stage (Cin = 2 Cout), the
+        # layer4-sized grids except the plain c1, and the c3 of layer3 -- 4-39 us faster per launch than
+        # gemm_x3 / the split pass + x3p there; elsewhere gemm_x3 or x3p stay ahead
+        x3d = (_X3D and not nchw and not smallk and self.x3 and ci % 32 == 0 and Kd % 32 == 0 and (
+            st == 2
+            or (kh == 1 and in_ss is None and ci == 2 * co)
+            or (rows <= 3136 and not (kh == 1 and in_ss is None))
+            or (kh == 1 and in_ss is not None and co == 4 * ci and rows <= 12544)))
+        x3p = (not nchw and not smallk and not x3d and self.x3 and in_ss is not None and co >= 128
+               and ci % 32 == 0 and Kd >= 128 and rows >= 12544)
         if isinstance(in_ss, _DeferredBN) and not x3p:
             in_ss = in_ss.now()  # only the x3p split pass takes the finalize fused
         if nchw:
@@ -280,6 +292,20 @@ class EncoderRunner:
                 prob = K.problem(rows, co, Kd, x, 0, w, Kd, out, co, conv=geo, in_scale=sc, in_shift=sh, **kw_)
                 mode = CAPMI_A_CONV_NHWC
             split3 = True
+        elif x3d:
+            w3 = self._packed_x3(conv, tap_inner=True)
+            if kh == 1 and st == 1 and in_ss is None:
+                prob, mode = K.problem(rows, co, Kd, x, ci, w3, Kd, out, co, **kw_), CAPMI_A_KMAJOR
+            else:
+                sc, sh = in_ss if in_ss is not None else (None, None)
+                prob = K.problem(rows, co, Kd, x, 0, w3, Kd, out, co, conv=geo, in_scale=sc, in_shift=sh, **kw_)
+                mode = CAPMI_A_CONV_NHWC
+            launch = lambda: K.gemm_x3d(prob, mode, self._ws["sk"])  # noqa: E731
+            if self.conv_hook is not None:
+                self.conv_hook(tag, 2.0 * rows * co * Kd, launch, K.gemm_x3d_kernel_name(prob, mode))
+            else:
+                launch()
+            return Ho, Wo, rows
         elif x3p:
             # x3p: the conv input relu(bn(y)) split once into three bf16 planes, then the GEMM with
             # both operands pre-split (gemm_x3p.hip). Where it pays (tools/x3_ab.py, batch 64): the

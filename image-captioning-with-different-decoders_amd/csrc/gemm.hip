@@ -664,6 +664,7 @@ int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gemm
             long long& total);
 int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total,
              int& bk);
+int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total);
 }  // namespace
 
 extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, int flags,
@@ -681,6 +682,18 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
     if (bn) *bn = 128;
     if (stream_k) *stream_k = sk ? 1 : 0;
     if (generic) *generic = bk;  // CAPMI_GEMM_X3P: the k-tile depth
+    return 0;
+  }
+  if (flags == CAPMI_GEMM_X3D) {
+    GemmArgs a;
+    long long total = 0;
+    const int rc = x3d_plan(prob, amode, bmode, a, sk, total);
+    if (rc) return rc;
+    if (threads) *threads = 512;
+    if (bm) *bm = 256;
+    if (bn) *bn = 128;
+    if (stream_k) *stream_k = sk ? 1 : 0;
+    if (generic) *generic = 32;
     return 0;
   }
   if (flags == CAPMI_GEMM_X3) {
@@ -880,6 +893,64 @@ int gemm_x3p(const capmi_gemm_problem* prob, int amode, int bmode, void* workspa
   return gemm_x3p_launch(a, amode, bk, a.sk_workers, s);
 }
 
+// CAPMI_GEMM_X3D: fp32 A (+ BN prologue for convs) split in-kernel x three-plane B in the x3p k order
+// (gemm_x3p.hip, ASPLIT): 256x128 tiles, 512 threads, k-tiles of 32, one workgroup per CU, stream-K
+// when the tiles under-fill the chip
+int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total) {
+  CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
+  const capmi_gemm_problem& p = *prob;
+  CAPMI_REQUIRE(bmode == CAPMI_B_NMAJOR_W && (amode == CAPMI_A_KMAJOR || amode == CAPMI_A_CONV_NHWC), CAPMI_EINVAL);
+  CAPMI_REQUIRE(p.A && p.B && p.C && p.M >= 0 && p.N > 0 && p.K > 0 && p.K % 32 == 0 && p.ksplit == 1, CAPMI_EINVAL);
+  CAPMI_REQUIRE(amode == CAPMI_A_CONV_NHWC || (!p.in_scale && !p.in_shift), CAPMI_EINVAL);
+  CAPMI_REQUIRE((p.in_scale == nullptr) == (p.in_shift == nullptr), CAPMI_EINVAL);
+  CAPMI_REQUIRE(p.a_r1 <= 0 && (p.stats == nullptr || p.c_r1 <= 0), CAPMI_EINVAL);
+  CAPMI_REQUIRE(aligned16(p.A) && aligned16(p.B) && p.ldb % 8 == 0 && p.ldb >= p.K, CAPMI_EALIGN);
+  CAPMI_REQUIRE(p.in_scale == nullptr || (aligned16(p.in_scale) && aligned16(p.in_shift)), CAPMI_EALIGN);
+  CAPMI_REQUIRE(3LL * p.N * p.ldb * 2 < (1LL << 31), CAPMI_ERANGE);
+  if (amode == CAPMI_A_CONV_NHWC) {
+    CAPMI_REQUIRE(p.cCin % 32 == 0 && p.K == p.cKH * p.cKW * p.cCin && p.M == p.cN * p.cHo * p.cWo, CAPMI_EINVAL);
+    CAPMI_REQUIRE((long long)p.cN * p.cH * p.cW * p.cCin * 4 < (1LL << 31), CAPMI_ERANGE);
+  } else {
+    CAPMI_REQUIRE(p.lda % 4 == 0 && p.lda >= p.K, CAPMI_EALIGN);
+    CAPMI_REQUIRE((long long)p.M * p.lda * 4 < (1LL << 31), CAPMI_ERANGE);
+  }
+  memset(&a, 0, sizeof(a));
+  a.nprob = 1;
+  a.p[0] = p;
+  a.tiles_m[0] = (int)cdiv(p.M, 256);
+  a.tiles_n[0] = (int)cdiv(p.N, 128);
+  total = (long long)a.tiles_m[0] * a.tiles_n[0];
+  a.tiles_begin[1] = (int)total;
+  const long long slots = sk_cus();
+  const int nkt = p.K / 32;
+  const long long rounds = (total + slots - 1) / slots;
+  sk = !sk_off() && total > 0 && nkt >= 8 && (double)total / (double)(rounds * slots) < 0.9;
+  return 0;
+}
+
+int gemm_x3d(const capmi_gemm_problem* prob, int amode, int bmode, void* workspace, long long ws_bytes,
+             hipStream_t s) {
+  GemmArgs a;
+  bool sk = false;
+  long long total = 0;
+  const int rc = x3d_plan(prob, amode, bmode, a, sk, total);
+  if (rc) return rc;
+  if (prob->M == 0) return 0;
+  if (!sk || workspace == nullptr) return gemm_x3d_launch(a, amode, (int)total, s);
+  CAPMI_REQUIRE(aligned16(workspace), CAPMI_EINVAL);
+  CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
+  const int cus = cu_count();
+  const long long slots = sk_cus();
+  a.sk_nkt = prob->K / 32;
+  a.sk_dp_tiles = sk_hybrid() && total >= 2 * slots ? (int)((total / slots - 1) * slots) : 0;
+  a.sk_units = (total - a.sk_dp_tiles) * a.sk_nkt;
+  a.sk_workers = (int)std::min<long long>(slots, a.sk_units);
+  a.sk_groups = sk_xcd_groups() && a.sk_workers % 8 == 0 && total >= 64 ? 8 : 1;
+  a.sk_flags = static_cast<int*>(workspace);
+  a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
+  return gemm_x3d_launch(a, amode, a.sk_workers, s);
+}
+
 int gemm_x3(const capmi_gemm_problem* prob, int amode, int bmode, int tile, void* workspace, long long ws_bytes,
             hipStream_t s) {
   GemmArgs a;
@@ -912,6 +983,7 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   if (flags == CAPMI_GEMM_BF16_IO) return gemm_bf16_io(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3) return gemm_x3(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3P) return gemm_x3p(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
+  if (flags == CAPMI_GEMM_X3D) return gemm_x3d(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
   int terms = flag_terms(flags);
   CAPMI_REQUIRE(terms >= 0, CAPMI_EINVAL);
   CAPMI_REQUIRE(terms_mode_ok(terms, amode, bmode), CAPMI_EINVAL);

@@ -39,6 +39,8 @@ int gemm_x3_launch(const GemmArgs& a, int amode, int bn, int blocks, hipStream_t
 // bk (16: two workgroups per CU, data-parallel grids only; 32: one, stream-K capable) is the unit
 // of GemmArgs::sk_nkt for it
 int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_t s);
+// x3p with A fp32 split in-kernel ("x3d": register-staged A + optional conv BN prologue, LDS-DMA B)
+int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s);
 // resident workgroups per CU of the NT kernel for a tile shape (LDS / register bound)
 // (terms 3: three bf16 LDS planes per operand, 60 KB for 64x64 and >= 90 KB for the larger tiles)
 inline int gemm_nt_wg_per_cu(int bm, int bn, int terms = 0) {

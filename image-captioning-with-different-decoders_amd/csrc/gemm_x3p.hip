@@ -49,9 +49,15 @@ struct X3pGeo {
   static constexpr int WPE = PBK == 16 ? 4 : 2;     // waves per SIMD: two workgroups per CU at BK = 16
 };
 
-template <int AMODE, bool SK, int PBK>
+// ASPLIT ("x3d"): A is the fp32 operand itself (dense, or the NHWC conv input with the optional BN-apply
+// + ReLU prologue PRO), loaded to registers one k-tile ahead and split into the three swizzled LDS
+// planes after the k-tile's MFMAs; B stays LDS-DMA. It replaces gemm_x3 (both operands through
+// registers) and the separate split pass of x3p (BK = 32 only).
+template <int AMODE, bool SK, int PBK, bool ASPLIT = false, bool PRO = false>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(X3pGeo<PBK>::WPE)))
 gemm_x3p_kernel(const GemmArgs args) {
+  static_assert(!ASPLIT || PBK == 32, "x3d: 32-deep k-tiles");
+  static_assert(!PRO || (ASPLIT && AMODE == 2), "prologue: x3d conv");
   using G_ = X3pGeo<PBK>;
   constexpr int PROWB = G_::PROWB, CPR = G_::CPR, RPB = G_::RPB, SWZ = G_::SWZ;
   constexpr int PA_BYTES = G_::PA_BYTES, PBUF = G_::PBUF, NAB = G_::NAB, NBB = G_::NBB;
@@ -86,7 +92,7 @@ gemm_x3p_kernel(const GemmArgs args) {
 #define X3P_SKIP 0
 #endif
     // X3P_PRICE (timing-only builds): 1 = A descriptor with zero records (no A traffic), 2 = B, 3 = both
-    const auto ra = rsrc_p(P.A, (X3P_PRICE & 1) ? 0u : (unsigned)(3 * planeA * 2));
+    const auto ra = rsrc_p(P.A, (X3P_PRICE & 1) ? 0u : (unsigned)(ASPLIT ? planeA * 4 : 3 * planeA * 2));
     const auto rb = rsrc_p(P.B, (X3P_PRICE & 2) ? 0u : (unsigned)(3 * planeB * 2));
     // this lane's two A rows (row blocks 2 wid, 2 wid + 1) and one B row (row block wid)
     // (arrays sized 2 >= NAB: a dependent bound in the nested lambda loses the host launch stub)
@@ -117,6 +123,37 @@ gemm_x3p_kernel(const GemmArgs args) {
     const int b_ch = dslot ^ ((br / SWZ) % CPR);
     const bool b_ok = bw && n0 + br < N;
     const unsigned b_base = (unsigned)(((long long)(b_ok ? n0 + br : 0) * P.ldb + b_ch * 8) * 2);
+    // x3d: four fp32 float4 slots per thread, slot i = row (tid + 512 i) / 8, k 4 ((tid + 512 i) % 8)
+    constexpr int NSA = ASPLIT ? 4 : 1;
+    const int aq = tid & 7;
+    unsigned s_base[NSA];
+    int s_ih0[NSA], s_iw0[NSA];
+    bool s_ok[NSA];
+    int s_lds[NSA];  // byte offset of the slot's 8 B in plane 0 (swizzled chunk)
+    if (ASPLIT) {
+#pragma unroll
+      for (int i = 0; i < NSA; ++i) {
+        const int r = (tid + 512 * i) >> 3;
+        const int row = m0 + r;
+        s_ok[i] = row < M;
+        s_lds[i] = r * PROWB + (((aq >> 1) ^ ((r / SWZ) % CPR)) << 4) + (aq & 1) * 8;
+        if (AMODE == 0) {
+          s_base[i] = (unsigned)(((long long)(s_ok[i] ? row : 0) * P.lda + aq * 4) * 4);
+          s_ih0[i] = s_iw0[i] = 0;
+        } else {
+          const int hw = P.cHo * P.cWo;
+          const int rr = s_ok[i] ? row : 0;
+          const int n = rr / hw, rem = rr - n * hw;
+          const int oh = rem / P.cWo, ow = rem - oh * P.cWo;
+          s_ih0[i] = oh * P.cStride - P.cPad;
+          s_iw0[i] = ow * P.cStride - P.cPad;
+          s_base[i] = (unsigned)(n * cH * cW);
+        }
+      }
+    }
+    float4 areg[NSA];
+    float4 a_sc = make_float4(1.f, 1.f, 1.f, 1.f), a_sh = make_float4(0.f, 0.f, 0.f, 0.f);
+    unsigned a_msk = 0;
     // conv k order (ci / 32, kh, kw, ci % 32): the taps of one 32-channel slice are consecutive
     // k-tiles, so the input rows a tile re-reads for its KH*KW taps are re-read within KH*KW k-tiles
     // (L2-resident) instead of once per full sweep over Cin; the weights are packed to match
@@ -142,9 +179,32 @@ gemm_x3p_kernel(const GemmArgs args) {
 #endif
       const int k = k_lo + kt * PBK;
       const bool kok = k < k_hi;
+      if (ASPLIT) {
+        a_msk = 0;
+        if (PRO && kok) {  // (past the last k-tile the walk is past Cin: no read)
+          a_sc = *reinterpret_cast<const float4*>(P.in_scale + c_ci + aq * 4);
+          a_sh = *reinterpret_cast<const float4*>(P.in_shift + c_ci + aq * 4);
+        }
+#pragma unroll
+        for (int i = 0; i < NSA; ++i) {
+          unsigned off;
+          bool ok;
+          if (AMODE == 0) {
+            ok = s_ok[i] && kok;
+            off = s_base[i] + (unsigned)k * 4;
+          } else {
+            const int ih = s_ih0[i] + c_kh, iw = s_iw0[i] + c_kw;
+            ok = s_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
+            off = ((s_base[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + aq * 4)) * 4u;
+          }
+          areg[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off : kOOBp, 0, 0));
+          a_msk |= (unsigned)ok << i;
+        }
+      }
       unsigned aoff[2];
 #pragma unroll
       for (int i = 0; i < NAB; ++i) {
+        if (ASPLIT) break;
         if (AMODE == 0) {
           aoff[i] = a_ok[i] && kok ? a_base[i] + (unsigned)k * 2 : kOOBp;
         } else {
@@ -168,7 +228,7 @@ gemm_x3p_kernel(const GemmArgs args) {
 #pragma unroll
       for (int p = 0; p < 3; ++p)
 #pragma unroll
-        for (int i = 0; i < NAB; ++i)
+        for (int i = 0; i < (ASPLIT ? 0 : NAB); ++i)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
               ra, (lds_ptr_t)(base + p * PBM * PROWB + (NAB * wid + i) * RPB * PROWB), 16,
               aoff[i] == kOOBp ? kOOBp : aoff[i] + p * pA2, 0, 0, 0);
@@ -179,6 +239,37 @@ gemm_x3p_kernel(const GemmArgs args) {
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
               rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * RPB * PROWB), 16,
               boff == kOOBp ? kOOBp : boff + p * pB2, 0, 0, 0);
+      }
+    };
+    // x3d: the registers of the k-tile loaded by the last issue() -> (prologue) -> three planes
+    auto store_a = [&](int buf) {
+      if (!ASPLIT) return;
+      unsigned char* base = lds + buf * PBUF;
+#pragma unroll
+      for (int i = 0; i < NSA; ++i) {
+        float4 v = areg[i];
+        if (PRO) v = make_float4(fmaxf(fmaf(v.x, a_sc.x, a_sh.x), 0.f), fmaxf(fmaf(v.y, a_sc.y, a_sh.y), 0.f),
+                                 fmaxf(fmaf(v.z, a_sc.z, a_sh.z), 0.f), fmaxf(fmaf(v.w, a_sc.w, a_sh.w), 0.f));
+        if (!((a_msk >> i) & 1u)) v = make_float4(0.f, 0.f, 0.f, 0.f);  // padding taps: zeros AFTER the BN
+        const float e[4] = {v.x, v.y, v.z, v.w};
+        unsigned short h[3][4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const __bf16 h0 = (__bf16)e[q];
+          const float r1 = e[q] - (float)h0;
+          const __bf16 h1 = (__bf16)r1;
+          const __bf16 h2 = (__bf16)(r1 - (float)h1);
+          h[0][q] = __builtin_bit_cast(unsigned short, h0);
+          h[1][q] = __builtin_bit_cast(unsigned short, h1);
+          h[2][q] = __builtin_bit_cast(unsigned short, h2);
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          uint2 w;
+          w.x = (unsigned)h[p][0] | ((unsigned)h[p][1] << 16);
+          w.y = (unsigned)h[p][2] | ((unsigned)h[p][3] << 16);
+          *reinterpret_cast<uint2*>(base + p * PBM * PROWB + s_lds[i]) = w;
+        }
       }
     };
     auto compute = [&](int buf) {
@@ -238,6 +329,7 @@ gemm_x3p_kernel(const GemmArgs args) {
     };
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store_a(0);
     __syncthreads();
     for (int kt = 0; kt < nkt; ++kt) {
       issue(kt + 1, (kt + 1) & 1);  // past the end: OOB loads (zeros) into the idle buffer
@@ -246,6 +338,7 @@ gemm_x3p_kernel(const GemmArgs args) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      store_a((kt + 1) & 1);  // x3d: buffer (kt + 1) & 1 was last read by compute(kt - 1)
       __syncthreads();
 #endif
     }
@@ -454,6 +547,26 @@ __global__ void __launch_bounds__(256) bn_relu_split3_kernel(const float4* __res
 }
 
 }  // namespace
+
+int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
+  const dim3 g(blocks), b(PNT);
+  const bool sk = a.sk_workers > 0;
+  const bool pro = a.p[0].in_scale != nullptr;
+  CAPMI_REQUIRE(!pro || amode == 2, CAPMI_EINVAL);
+#define X3D_GO(M, S, PR) hipLaunchKernelGGL((gemm_x3p_kernel<M, S, 32, true, PR>), g, b, 0, s, a)
+  if (amode == 2) {
+    if (pro) {
+      if (sk) X3D_GO(2, true, true); else X3D_GO(2, false, true);
+    } else {
+      if (sk) X3D_GO(2, true, false); else X3D_GO(2, false, false);
+    }
+  } else {
+    if (sk) X3D_GO(0, true, false); else X3D_GO(0, false, false);
+  }
+#undef X3D_GO
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
 
 int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_t s) {
   const dim3 g(blocks), b(PNT);

@@ -133,6 +133,11 @@ int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int t
  * when there are >= 2 x CUs tiles filling >= 70 % of the last round, else k-tiles of 32, one
  * workgroup per CU, stream-K as capmi_gemm_sk. */
 #define CAPMI_GEMM_X3P 8
+/* CAPMI_GEMM_X3D (alone): the CAPMI_GEMM_X3P kernel with A the fp32 operand itself (CAPMI_A_KMAJOR,
+ * lda % 4 == 0, or CAPMI_A_CONV_NHWC, Cin % 32 == 0, with the optional BN-apply + ReLU prologue),
+ * split into the three bf16 planes in-kernel while B (pre-split, x3p k order) is LDS-DMA staged;
+ * 256x128 tiles, k-tiles of 32, one workgroup per CU, stream-K as capmi_gemm_sk. */
+#define CAPMI_GEMM_X3D 32
 /* CAPMI_GEMM_SPLIT3 (alone): fp32 A and B, both split exactly into three bf16 terms when staged to
  * LDS (the CAPMI_GEMM_X3 arithmetic with no pre-split operand: fp32-accurate on the bf16 matrix
  * cores). Dense modes only: CAPMI_A_KMAJOR x CAPMI_B_NMAJOR_W / CAPMI_B_KROWS and CAPMI_A_MMAJOR x

@@ -198,3 +198,47 @@ def test_x3p_conv_stats(N, H, Cin, Cout, k, stride, pro):
     st = stats.double().cpu()[: 2 * ((rows + 63) // 64) * Cout].view(-1, Cout, 2)
     torch.testing.assert_close(st[..., 0].sum(0), o.sum(0), rtol=1e-5, atol=1e-3)
     torch.testing.assert_close(st[..., 1].sum(0), (o * o).sum(0), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,k,stride,pro", [
+    (4, 14, 256, 256, 3, 1, True), (4, 28, 128, 128, 3, 2, True), (2, 56, 64, 256, 1, 1, True),
+    (3, 14, 256, 1024, 1, 1, True), (2, 7, 512, 2048, 1, 1, False), (64, 14, 256, 256, 3, 1, True),
+    (1, 9, 64, 128, 3, 1, True), (64, 14, 1024, 256, 1, 1, False), (64, 28, 128, 128, 3, 1, True),
+    (64, 14, 256, 1024, 1, 1, True), (64, 56, 128, 128, 3, 2, True), (64, 28, 512, 256, 1, 2, False)])
+def test_x3d_conv_stats(N, H, Cin, Cout, k, stride, pro):
+    """A fp32 split in-kernel with the BN prologue, B pre-split in the x3p order (CAPMI_GEMM_X3D):
+    the conv of relu(x*s+b) vs fp64 under the x3 rule, and the BN statistics; dense 1x1 (no prologue,
+    stride 1) through CAPMI_A_KMAJOR."""
+    K = _K()
+    pad = k // 2
+    Ho = (H + 2 * pad - k) // stride + 1
+    x = rnd(N, H, H, Cin, seed=21)
+    w = rnd(Cout, k, k, Cin, seed=22) * (2.0 / (k * k * Cin)) ** 0.5
+    s, b = rnd(Cin, seed=23) + 1.0, rnd(Cin, seed=24)
+    xin = torch.relu(torch.addcmul(b, x, s)) if pro else x
+    rows, Kd = N * Ho * Ho, k * k * Cin
+    ws = K.gemm_workspace(DEV)
+    xd = x.to(DEV).contiguous()
+    stats = torch.zeros(2 * K.stat_tiles(rows) * Cout, device=DEV)
+    out = torch.full((rows, Cout), float("nan"), device=DEV)
+    w3 = split3(K.conv_weight_order_x3p(w.reshape(Cout, Kd), k, k, Cin).contiguous().to(DEV))
+    if k == 1 and stride == 1 and not pro:
+        prob, mode = K.problem(rows, Cout, Kd, xd, Cin, w3, Kd, out, Cout, stats=stats), 0
+    else:
+        geo = dict(N=N, H=H, W=H, Cin=Cin, KH=k, KW=k, stride=stride, pad=pad, Ho=Ho, Wo=Ho)
+        prob = K.problem(rows, Cout, Kd, xd, 0, w3, Kd, out, Cout, conv=geo, stats=stats,
+                         in_scale=s.to(DEV) if pro else None, in_shift=b.to(DEV) if pro else None)
+        mode = 2
+    K.gemm_x3d(prob, mode, ws)
+    torch.cuda.synchronize()
+    K.sk_check([ws])
+    xi = xin.double().permute(0, 3, 1, 2)
+    wt = w.double().permute(0, 3, 1, 2)
+    ref = F.conv2d(xi, wt, stride=stride, padding=pad).permute(0, 2, 3, 1).reshape(rows, Cout)
+    ref_abs = F.conv2d(xi.abs(), wt.abs(), stride=stride, padding=pad).permute(0, 2, 3, 1).reshape(rows, Cout)
+    r3, _ = _errs(out, ref, ref_abs)
+    assert r3 <= 1.0, r3
+    o = out.double().cpu()
+    st = stats.double().cpu()[: 2 * ((rows + 63) // 64) * Cout].view(-1, Cout, 2)
+    torch.testing.assert_close(st[..., 0].sum(0), o.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(st[..., 1].sum(0), (o * o).sum(0), rtol=1e-5, atol=1e-3)

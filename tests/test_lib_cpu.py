@@ -76,7 +76,7 @@ def test_gemm_sk_plan_on_host():
     assert rc == 0 and (bm, bn, generic, nt) == (128, 128, 0, 512)
     assert plan(64)[1][4] == 256
     assert plan(256, flags=1)[1][4] == 256
-    assert plan(256, flags=32)[0] == 1001  # unknown flag
+    assert plan(256, flags=64)[0] == 1001  # unknown flag
     assert plan(256, flags=1 | 16)[0] == 1001  # flags do not combine
     # CAPMI_GEMM_SPLIT3 (16) on a conv: the 256-thread split-staged kernel, two workgroups per CU
     # for 64x64 (stream-K sized for that)

@@ -67,6 +67,11 @@ def main():
         arms = [("native", lambda: K.gemm_sk(pn, mode, ws)), ("x3", lambda: K.gemm_x3(p3, mode, ws)),
                 ("nts", lambda: K.gemm_sk(pn, mode, ws, flags=CAPMI_GEMM_SPLIT3)),
                 ("nts128", lambda: K.gemm_sk(pn, mode, ws, K.TILE_128x64, flags=CAPMI_GEMM_SPLIT3))]
+        if Cin % 32 == 0:  # x3d: A fp32 split in-kernel (+ prologue), B pre-split in the x3p order, DMA
+            w3d = torch.empty_like(w3)
+            K.split3_bf16(K.conv_weight_order_x3p(w, k, k, Cin).contiguous(), w3d)
+            pd = K.problem(rows, Cout, Kd, x, Cin if dense else 0, w3d, Kd, out, Cout, **kw)
+            arms.append(("x3d", lambda: K.gemm_x3d(pd, mode, ws)))
         if pro and Cout >= 128 and Cin % 32 == 0:  # x3p candidates: split pass + pre-split GEMM
             xp = torch.empty(3 * x.numel(), device=dev, dtype=torch.bfloat16)
             w3p = torch.empty_like(w3)
@@ -98,7 +103,7 @@ def main():
         print(f"| {tag} | {cnt} | {rows} | {Cout} | {Kd} | {res['native']:.1f} | {f / res['native'] / 1e6:.1f} | "
               f"{res['x3']:.1f} | {f / res['x3'] / 1e6:.1f} | {res['native'] / best:.2f} | "
               f"{K.gemm_x3_kernel_name(p3, mode)}{x3p} | split-staged 64x64 {res['nts']:.1f} us, 128x64 "
-              f"{res['nts128']:.1f} us |")
+              f"{res['nts128']:.1f} us | x3d {res.get('x3d', float('nan')):.1f} us |")
     print(f"\nlayer1-4 convs per forward: native {tot['native'] / 1e3:.3f} ms, best x3 form {tot['x3'] / 1e3:.3f} ms")
 
 
