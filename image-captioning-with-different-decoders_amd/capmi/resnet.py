@@ -145,9 +145,8 @@ def pool_dup(H, W, out_hw):
 
 # x3 mode: convs with K <= this run both operands split in-kernel (CAPMI_GEMM_SPLIT3) instead of gemm_x3
 _X3_SMALLK = int(os.environ.get("CAPMI_X3_SMALLK", "0"))
-# x3 mode: route the shapes where it measured fastest to the x3d kernel (CAPMI_X3D=1; off by default
-# until the encoder-level fault seen with it at batch 2 is found)
-_X3D = os.environ.get("CAPMI_X3D", "0") == "1"
+# x3 mode: route the shapes where it measured fastest to the x3d kernel (CAPMI_X3D=0: off, A/B)
+_X3D = os.environ.get("CAPMI_X3D", "1") != "0"
 # train-mode BN finalize fused into the consumer pass where it fits (capmi_bn_finalize_apply), opt-in
 # with CAPMI_BN_FUSE=1: measured slower than the separate finalize launch (headline 5558 -> 5458,
 # bf16 config 10559 -> 9732 img/s)
