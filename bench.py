@@ -483,7 +483,7 @@ def main():
         fam_ms = sum(v[2] for v in per.values())
         per_img = sum(v[1] for v in per.values()) / args.steps / B
         peak = BF16_MFMA_PEAK_TF if encoder._runner.bf16 else FP32_MFMA_PEAK_TF
-        if "x3" in key:
+        if "x3" in key or (key.startswith("gemm_nts_kernel<") and key.split(",")[5].strip().startswith("3")):
             # the x3 kernels run six bf16 MFMAs per fp32 multiply-add: their matrix-core bound for
             # fp32 arithmetic is the dense bf16 peak / 6 (417 TF/s)
             peak = round(BF16_MFMA_PEAK_TF / 6, 1)

@@ -205,7 +205,7 @@ def gemm_x3p_kernel_name(prob, amode):
     v = [ctypes.c_int(0) for _ in range(5)]
     call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3P,
          *[ctypes.byref(x) for x in v])
-    return f"gemm_x3p_kernel<{amode}, {'true' if v[2].value else 'false'}, {v[3].value}>"
+    return f"gemm_x3p_kernel<{amode}, {'true' if v[2].value else 'false'}, {v[3].value}, false, false>"
 
 
 def gemm_x3_kernel_name(prob, amode, tile=CAPMI_TILE_AUTO):
