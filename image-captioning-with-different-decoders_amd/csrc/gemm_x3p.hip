@@ -272,7 +272,11 @@ gemm_x3p_kernel(const GemmArgs args) {
         }
       }
     };
-    auto compute = [&](int buf) {
+#ifndef X3D_MID
+#define X3D_MID 0
+#endif
+    // X3D_MID (A/B): x3d writes the next k-tile's A planes between the two 16-k chunks' MFMAs
+    auto compute = [&](int buf, int nbuf) {
       const unsigned char* A_ = lds + buf * PBUF;
       const unsigned char* B_ = A_ + PA_BYTES;
       // every fragment of the k-tile is requested up front (2 x 12 ds_read_b128): the second
@@ -325,7 +329,12 @@ gemm_x3p_kernel(const GemmArgs args) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[g][i][1], b[g][j][0], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[g][i][0], b[g][j][0], acc[i][j], 0, 0, 0);
           }
+        if (X3D_MID && ASPLIT && g == 0) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          store_a(nbuf);
+        }
       }
+      (void)nbuf;
     };
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -333,12 +342,12 @@ gemm_x3p_kernel(const GemmArgs args) {
     __syncthreads();
     for (int kt = 0; kt < nkt; ++kt) {
       issue(kt + 1, (kt + 1) & 1);  // past the end: OOB loads (zeros) into the idle buffer
-      compute(kt & 1);
+      compute(kt & 1, (kt + 1) & 1);
 #if X3P_SKIP & 4  // timing-only: no barrier inside the k-loop
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      store_a((kt + 1) & 1);  // x3d: buffer (kt + 1) & 1 was last read by compute(kt - 1)
+      if (!X3D_MID) store_a((kt + 1) & 1);  // x3d: buffer (kt + 1) & 1 was last read by compute(kt - 1)
       __syncthreads();
 #endif
     }
