@@ -81,8 +81,8 @@ def parse():
                          "v_mfma_f32_32x32x2_f32")
     ap.add_argument("--dec", default="auto", choices=["auto", "x3", "fp32", "bf16"],
                     help="decoder GEMM arithmetic (AttentionDecoder.set_compute_precision): auto = bf16 for the "
-                         "bf16 config, else fp32 (v_mfma_f32_32x32x2_f32; tools/dec_gemm_ab.py: the x3 split is "
-                         "slower on the transposed-operand backward GEMMs); x3 = fp32-accurate three-term split")
+                         "bf16 config, else x3 (fp32-accurate three-term split on the bf16 matrix cores: 1.80 vs "
+                         "1.92 ms of decoder GEMMs per step, +0.4 %% img/s); fp32 = v_mfma_f32_32x32x2_f32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="cpu_baseline: keep stepping the oracle at the full batch until this much time "
@@ -406,7 +406,7 @@ def main():
             encoder.set_compute_precision("bf16")  # config 5 is the bf16 config
     if not encoder._runner.bf16 and args.conv == "x3":
         encoder.set_compute_precision("fp32-x3")
-    dec_prec = args.dec if args.dec != "auto" else ("bf16" if encoder._runner.bf16 else "fp32")
+    dec_prec = args.dec if args.dec != "auto" else ("bf16" if encoder._runner.bf16 else "x3")
     decoder.set_compute_precision({"x3": "fp32-x3", "fp32": "fp32", "bf16": "bf16"}[dec_prec])
     if ft:
         # synthetic GloVe-300 table, fp64 like load_glove_vectors (embed.py:64-68, Q7)
