@@ -29,7 +29,17 @@
 namespace {
 
 constexpr int XBK = 32;       // fp32 k per k-tile
-constexpr int XSB = XBK + 8;  // LDS row stride (bf16 elements)
+#ifndef X3_SWZ
+#define X3_SWZ 0
+#endif
+// LDS row stride (bf16 elements). X3_SWZ (default): 64-B rows with x3p's 16-B chunk swizzle (chunk c
+// of row r at c ^ ((r / 4) % 4)): the 8-B split stores of a wave (8 rows x 64 B) and the 16-lane
+// ds_read_b128 groups both hit 64 distinct banks. Else 80-B padded rows (the reads conflict-free,
+// the split stores 2-3-way conflicted: PMC lds_conflict 29 %, profiles/r02_pmc_sq.txt).
+constexpr int XSB = X3_SWZ ? XBK : XBK + 8;
+__device__ __forceinline__ int xoff(int row, int chunk) {  // bf16 offset of 8-element chunk `chunk` of `row`
+  return row * XSB + ((X3_SWZ ? (chunk ^ ((row >> 2) & 3)) : chunk) << 3);
+}
 constexpr int XNT = 512;
 typedef unsigned u32x4_x __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_x __attribute__((ext_vector_type(8)));
@@ -121,7 +131,7 @@ gemm_x3_kernel(const GemmArgs args) {
       const int n = n0 + r;
       const bool ok = c < 3 * BN * 4 && n < N;
       b_off[i] = ok ? (unsigned)((p * plane + (long long)n * P.ldb + kc) * 2) : kOOBx;
-      b_lds[i] = c < 3 * BN * 4 ? (p * BN * XSB + r * XSB + kc) : -1;
+      b_lds[i] = c < 3 * BN * 4 ? (p * BN * XSB + xoff(r, kc >> 3)) : -1;
     }
     int c_ci = 0, c_kh = 0, c_kw = 0;  // conv k walk, advanced XBK per k-tile
     if (AMODE == 2) {
@@ -193,7 +203,7 @@ gemm_x3_kernel(const GemmArgs args) {
         const bf16x4_x h1 = cvt4(r1);
         const bf16x4_x h2 = cvt4(sub4(r1, back4(h1)));
 #endif
-        const int o = ((tid + i * XNT) >> 3) * XSB + kq;
+        const int o = xoff((tid + i * XNT) >> 3, kq >> 3) + (kq & 7);
         *reinterpret_cast<bf16x4_x*>(&As[buf][0][o]) = h0;
         *reinterpret_cast<bf16x4_x*>(&As[buf][1][o]) = h1;
         *reinterpret_cast<bf16x4_x*>(&As[buf][2][o]) = h2;
@@ -206,14 +216,14 @@ gemm_x3_kernel(const GemmArgs args) {
 #pragma unroll
       for (int g = 0; g < XBK / 16; ++g) {
         bf16x8_x a[3], b[3][TN];
-        const int ao = (wm0 + lr) * XSB + 16 * g + 8 * lh;
+        const int ao = xoff(wm0 + lr, 2 * g + lh);
 #pragma unroll
         for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8_x*>(&As[buf][p][ao]);
 #pragma unroll
         for (int p = 0; p < 3; ++p)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            b[p][j] = *reinterpret_cast<const bf16x8_x*>(&Bs[buf][p][(wn0 + 32 * j + lr) * XSB + 16 * g + 8 * lh]);
+            b[p][j] = *reinterpret_cast<const bf16x8_x*>(&Bs[buf][p][xoff(wn0 + 32 * j + lr, 2 * g + lh)]);
         // smallest terms first into the fp32 accumulator
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
