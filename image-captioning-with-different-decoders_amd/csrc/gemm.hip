@@ -598,6 +598,16 @@ bool sk_off() {
   }();
   return off;
 }
+// the three-term conv weight gradients keep the fp32 wgrad tile rule (128x128 / 128x64, one workgroup per
+// CU): fine-tune config 1633 -> 1647 img/s against 64x64 (fewer re-reads of dY and the im2col rows).
+// CAPMI_X3_WGRAD_WIDE=0: 64x64 (A/B measurement)
+bool x3_wgrad_wide() {
+  static const bool on = [] {
+    const char* e = getenv("CAPMI_X3_WGRAD_WIDE");
+    return !(e && e[0] == '0' && e[1] == 0);
+  }();
+  return on;
+}
 // the launch capmi_gemm_sk makes for a problem (shared by the launcher and the plan query)
 int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, int terms, GemmPlan& g, bool& sk) {
   const bool bf16 = terms > 0;
@@ -616,7 +626,7 @@ int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, in
     tile = (prob->M >= 256 && prob->N >= 2048) ? CAPMI_TILE_128 : CAPMI_TILE_128x64;
   // three-term split staging: 64x64 everywhere (two workgroups per CU; the larger tiles hold one:
   // tools/dec_gemm_ab.py --tile, 5-20 % faster on every decoder GEMM at 64x64)
-  if (automatic && terms == 3) tile = CAPMI_TILE_64;
+  if (automatic && terms == 3 && !(bmode == CAPMI_B_CONV_NHWC && x3_wgrad_wide())) tile = CAPMI_TILE_64;
   int rc = gemm_plan(prob, 1, amode, bmode, tile, g);
   if (rc) return rc;
   // the 512-thread 128x128 form (tools/w8_ab.sh over all 19 encoder conv shapes, batch 64):
