@@ -237,8 +237,8 @@ def gemm_sk_kernel_name(prob, amode, bmode=CAPMI_B_NMAJOR_W, bf16=False, tile=CA
         return f"gemm_nt8_kernel<{amode}, {pro}, {b(sk)}>"
     split = f == CAPMI_GEMM_SPLIT3 or (f == 1 and (amode == 1 or bmode == 1))
     if split and not (f == 1 and bmode == 0 and amode != 1):
-        tail = ", true" if prob.in_scale else ""  # the BN-prologue conv form
-        return f"gemm_nts_kernel<{bm}, {bn}, {amode}, {bmode}, {b(sk)}, {3 if f == CAPMI_GEMM_SPLIT3 else 1}{tail}>"
+        # rocprofv3 prints the defaulted PRO argument too (true: the BN-prologue conv form)
+        return f"gemm_nts_kernel<{bm}, {bn}, {amode}, {bmode}, {b(sk)}, {3 if f == CAPMI_GEMM_SPLIT3 else 1}, {pro}>"
     return f"gemm_nt_kernel<{bm}, {bn}, {amode}, {bmode}, {pro}, {b(sk)}, {b(f == 1)}>"
 
 

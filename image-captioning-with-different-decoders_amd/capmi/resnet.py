@@ -591,6 +591,10 @@ class _Pool:
 
 _FT_DGRAD_X3 = os.environ.get("CAPMI_FT_DGRAD_X3", "1") != "0"
 _FT_WGRAD_X3 = os.environ.get("CAPMI_FT_WGRAD_X3", "1") != "0"
+# x3 mode: 3x3 / sub-pixel data gradients on x3d (dY split in registers x the x3p-ordered split of
+# the packed dgrad weight, re-split every step) instead of the split-staging nts form
+_FT_DGRAD_X3D = os.environ.get("CAPMI_FT_DGRAD_X3D", "1") != "0"
+_FT_DGRAD1_X3D = os.environ.get("CAPMI_FT_DGRAD1_X3D", "0") != "0"  # 1x1 dgrads: neutral (1666 both), off
 
 
 class FineTuneRunner:
@@ -761,6 +765,34 @@ class FineTuneRunner:
                 hook(tag, flops, lambda: self._gemm(prob, amode, bmode, tile),
                      K.gemm_sk_kernel_name(prob, amode, bmode, tile=tile, flags=self._flags(prob, amode, bmode)))
 
+        x3d = self.r.x3 and _FT_DGRAD_X3 and _FT_DGRAD_X3D
+        x3d1 = self.r.x3 and _FT_DGRAD_X3 and _FT_DGRAD1_X3D
+        if x3d or x3d1:
+            word = gp("w_dgrad_ord", max(wmax, w1max), dev)
+            w3 = gp("w_dgrad_x3", 3 * max(wmax, w1max), dev, dtype=torch.bfloat16)
+
+        def run_dgrad(tag, flops, prob, w, kh=1, kw=1, cin=None):
+            """Data gradient with B = the packed dgrad weight w ([N][K]); A = dY (3x3 / sub-pixel:
+            through the implicit im2col, kh x kw taps of cin channels). x3 mode: x3d on w re-ordered
+            to the x3p k order and split (CAPMI_FT_DGRAD_X3D / CAPMI_FT_DGRAD1_X3D for the 1x1s)."""
+            n, kd = prob.N, prob.K
+            conv = kh * kw > 1 or cin is not None
+            amode = AC if conv else AK
+            use = (x3d if conv else x3d1) and kd % 32 == 0 and (not conv or cin % 32 == 0)
+            if not use:
+                return run(tag, flops, prob, amode, BW)
+            src = w[:n * kd].view(n, kd)
+            if kh * kw > 1:
+                word[:n * kd].view(n, kd).copy_(K.conv_weight_order_x3p(src, kh, kw, cin))
+                src = word[:n * kd]
+            K.split3_bf16(src, w3[:3 * n * kd])
+            prob.B = w3.data_ptr()
+            launch = lambda: K.gemm_x3d(prob, amode, self.r._ws["sk"])  # noqa: E731
+            if hook is None:
+                launch()
+            else:
+                hook(tag, flops, launch, K.gemm_x3d_kernel_name(prob, amode))
+
         K.adaptive_avgpool_bwd_nhwc(dfeat.contiguous(), N, stt["H"], stt["W"], stt["C"], stt["OH"], stt["OW"],
                                     dA[0])
         cur = 0
@@ -795,8 +827,8 @@ class FineTuneRunner:
                               in_shift=b2), AMM, BCONV)
             da2 = dmid[:r3 * wd]
             K.conv_weight_pack_dgrad(c3.weight.detach(), wt[:Cout * wd])
-            run(tag + ".conv3.dgrad", 2.0 * r3 * Cout * wd,
-                K.problem(r3, wd, Cout, dy3, Cout, wt, Cout, da2, wd), AK, BW)
+            run_dgrad(tag + ".conv3.dgrad", 2.0 * r3 * Cout * wd,
+                      K.problem(r3, wd, Cout, dy3, Cout, wt, Cout, da2, wd), wt)
             # ---- bn2 + relu
             bn2 = blk.bn2
             K.bn_bwd_reduce(K.BNB_RELU_Y, da2, b["y2"], None, s2, b2, bn2.weight, m2[0], m2[1], bn2.eps, r3, wd,
@@ -814,8 +846,8 @@ class FineTuneRunner:
             if s == 1:
                 K.conv_weight_pack_dgrad(c2.weight.detach().contiguous(), wdg[:wd * 9 * wd])
                 geod = dict(N=N, H=H, W=W, Cin=wd, KH=3, KW=3, stride=1, pad=1, Ho=H, Wo=W)
-                run(tag + ".conv2.dgrad", 2.0 * r3 * wd * 9 * wd,
-                    K.problem(r1, wd, 9 * wd, da2, 0, wdg, 9 * wd, da1, wd, conv=geod), AC, BW)
+                run_dgrad(tag + ".conv2.dgrad", 2.0 * r3 * wd * 9 * wd,
+                          K.problem(r1, wd, 9 * wd, da2, 0, wdg, 9 * wd, da1, wd, conv=geod), wdg, 3, 3, wd)
             else:
                 # sub-pixel form: input pixel (2i+ph, 2j+pw) is a (ph+1)x(pw+1) stride-1 pad-0 conv of
                 # dY (9 taps over the 4 classes, vs 36 on a zero-upsampled grid); the class's rows
@@ -827,9 +859,9 @@ class FineTuneRunner:
                         kk = th * tw * wd
                         K.conv_weight_pack_dgrad_s2(c2.weight.detach().contiguous(), ph, pw, wdg[:wd * kk])
                         geoc = dict(N=N, H=H2, W=W2, Cin=wd, KH=th, KW=tw, stride=1, pad=0, Ho=H2, Wo=W2)
-                        run(tag + f".conv2.dgrad.p{ph}{pw}", 2.0 * r3 * wd * kk,
-                            K.problem(r3, wd, kk, da2, 0, wdg, kk, da1[(ph * W + pw) * wd:], 2 * wd, conv=geoc,
-                                      c_r1=W2, c_s2=2 * W * wd), AC, BW)
+                        run_dgrad(tag + f".conv2.dgrad.p{ph}{pw}", 2.0 * r3 * wd * kk,
+                                  K.problem(r3, wd, kk, da2, 0, wdg, kk, da1[(ph * W + pw) * wd:], 2 * wd,
+                                            conv=geoc, c_r1=W2, c_s2=2 * W * wd), wdg, th, tw, wd)
             # ---- bn1 + relu
             bn1 = blk.bn1
             K.bn_bwd_reduce(K.BNB_RELU_Y, da1, b["y1"], None, s1, b1, bn1.weight, m1[0], m1[1], bn1.eps, r1, wd,
@@ -842,9 +874,8 @@ class FineTuneRunner:
                     K.problem(wd, Cin, r1, da1, wd, b["x"], Cin, G(c1.weight), Cin), AMM, BKR)
             if need_dx:
                 K.conv_weight_pack_dgrad(c1.weight.detach(), wt[:wd * Cin])
-                run(tag + ".conv1.dgrad", 2.0 * r1 * wd * Cin,
-                    K.problem(r1, Cin, wd, da1, wd, wt, wd, dx, Cin, beta=1.0 if ds is None else 0.0),
-                    AK, BW)
+                run_dgrad(tag + ".conv1.dgrad", 2.0 * r1 * wd * Cin,
+                          K.problem(r1, Cin, wd, da1, wd, wt, wd, dx, Cin, beta=1.0 if ds is None else 0.0), wt)
             # ---- downsample (1x1, stride s) on x
             if ds is not None:
                 cd = ds[0]
@@ -856,9 +887,8 @@ class FineTuneRunner:
                     # dX[n, s*i, s*j, :] += dYd[n, i, j, :] W_d  (rows (n, i, j) -> strided NHWC rows)
                     rm = dict(c_r1=W2, c_s2=s * W * Cin) if s > 1 else {}
                     K.conv_weight_pack_dgrad(cd.weight.detach(), wt[:Cout * Cin])
-                    run(tag + ".downsample.dgrad", 2.0 * r3 * Cout * Cin,
-                        K.problem(r3, Cin, Cout, dyd, Cout, wt, Cout, dx, s * Cin, beta=1.0, **rm),
-                        AK, BW)
+                    run_dgrad(tag + ".downsample.dgrad", 2.0 * r3 * Cout * Cin,
+                              K.problem(r3, Cin, Cout, dyd, Cout, wt, Cout, dx, s * Cin, beta=1.0, **rm), wt)
             cur ^= 1
         self.state = None
 
