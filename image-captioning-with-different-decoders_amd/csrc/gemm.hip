@@ -608,6 +608,16 @@ bool x3_wgrad_wide() {
   }();
   return on;
 }
+// the encoder-sized three-term GEMMs that keep the fp32 tile rule instead of 64x64 (bit mask, A/B
+// measurement; CAPMI_X3_KEEP_TILE): 1 the 1x1 weight gradients (k rows, K >= 8192 output pixels),
+// 2 the 1x1 data gradients (M >= 8192 output pixels). The decoder's GEMMs stay below both bounds.
+int x3_keep_tile() {
+  static const int m = [] {
+    const char* e = getenv("CAPMI_X3_KEEP_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
+}
 // the launch capmi_gemm_sk makes for a problem (shared by the launcher and the plan query)
 int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, int terms, GemmPlan& g, bool& sk) {
   const bool bf16 = terms > 0;
@@ -626,7 +636,10 @@ int sk_decide(const capmi_gemm_problem* prob, int amode, int bmode, int tile, in
     tile = (prob->M >= 256 && prob->N >= 2048) ? CAPMI_TILE_128 : CAPMI_TILE_128x64;
   // three-term split staging: 64x64 everywhere (two workgroups per CU; the larger tiles hold one:
   // tools/dec_gemm_ab.py --tile, 5-20 % faster on every decoder GEMM at 64x64)
-  if (automatic && terms == 3 && !(bmode == CAPMI_B_CONV_NHWC && x3_wgrad_wide())) tile = CAPMI_TILE_64;
+  const bool keep = (bmode == CAPMI_B_CONV_NHWC && x3_wgrad_wide()) ||
+                    ((x3_keep_tile() & 1) && amode == CAPMI_A_MMAJOR && bmode == CAPMI_B_KROWS && prob->K >= 8192) ||
+                    ((x3_keep_tile() & 2) && amode == CAPMI_A_KMAJOR && bmode == CAPMI_B_NMAJOR_W && prob->M >= 8192);
+  if (automatic && terms == 3 && !keep) tile = CAPMI_TILE_64;
   int rc = gemm_plan(prob, 1, amode, bmode, tile, g);
   if (rc) return rc;
   // the 512-thread 128x128 form (tools/w8_ab.sh over all 19 encoder conv shapes, batch 64):
