@@ -406,6 +406,18 @@ def conv_weight_pack_dgrad_s2(w, ph, pw, out):
     call("capmi_conv_weight_pack_dgrad_s2", ptr(w), co, ci, int(ph), int(pw), ptr(out), stream())
 
 
+def conv_weight_pack_dgrad_x3(w, out, ph=-1, pw=-1):
+    """The dgrad weight pack (ph < 0: conv_weight_pack_dgrad; else the sub-pixel class (ph, pw) of
+    conv_weight_pack_dgrad_s2) in the x3p conv k order, split into out bf16 [3][Cin][T * Cout]
+    (the x3d B operand; == split3_bf16(conv_weight_order_x3p(pack)))."""
+    _cuda(w)
+    _cuda(out, dtype=torch.bfloat16)
+    co, ci, kh, kw = w.shape
+    taps = kh * kw if ph < 0 else (ph + 1) * (pw + 1)
+    assert w.is_contiguous() and co % 32 == 0 and out.numel() >= 3 * taps * co * ci
+    call("capmi_conv_weight_pack_dgrad_x3", ptr(w), co, ci, kh, kw, int(ph), int(pw), ptr(out), stream())
+
+
 def conv_weight_unpack(packed, shape, out):
     """[Cout][KH][KW][Cin] -> out [Cout][Cin][KH][KW] (``shape`` = nn.Conv2d weight shape)"""
     _cuda(packed, out)

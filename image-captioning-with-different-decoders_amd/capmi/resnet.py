@@ -594,6 +594,8 @@ _FT_WGRAD_X3 = os.environ.get("CAPMI_FT_WGRAD_X3", "1") != "0"
 # x3 mode: 3x3 / sub-pixel data gradients on x3d (dY split in registers x the x3p-ordered split of
 # the packed dgrad weight, re-split every step) instead of the split-staging nts form
 _FT_DGRAD_X3D = os.environ.get("CAPMI_FT_DGRAD_X3D", "1") != "0"
+# the 3x3 dgrad weight packed, ordered and split in one kernel (0: three passes, A/B)
+_FT_PACK_X3 = os.environ.get("CAPMI_FT_PACK_X3", "1") != "0"
 _FT_DGRAD1_X3D = os.environ.get("CAPMI_FT_DGRAD1_X3D", "0") != "0"  # 1x1 dgrads: neutral (1666 both), off
 
 
@@ -771,21 +773,31 @@ class FineTuneRunner:
             word = gp("w_dgrad_ord", max(wmax, w1max), dev)
             w3 = gp("w_dgrad_x3", 3 * max(wmax, w1max), dev, dtype=torch.bfloat16)
 
-        def run_dgrad(tag, flops, prob, w, kh=1, kw=1, cin=None):
+        def run_dgrad(tag, flops, prob, w, kh=1, kw=1, cin=None, conv_w=None, ph=-1, pw=-1):
             """Data gradient with B = the packed dgrad weight w ([N][K]); A = dY (3x3 / sub-pixel:
             through the implicit im2col, kh x kw taps of cin channels). x3 mode: x3d on w re-ordered
-            to the x3p k order and split (CAPMI_FT_DGRAD_X3D / CAPMI_FT_DGRAD1_X3D for the 1x1s)."""
+            to the x3p k order and split (CAPMI_FT_DGRAD_X3D / CAPMI_FT_DGRAD1_X3D for the 1x1s); for
+            a 3x3 conv_w (the nn.Conv2d weight) is packed, ordered and split in one pass instead."""
             n, kd = prob.N, prob.K
             conv = kh * kw > 1 or cin is not None
             amode = AC if conv else AK
             use = (x3d if conv else x3d1) and kd % 32 == 0 and (not conv or cin % 32 == 0)
+            if conv_w is not None and not (use and _FT_PACK_X3):  # the fp32 pack
+                if ph < 0:
+                    K.conv_weight_pack_dgrad(conv_w, w[:n * kd])
+                else:
+                    K.conv_weight_pack_dgrad_s2(conv_w, ph, pw, w[:n * kd])
+                conv_w = None
             if not use:
                 return run(tag, flops, prob, amode, BW)
-            src = w[:n * kd].view(n, kd)
-            if kh * kw > 1:
-                word[:n * kd].view(n, kd).copy_(K.conv_weight_order_x3p(src, kh, kw, cin))
-                src = word[:n * kd]
-            K.split3_bf16(src, w3[:3 * n * kd])
+            if conv_w is not None:
+                K.conv_weight_pack_dgrad_x3(conv_w, w3[:3 * n * kd], ph, pw)
+            else:
+                src = w[:n * kd].view(n, kd)
+                if kh * kw > 1:
+                    word[:n * kd].view(n, kd).copy_(K.conv_weight_order_x3p(src, kh, kw, cin))
+                    src = word[:n * kd]
+                K.split3_bf16(src, w3[:3 * n * kd])
             prob.B = w3.data_ptr()
             launch = lambda: K.gemm_x3d(prob, amode, self.r._ws["sk"])  # noqa: E731
             if hook is None:
@@ -844,10 +856,10 @@ class FineTuneRunner:
                 K.conv_weight_unpack(dwp, tuple(c2.weight.shape), G(c2.weight))
             da1 = dy3[:r1 * wd]  # dy3 is consumed
             if s == 1:
-                K.conv_weight_pack_dgrad(c2.weight.detach().contiguous(), wdg[:wd * 9 * wd])
                 geod = dict(N=N, H=H, W=W, Cin=wd, KH=3, KW=3, stride=1, pad=1, Ho=H, Wo=W)
                 run_dgrad(tag + ".conv2.dgrad", 2.0 * r3 * wd * 9 * wd,
-                          K.problem(r1, wd, 9 * wd, da2, 0, wdg, 9 * wd, da1, wd, conv=geod), wdg, 3, 3, wd)
+                          K.problem(r1, wd, 9 * wd, da2, 0, wdg, 9 * wd, da1, wd, conv=geod), wdg, 3, 3, wd,
+                          conv_w=c2.weight.detach().contiguous())
             else:
                 # sub-pixel form: input pixel (2i+ph, 2j+pw) is a (ph+1)x(pw+1) stride-1 pad-0 conv of
                 # dY (9 taps over the 4 classes, vs 36 on a zero-upsampled grid); the class's rows
@@ -857,11 +869,11 @@ class FineTuneRunner:
                     for pw in (0, 1):
                         th, tw = ph + 1, pw + 1
                         kk = th * tw * wd
-                        K.conv_weight_pack_dgrad_s2(c2.weight.detach().contiguous(), ph, pw, wdg[:wd * kk])
                         geoc = dict(N=N, H=H2, W=W2, Cin=wd, KH=th, KW=tw, stride=1, pad=0, Ho=H2, Wo=W2)
                         run_dgrad(tag + f".conv2.dgrad.p{ph}{pw}", 2.0 * r3 * wd * kk,
                                   K.problem(r3, wd, kk, da2, 0, wdg, kk, da1[(ph * W + pw) * wd:], 2 * wd,
-                                            conv=geoc, c_r1=W2, c_s2=2 * W * wd), wdg, th, tw, wd)
+                                            conv=geoc, c_r1=W2, c_s2=2 * W * wd), wdg, th, tw, wd,
+                                  conv_w=c2.weight.detach().contiguous(), ph=ph, pw=pw)
             # ---- bn1 + relu
             bn1 = blk.bn1
             K.bn_bwd_reduce(K.BNB_RELU_Y, da1, b["y1"], None, s1, b1, bn1.weight, m1[0], m1[1], bn1.eps, r1, wd,

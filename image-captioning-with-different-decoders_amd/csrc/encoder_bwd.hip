@@ -76,6 +76,53 @@ extern "C" int capmi_conv_weight_pack_dgrad_s2(const float* w, int Cout, int Cin
   return 0;
 }
 
+// The two packs above, re-ordered to the x3p conv k order and split, in one pass: the B operand of
+// the x3d data gradient (CAPMI_GEMM_X3D), three bf16 planes out[3][Cin][T*Cout] (T = the taps of the
+// dgrad conv) with k = ((co / 32) * T + tap) * 32 + co % 32 (gemm_x3p.hip: the taps of one
+// 32-channel slice consecutive) and the exact three-term split of split3_bf16. ph < 0: the full
+// flipped KHxKW kernel (stride 1); ph, pw in {0, 1}: the sub-pixel class of a 3x3 / stride-2 conv.
+__global__ void conv_weight_pack_dgrad_x3_kernel(const float* __restrict__ w, int Cout, int Cin, int KH, int KW,
+                                                 int ph, int pw, __bf16* __restrict__ out) {
+  const int TH = ph < 0 ? KH : ph + 1, TW = ph < 0 ? KW : pw + 1, T = TH * TW;
+  const long long K = (long long)T * Cout, n = (long long)Cin * K;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int ci = (int)(i / K);
+    const int j = (int)(i - (long long)ci * K);
+    const int slice = j / (T * 32), rem = j - slice * T * 32;
+    const int tap = rem >> 5, co = slice * 32 + (rem & 31);
+    const int th = tap / TW, tw = tap - th * TW;
+    int kh, kw;
+    if (ph < 0) {
+      kh = KH - 1 - th;
+      kw = KW - 1 - tw;
+    } else {
+      kh = ph ? 2 - 2 * th : 1;
+      kw = pw ? 2 - 2 * tw : 1;
+    }
+    const float x = w[(((long long)co * Cin + ci) * KH + kh) * KW + kw];
+    const __bf16 h0 = (__bf16)x;
+    const float r1 = x - (float)h0;
+    const __bf16 h1 = (__bf16)r1;
+    out[i] = h0;
+    out[n + i] = h1;
+    out[2 * n + i] = (__bf16)(r1 - (float)h1);
+  }
+}
+
+extern "C" int capmi_conv_weight_pack_dgrad_x3(const float* w, int Cout, int Cin, int KH, int KW, int ph, int pw,
+                                               void* out, void* stream) {
+  CAPMI_REQUIRE(w && out && Cout > 0 && Cin > 0 && KH > 0 && KW > 0 && Cout % 32 == 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE(ph < 0 || (KH == 3 && KW == 3 && (ph == 0 || ph == 1) && (pw == 0 || pw == 1)), CAPMI_EINVAL);
+  const long long T = ph < 0 ? (long long)KH * KW : (long long)(ph + 1) * (pw + 1);
+  const long long n = T * Cout * Cin;
+  CAPMI_REQUIRE(3 * n < (1LL << 31), CAPMI_ERANGE);
+  hipLaunchKernelGGL(conv_weight_pack_dgrad_x3_kernel, dim3(std::min<long long>(cdiv(n, 256), 8192)), dim3(256),
+                     0, as_stream(stream), w, Cout, Cin, KH, KW, ph, pw, static_cast<__bf16*>(out));
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
 // out[co][ci][kh][kw] (= nn.Conv2d weight layout) from the GEMM layout g[co][kh][kw][ci]
 __global__ void conv_weight_unpack_kernel(const float* __restrict__ g, int Cout, int Cin, int KH, int KW,
                                           float* __restrict__ out) {

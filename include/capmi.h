@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 14
+#define CAPMI_ABI_VERSION 15
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -250,6 +250,13 @@ int capmi_conv_weight_pack_dgrad(const float* w, int Cout, int Cin, int KH, int 
  * data gradient is a (ph+1)x(pw+1) stride-1 pad-0 conv over dY written to rows (2i+ph, 2j+pw)
  * (sub-pixel form: 9 taps in total over the 4 classes instead of 36 on the zero-upsampled grid). */
 int capmi_conv_weight_pack_dgrad_s2(const float* w, int Cout, int Cin, int ph, int pw, float* out, void* stream);
+/* The two packs above in the x3p conv k order, split exactly into three bf16 planes (ABI 15): the B
+ * operand of the CAPMI_GEMM_X3D data gradient. out[3][Cin][T*Cout] bf16, k = ((co/32)*T + tap)*32 +
+ * co%32 with tap = th*TW + tw over the T = TH*TW taps; ph < 0: the flipped KHxKW kernel of
+ * capmi_conv_weight_pack_dgrad, else parity class (ph, pw) of capmi_conv_weight_pack_dgrad_s2
+ * (KH = KW = 3). Cout % 32 == 0. */
+int capmi_conv_weight_pack_dgrad_x3(const float* w, int Cout, int Cin, int KH, int KW, int ph, int pw, void* out,
+                                    void* stream);
 /* [Cout][KH][KW][Cin] (GEMM layout of a weight gradient) -> [Cout][Cin][KH][KW] (nn.Conv2d layout) */
 int capmi_conv_weight_unpack(const float* packed, int Cout, int Cin, int KH, int KW, float* out, void* stream);
 /* out (N,H,W,C) = dy (N,Ho,Wo,C) at even (h, w), zero elsewhere (stride-2 conv data gradient) */
