@@ -596,6 +596,8 @@ _FT_WGRAD_X3 = os.environ.get("CAPMI_FT_WGRAD_X3", "1") != "0"
 _FT_DGRAD_X3D = os.environ.get("CAPMI_FT_DGRAD_X3D", "1") != "0"
 # the 3x3 dgrad weight packed, ordered and split in one kernel (0: three passes, A/B)
 _FT_PACK_X3 = os.environ.get("CAPMI_FT_PACK_X3", "1") != "0"
+# 1x1 dgrads read the weight itself as k rows (CAPMI_B_KROWS) instead of a per-step transposed pack
+_FT_DGRAD1_KROWS = os.environ.get("CAPMI_FT_DGRAD1_KROWS", "0") != "0"
 _FT_DGRAD1_X3D = os.environ.get("CAPMI_FT_DGRAD1_X3D", "0") != "0"  # 1x1 dgrads: neutral (1666 both), off
 
 
@@ -718,6 +720,8 @@ class FineTuneRunner:
             return 0
         if bmode == CAPMI_B_NMAJOR_W and amode in (CAPMI_A_KMAJOR, CAPMI_A_CONV_NHWC) and not prob.in_scale:
             return CAPMI_GEMM_SPLIT3
+        if bmode == CAPMI_B_KROWS and amode == CAPMI_A_KMAJOR:  # 1x1 dgrads on the weight itself
+            return CAPMI_GEMM_SPLIT3
         if amode == CAPMI_A_MMAJOR and bmode in (CAPMI_B_KROWS, CAPMI_B_CONV_NHWC) and _FT_WGRAD_X3:
             # weight gradients dY^T X: on a materialised input (k rows) or the implicit im2col of the
             # saved pre-BN output with the BN-apply + ReLU prologue
@@ -838,9 +842,13 @@ class FineTuneRunner:
                     K.problem(Cout, wd, r3, dy3, Cout, b["y2"], 0, G(c3.weight), wd, conv=geo3, in_scale=s2,
                               in_shift=b2), AMM, BCONV)
             da2 = dmid[:r3 * wd]
-            K.conv_weight_pack_dgrad(c3.weight.detach(), wt[:Cout * wd])
-            run_dgrad(tag + ".conv3.dgrad", 2.0 * r3 * Cout * wd,
-                      K.problem(r3, wd, Cout, dy3, Cout, wt, Cout, da2, wd), wt)
+            if _FT_DGRAD1_KROWS:
+                run(tag + ".conv3.dgrad", 2.0 * r3 * Cout * wd,
+                    K.problem(r3, wd, Cout, dy3, Cout, c3.weight.detach(), wd, da2, wd), AK, BKR)
+            else:
+                K.conv_weight_pack_dgrad(c3.weight.detach(), wt[:Cout * wd])
+                run_dgrad(tag + ".conv3.dgrad", 2.0 * r3 * Cout * wd,
+                          K.problem(r3, wd, Cout, dy3, Cout, wt, Cout, da2, wd), wt)
             # ---- bn2 + relu
             bn2 = blk.bn2
             K.bn_bwd_reduce(K.BNB_RELU_Y, da2, b["y2"], None, s2, b2, bn2.weight, m2[0], m2[1], bn2.eps, r3, wd,
@@ -885,9 +893,14 @@ class FineTuneRunner:
                 run(tag + ".conv1.wgrad", 2.0 * r1 * wd * Cin,
                     K.problem(wd, Cin, r1, da1, wd, b["x"], Cin, G(c1.weight), Cin), AMM, BKR)
             if need_dx:
-                K.conv_weight_pack_dgrad(c1.weight.detach(), wt[:wd * Cin])
-                run_dgrad(tag + ".conv1.dgrad", 2.0 * r1 * wd * Cin,
-                          K.problem(r1, Cin, wd, da1, wd, wt, wd, dx, Cin, beta=1.0 if ds is None else 0.0), wt)
+                if _FT_DGRAD1_KROWS:
+                    run(tag + ".conv1.dgrad", 2.0 * r1 * wd * Cin,
+                        K.problem(r1, Cin, wd, da1, wd, c1.weight.detach(), Cin, dx, Cin,
+                                  beta=1.0 if ds is None else 0.0), AK, BKR)
+                else:
+                    K.conv_weight_pack_dgrad(c1.weight.detach(), wt[:wd * Cin])
+                    run_dgrad(tag + ".conv1.dgrad", 2.0 * r1 * wd * Cin,
+                              K.problem(r1, Cin, wd, da1, wd, wt, wd, dx, Cin, beta=1.0 if ds is None else 0.0), wt)
             # ---- downsample (1x1, stride s) on x
             if ds is not None:
                 cd = ds[0]
@@ -898,9 +911,14 @@ class FineTuneRunner:
                 if need_dx:
                     # dX[n, s*i, s*j, :] += dYd[n, i, j, :] W_d  (rows (n, i, j) -> strided NHWC rows)
                     rm = dict(c_r1=W2, c_s2=s * W * Cin) if s > 1 else {}
-                    K.conv_weight_pack_dgrad(cd.weight.detach(), wt[:Cout * Cin])
-                    run_dgrad(tag + ".downsample.dgrad", 2.0 * r3 * Cout * Cin,
-                              K.problem(r3, Cin, Cout, dyd, Cout, wt, Cout, dx, s * Cin, beta=1.0, **rm), wt)
+                    if _FT_DGRAD1_KROWS:
+                        run(tag + ".downsample.dgrad", 2.0 * r3 * Cout * Cin,
+                            K.problem(r3, Cin, Cout, dyd, Cout, cd.weight.detach(), Cin, dx, s * Cin, beta=1.0, **rm),
+                            AK, BKR)
+                    else:
+                        K.conv_weight_pack_dgrad(cd.weight.detach(), wt[:Cout * Cin])
+                        run_dgrad(tag + ".downsample.dgrad", 2.0 * r3 * Cout * Cin,
+                                  K.problem(r3, Cin, Cout, dyd, Cout, wt, Cout, dx, s * Cin, beta=1.0, **rm), wt)
             cur ^= 1
         self.state = None
 
