@@ -55,6 +55,51 @@ def finetune_train_step(resnet_params, dec_params, dec_trainable, imgs, captions
                 dec_new=dec_new, net=net)
 
 
+def _relu_at(z, name, masks, record, pre=None):
+    """ReLU whose 0/1 mask is ``masks[name]`` when given (else z > 0); the mask taken is recorded.
+    z * mask has the same value and the same gradient as torch.relu(z) under that mask
+    (threshold_backward passes the gradient where z > 0)."""
+    m = masks[name] if masks is not None else (z.detach() > 0)
+    if record is not None:
+        record[name] = m
+    if pre is not None:
+        pre[name] = z.detach().clone()
+    return z * m.to(z.dtype)
+
+
+def encoder_backward_masked(resnet_params, imgs, dfeat, dtype=torch.float64, layers=(3, 4, 23, 3), masks=None,
+                            record=None, pre=None):
+    """encoder_backward with the ReLUs of the trainable blocks (layer2-4: after bn1, after bn2, and the
+    block output relu(bn3(y3) + identity), models/encoder.py:90-91 via torchvision's Bottleneck) taken
+    on a GIVEN branch: ``masks[f"{layer}.{block}.relu{1,2,3}"]`` (bool, NCHW). ``record`` receives the
+    masks this forward used (its own sign tests when ``masks`` is None), ``pre`` the pre-activations.
+
+    Why: the encoder is piecewise linear in its ReLUs. An fp32 forward whose error is at rounding
+    level still lands some pre-activation within that error of 0 on the other side of it, and each
+    such flip moves the gradient by a full element of the upstream gradient -- a discrete event
+    that no arithmetic tolerance describes. Differentiating the fp64 forward on the fp32 run's own
+    branch compares the two on the same piecewise-linear function, where the gradient IS a
+    continuous function of the arithmetic (the flips themselves are counted separately)."""
+    net = build_resnet101(resnet_params, layers).to(dtype)
+    net.train()
+    names = trainable_names(net)
+    for n, q in net.named_parameters():
+        q.requires_grad_(n in names)
+    x = net.maxpool(net.relu(net.bn1(net.conv1(imgs.to(dtype)))))
+    x = net.layer1(x)
+    for li in (2, 3, 4):
+        for bi, blk in enumerate(getattr(net, f"layer{li}")):
+            tag = f"layer{li}.{bi}"
+            idt = x if blk.downsample is None else blk.downsample(x)
+            a1 = _relu_at(blk.bn1(blk.conv1(x)), tag + ".relu1", masks, record, pre)
+            a2 = _relu_at(blk.bn2(blk.conv2(a1)), tag + ".relu2", masks, record, pre)
+            x = _relu_at(blk.bn3(blk.conv3(a2)) + idt, tag + ".relu3", masks, record, pre)
+    feats = torch.nn.functional.adaptive_avg_pool2d(x, (14, 14)).permute(0, 2, 3, 1)
+    feats.backward(dfeat.to(dtype))
+    named = dict(net.named_parameters())
+    return feats.detach(), {n: named[n].grad.detach().clone() for n in names}, net
+
+
 def encoder_backward(resnet_params, imgs, dfeat, dtype=torch.float64, layers=(3, 4, 23, 3)):
     """Encoder-only: features and d(<features, dfeat>)/d(layer2-4 params) by autograd
     (``layers``: blocks per stage; shallower stacks are better conditioned in train-mode BN)."""

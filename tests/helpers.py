@@ -34,6 +34,32 @@ def rel_err(a, b):
     return float((a - b).norm() / max(b.norm(), 1e-30))
 
 
+def ft_relu_masks(ft):
+    """The ReLU branch a capmi fine-tune forward took in every trainable block (FineTuneRunner.state,
+    read after forward, before backward), keyed as oracle.finetune_ref.encoder_backward_masked
+    expects: relu1 / relu2 = [fma(y, scale, shift) > 0] (the sign of the exact value, which fp64
+    y*s + b preserves; the backward kernels' own mask), relu3 = [out > 0] of the saved block output."""
+    masks = {}
+    N = ft.state["N"]
+    for b in ft.state["blocks"]:
+        H, W, H2, W2, wd, Co = b["H"], b["W"], b["H2"], b["W2"], b["wd"], b["Cout"]
+
+        def nchw(x, h, w, c):
+            return x[: N * h * w * c].view(N, h, w, c).permute(0, 3, 1, 2).double().cpu()
+
+        (s1, b1, _), (s2, b2, _) = b["ss"][0], b["ss"][1]
+        v = lambda a: a.detach().double().cpu().view(1, -1, 1, 1)  # noqa: E731
+        masks[b["tag"] + ".relu1"] = nchw(b["y1"], H, W, wd) * v(s1) + v(b1) > 0
+        masks[b["tag"] + ".relu2"] = nchw(b["y2"], H2, W2, wd) * v(s2) + v(b2) > 0
+        masks[b["tag"] + ".relu3"] = nchw(b["out"], H2, W2, Co) > 0
+    return masks
+
+
+def mask_flips(got, ref):
+    """Number of elements where two ReLU branches disagree, over all masks."""
+    return sum(int((got[k] != ref[k]).sum()) for k in ref)
+
+
 def assert_close(a, b, rtol, atol, what=""):
     a = a.detach().double().cpu()
     b = b.detach().double().cpu()

@@ -223,3 +223,31 @@ def test_beam_search(golden, tag):
     assert seq == fx["seq"].tolist()
     np.testing.assert_allclose(np.array(alphas, dtype=np.float32).reshape(fx["alphas"].shape), fx["alphas"],
                                rtol=1e-5, atol=1e-7)
+
+
+def test_encoder_backward_masked_is_autograd_on_a_branch():
+    """oracle.finetune_ref.encoder_backward_masked: with no masks it IS the plain fp64 autograd of the
+    encoder (same features and gradients as encoder_backward); on its own recorded branch it gives the
+    same again; on a branch with one ReLU decision flipped, only that decision's effect changes."""
+    from oracle.finetune_ref import encoder_backward, encoder_backward_masked
+    layers, seed = (1, 1, 1, 1), 5
+    params = gen.resnet101_params(seed, layers)
+    imgs = torch.from_numpy(gen.images(seed, 2, 64, 64))
+    g = torch.Generator().manual_seed(3)
+    dfeat = torch.rand((2, 14, 14, 2048), generator=g, dtype=torch.float64) * 2 - 1
+    f0, g0, _ = encoder_backward(params, imgs, dfeat, torch.float64, layers)
+    rec, pre = {}, {}
+    f1, g1, _ = encoder_backward_masked(params, imgs, dfeat, torch.float64, layers, record=rec, pre=pre)
+    assert torch.equal(f0, f1) and all(torch.equal(g0[k], g1[k]) for k in g0)
+    assert set(rec) == {f"layer{i}.0.relu{j}" for i in (2, 3, 4) for j in (1, 2, 3)}
+    _, g2, _ = encoder_backward_masked(params, imgs, dfeat, torch.float64, layers, masks=rec)
+    assert all(torch.equal(g0[k], g2[k]) for k in g0)
+    flipped = {k: v.clone() for k, v in rec.items()}
+    z = pre["layer3.0.relu2"]
+    i = int(z.abs().reshape(-1).argmin())  # the decision closest to 0: flip it
+    flipped["layer3.0.relu2"].view(-1)[i] ^= True
+    _, g3, _ = encoder_backward_masked(params, imgs, dfeat, torch.float64, layers, masks=flipped)
+    rel = {k: float((g3[k] - g0[k]).norm() / g0[k].norm()) for k in g0}
+    # the forward moves by the flipped element's tiny value (layer4 barely changes); the gradients
+    # routed through that decision move by a whole upstream element
+    assert max(v for k, v in rel.items() if k.startswith("layer4")) < 1e-3 * rel["layer3.0.bn2.bias"], rel
