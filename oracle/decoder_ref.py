@@ -18,12 +18,15 @@ def _lin(x, p, name):
     return F.linear(x, p[name + ".weight"], p[name + ".bias"])
 
 
-def soft_attention(p, encoder_out, decoder_hidden, prefix="attention."):
-    """models/attention.py:43-61."""
+def soft_attention(p, encoder_out, decoder_hidden, prefix="attention.", mask=None):
+    """models/attention.py:43-61. ``mask`` (B, P, A bool, optional): take the score ReLU on that branch
+    (z * mask: torch.relu's value and gradient when mask = z > 0) -- the GPU run's own decisions, so a
+    pre-activation within rounding of 0 compares on the same piecewise-linear function."""
     att_enc = _lin(encoder_out, p, prefix + "enc_att")                     # :54
     att_dec = _lin(decoder_hidden, p, prefix + "dec_att")                  # :55
-    att = _lin(torch.relu(att_enc + att_dec.unsqueeze(1)), p,
-               prefix + "full_att").squeeze(2)                             # :56-57 (ReLU, not tanh)
+    z = att_enc + att_dec.unsqueeze(1)
+    act = torch.relu(z) if mask is None else z * mask.to(z.dtype)
+    att = _lin(act, p, prefix + "full_att").squeeze(2)                     # :56-57 (ReLU, not tanh)
     alpha = torch.softmax(att, dim=1)                                      # :58
     awe = (encoder_out * alpha.unsqueeze(2)).sum(dim=1)                   # :59-60
     return awe, alpha
@@ -45,12 +48,13 @@ def lstm_cell(x, h, c, p):
 
 
 def decoder_forward(p, encoder_out, encoded_captions, caption_lengths, dropout_p=0.0,
-                    dropout_masks=None, embeddings=None):
+                    dropout_masks=None, embeddings=None, att_masks=None):
     """models/attention.py:218-284 (regular-embedding branch, :247; ``embeddings`` (B, L', M)
     given = the BERT branch, :242-244, which uses precomputed features instead of the table).
 
     ``dropout_masks`` (optional, (T,B,D) of 0/1/(1-p) scale) replaces the
-    reference's RNG-driven nn.Dropout so a GPU run's mask can be replayed."""
+    reference's RNG-driven nn.Dropout so a GPU run's mask can be replayed; ``att_masks`` (optional,
+    (T, B, P, A) bool) the attention-score ReLU decisions (soft_attention's ``mask``) per step."""
     B = encoder_out.size(0)
     E = encoder_out.size(-1)
     enc = encoder_out.reshape(B, -1, E)                                    # :230
@@ -66,7 +70,8 @@ def decoder_forward(p, encoder_out, encoded_captions, caption_lengths, dropout_p
     alphas = torch.zeros(B, T, P, dtype=wdt)                               # :257-258
     for t in range(T):                                                     # :260
         bt = sum(l > t for l in decode_lengths)                            # :261
-        awe, alpha = soft_attention(p, enc[:bt], h[:bt])                   # :267-268
+        awe, alpha = soft_attention(p, enc[:bt], h[:bt],
+                                    mask=None if att_masks is None else att_masks[t, :bt])  # :267-268
         gate = torch.sigmoid(_lin(h[:bt], p, "f_beta"))                    # :270
         awe = gate * awe                                                   # :271
         x = torch.cat([embeddings[:bt, t, :].double(), awe.double()], 1)   # :274-275
@@ -118,14 +123,15 @@ def adam_step(params, grads, state, lr=1e-4, betas=(0.9, 0.999), eps=1e-8):
 
 
 def train_step(p, trainable, encoder_out, captions, caption_lengths, alpha_c=1.0,
-               grad_clip=5.0, lr=1e-4, state=None, dropout_masks=None, embeddings=None):
+               grad_clip=5.0, lr=1e-4, state=None, dropout_masks=None, embeddings=None, att_masks=None):
     """One decoder step of models/attention.py:386-430 (dropout off unless
     masks are given). ``p``: dict of float tensors; ``trainable``: names that
     require grad (the reference's filter(requires_grad), :352-355).
     Returns (loss, predictions, alphas, grads(clamped), new_params, state)."""
     leaves = {k: (v.detach().clone().requires_grad_(k in trainable)) for k, v in p.items()}
     preds, caps, dl, alphas = decoder_forward(leaves, encoder_out, captions, caption_lengths,
-                                              dropout_masks=dropout_masks, embeddings=embeddings)
+                                              dropout_masks=dropout_masks, embeddings=embeddings,
+                                              att_masks=att_masks)
     loss = attention_loss(preds, caps, dl, alphas, alpha_c)
     loss.backward()
     raw = {k: leaves[k].grad.detach().clone() for k in trainable}

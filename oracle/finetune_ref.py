@@ -26,19 +26,23 @@ def trainable_names(net):
 
 def finetune_train_step(resnet_params, dec_params, dec_trainable, imgs, captions, caption_lengths,
                         alpha_c=1.0, grad_clip=5.0, enc_lr=1e-4, dec_lr=1e-4, dtype=torch.float32,
-                        dfeat_only=False):
+                        dfeat_only=False, masks=None, record=None, pre=None):
     """Returns dict(loss, feats, enc_raw, dec_raw, enc_new, dec_new, net) -- raw = unclamped
     gradients (what the GPU writes), new = parameters after clamp + Adam (one step).
 
     ``dtype=torch.float64`` runs the ENCODER in fp64 (the decoder keeps the reference's fp32
     LSTM input cast, Q6): the "exact" answer the fp32 paths are measured against, since
-    train-mode BatchNorm at random init is ill-conditioned."""
+    train-mode BatchNorm at random init is ill-conditioned. ``masks`` / ``record`` / ``pre``: the
+    encoder's trainable ReLUs on a given branch (encoder_backward_masked)."""
     net = build_resnet101(resnet_params).to(dtype)
     net.train()
     names = trainable_names(net)
     for n, q in net.named_parameters():
         q.requires_grad_(n in names)
-    feats = encoder_attention_forward(net, imgs.to(dtype))                    # :389 encoder(imgs)
+    if masks is None and record is None and pre is None:
+        feats = encoder_attention_forward(net, imgs.to(dtype))                # :389 encoder(imgs)
+    else:
+        feats = encoder_features_on_branch(net, imgs.to(dtype), masks, record, pre)
     leaves = {k: v.detach().clone().requires_grad_(k in dec_trainable) for k, v in dec_params.items()}
     preds, caps, dl, alphas = R.decoder_forward(leaves, feats.float() if dtype != torch.float32 else feats,
                                                 captions, caption_lengths)    # :393
@@ -67,6 +71,21 @@ def _relu_at(z, name, masks, record, pre=None):
     return z * m.to(z.dtype)
 
 
+def encoder_features_on_branch(net, imgs, masks=None, record=None, pre=None):
+    """encoder_attention_forward (models/encoder.py:97-110) with the trainable blocks' ReLUs on a given
+    branch (see encoder_backward_masked); masks/record/pre None: the plain forward."""
+    x = net.maxpool(net.relu(net.bn1(net.conv1(imgs))))
+    x = net.layer1(x)
+    for li in (2, 3, 4):
+        for bi, blk in enumerate(getattr(net, f"layer{li}")):
+            tag = f"layer{li}.{bi}"
+            idt = x if blk.downsample is None else blk.downsample(x)
+            a1 = _relu_at(blk.bn1(blk.conv1(x)), tag + ".relu1", masks, record, pre)
+            a2 = _relu_at(blk.bn2(blk.conv2(a1)), tag + ".relu2", masks, record, pre)
+            x = _relu_at(blk.bn3(blk.conv3(a2)) + idt, tag + ".relu3", masks, record, pre)
+    return torch.nn.functional.adaptive_avg_pool2d(x, (14, 14)).permute(0, 2, 3, 1)
+
+
 def encoder_backward_masked(resnet_params, imgs, dfeat, dtype=torch.float64, layers=(3, 4, 23, 3), masks=None,
                             record=None, pre=None):
     """encoder_backward with the ReLUs of the trainable blocks (layer2-4: after bn1, after bn2, and the
@@ -85,16 +104,7 @@ def encoder_backward_masked(resnet_params, imgs, dfeat, dtype=torch.float64, lay
     names = trainable_names(net)
     for n, q in net.named_parameters():
         q.requires_grad_(n in names)
-    x = net.maxpool(net.relu(net.bn1(net.conv1(imgs.to(dtype)))))
-    x = net.layer1(x)
-    for li in (2, 3, 4):
-        for bi, blk in enumerate(getattr(net, f"layer{li}")):
-            tag = f"layer{li}.{bi}"
-            idt = x if blk.downsample is None else blk.downsample(x)
-            a1 = _relu_at(blk.bn1(blk.conv1(x)), tag + ".relu1", masks, record, pre)
-            a2 = _relu_at(blk.bn2(blk.conv2(a1)), tag + ".relu2", masks, record, pre)
-            x = _relu_at(blk.bn3(blk.conv3(a2)) + idt, tag + ".relu3", masks, record, pre)
-    feats = torch.nn.functional.adaptive_avg_pool2d(x, (14, 14)).permute(0, 2, 3, 1)
+    feats = encoder_features_on_branch(net, imgs.to(dtype), masks, record, pre)
     feats.backward(dfeat.to(dtype))
     named = dict(net.named_parameters())
     return feats.detach(), {n: named[n].grad.detach().clone() for n in names}, net

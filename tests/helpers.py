@@ -55,6 +55,25 @@ def ft_relu_masks(ft):
     return masks
 
 
+def decoder_att_masks(dup=1):
+    """The attention-score ReLU decisions of the last capmi decoder forward, (T, B, P, A) bool over the
+    reference's P positions: the score kernel takes relu(ATT_ENC[b, q] + AD[t, b]) in fp32 (att_enc and
+    att_dec with their biases, both kept for the backward), whose sign the exact fp64 sum preserves.
+    dup > 1: the distinct rows q of an F x F map, expanded to the pooled (F dup)^2 positions."""
+    from capmi import decoder_fn as DF
+    ws = next(iter(DF.CORE._ws.values()))
+    ae, ad = ws.ATT_ENC.double().cpu(), ws.AD.double().cpu()
+    T, B, A = ad.shape
+    out = []
+    for t_ in range(T):
+        m = ae + ad[t_].unsqueeze(1) > 0  # (B, Q, A)
+        if dup > 1:
+            F_ = int(round(m.shape[1] ** 0.5))
+            m = m.view(B, F_, F_, A).repeat_interleave(dup, 1).repeat_interleave(dup, 2).reshape(B, -1, A)
+        out.append(m)
+    return torch.stack(out)
+
+
 def mask_flips(got, ref):
     """Number of elements where two ReLU branches disagree, over all masks."""
     return sum(int((got[k] != ref[k]).sum()) for k in ref)

@@ -1,0 +1,216 @@
+"""GPU parity of the EXACT paths bench.py times, at the bench's size (B = 64, 224x224, L = 25,
+V = 8100), through AttentionTrainStep with the bench's launch mode and precisions:
+
+* config 2 (headline): x3 encoder + x3 decoder GEMMs, pipelined two-stream HIP graphs, the decoder on
+  the 49 distinct rows of the 7x7 map (dup = 2) -- vs the oracle's reference-restated
+  step (models/attention.py:386-430) on the pooled 14x14 map of the same features;
+* config 4: glove_att (GloVe-300 fp64 table, fine-tuned) + encoder fine-tune (layer2-4), x3 forward,
+  x3 data / weight gradients, x3 decoder GEMMs, one HIP graph per step -- vs the oracle's fine-tune
+  step (oracle/finetune_ref.py, pinned by tests/golden/train_step_finetune.npz) in fp64, on the GPU
+  run's own ReLU branch (tests/test_gpu_finetune.py::_check_branch_aligned);
+* config 5: bert_attention (768-d word features), bf16 encoder, bf16 decoder GEMMs, pipelined graphs
+  -- vs the fp32 oracle on the same features, under the bf16 aggregate rules of
+  tests/test_gpu_headline_parity.py::test_decoder_step_b64_bf16_gemms.
+
+The features the step decodes are not returned by it; a second encoder with the same weights runs the
+same kernel plan (deterministic: fixed stream-K orders, no atomics) and gives them bit for bit."""
+import numpy as np
+import pytest
+import torch
+
+import gen
+from helpers import assert_close, decoder_att_masks, ft_relu_masks, make_decoder, mask_flips, rel_err, t
+from oracle import decoder_ref as R
+from test_gpu_decoder import ALPHA_ATOL, LOGIT_ATOL, LOGIT_RTOL
+from test_gpu_headline_parity import _check_grads as _dec_grad_rule
+from test_gpu_headline_parity import _encoder, _threads
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+B, L, V = 64, 25, 8100
+
+
+def _pooled(fmap, d=2):
+    """(B, 7, 7, E) -> the (B, 196, E) map AdaptiveAvgPool2d(14) gives (exact 2x replicate)."""
+    x = fmap.detach().cpu().repeat_interleave(d, 1).repeat_interleave(d, 2)
+    return x.reshape(x.shape[0], -1, x.shape[-1])
+
+
+def _adam(params):
+    from capmi.optim import Adam
+    opt = Adam([q for q in params if q.requires_grad], lr=1e-4)
+    opt.set_clip(5.0)
+    return opt
+
+
+def test_config2_headline_step_b64():
+    """AttentionTrainStep(pipeline=True, graph=True) as bench.py runs config 2 (fp32-x3 encoder,
+    fp32-x3 decoder GEMMs, dup = 2): loss rtol 1e-5 and every decoder gradient by the decoder rule
+    (tests/test_gpu_decoder.py::_grad_check, no kink rows excused) against the oracle on the pooled map,
+    taken on the GPU's own attention-ReLU decisions (helpers.decoder_att_masks). The decoder's
+    logits / alphas on the same plan: test_decoder_step_b64_matches_oracle[fp32-x3-2]; the x3 encoder
+    at B = 64 against fp64: tests/test_gpu_x3.py::test_encoder_x3_matches_oracle[64-224]."""
+    from capmi.train_step import AttentionTrainStep
+    torch.set_num_threads(_threads())
+    seed = 101
+    params = gen.resnet101_params(seed)
+    enc = _encoder(params)
+    enc.set_compute_precision("fp32-x3")
+    dec, p = make_decoder(512, 512, 512, V, seed, DEV)
+    dec.set_compute_precision("fp32-x3")
+    dec.fine_tune_embeddings(False)
+    dec.train()
+    opt = _adam(dec.parameters())
+    x = t(gen.images(seed, B), DEV)
+    caps = gen.captions(seed, B, L, V)
+    twin = _encoder(params)
+    twin.set_compute_precision("fp32-x3")
+    fmap = torch.empty(B, 7, 7, 2048, device=DEV)
+    with torch.no_grad():
+        twin.forward_into(x, fmap, pooled=False)
+    step = AttentionTrainStep(enc, dec, opt, alpha_c=1.0, pipeline=True, graph=True, seed=1)
+    assert step(x, t(caps, DEV), [L] * B) is None  # the pipelined step returns the previous batch's loss
+    assert step.replayed == ["enc0"]
+    loss = step.flush()
+    torch.cuda.synchronize()
+    trainable = [n for n, q in dec.named_parameters() if q.requires_grad]
+    grads = {n: dec.get_parameter(n).grad.detach().clone() for n in trainable}
+    rloss, _, _, rraw, _, _, _ = R.train_step(p, set(trainable), _pooled(fmap), t(caps), [L] * B,
+                                              att_masks=decoder_att_masks(2))
+    assert_close(loss.view(()), rloss, 1e-5, 1e-6, "loss")
+    _dec_grad_rule(grads, rraw, trainable, aligned=True)
+
+
+def test_config4_glove_finetune_step_b64():
+    """AttentionTrainStep(encoder_optimizer=..., graph=True) as bench.py runs config 4: GloVe-300 fp64
+    table fine-tuned, encoder layer2-4 fine-tuned, everything fp32-x3. Against the oracle fine-tune step
+    in fp64 on the GPU's own ReLU branch: loss within 2x the CPU fp32 step's error (+1e-5), encoder and
+    decoder gradients (the fp64 embedding table's included) by the branch-aligned 2x / 4x rule, and the
+    ReLU flips counted and bounded as in tests/test_gpu_finetune.py."""
+    from capmi.train_step import AttentionTrainStep
+    from oracle.finetune_ref import finetune_train_step
+    from test_gpu_finetune import _check_grads, _child_key, _ft_encoder
+    torch.set_num_threads(_threads())
+    seed, M = 103, 300
+    params = gen.resnet101_params(seed)
+    enc = _ft_encoder(params)
+    enc.set_compute_precision("fp32-x3")
+    dec, p = make_decoder(512, 512, M, V, seed, DEV, emb_dtype=np.float64)
+    dec.set_compute_precision("fp32-x3")
+    dec.fine_tune_embeddings(True)
+    dec.train()
+    assert dec.embedding.weight.dtype == torch.float64 and dec.embedding.weight.requires_grad
+    x = t(gen.images(seed, B), DEV)
+    caps = gen.captions(seed, B, L, V)
+    twin = _ft_encoder(params)
+    twin.set_compute_precision("fp32-x3")
+    twin.ft_forward(x, pooled=False)
+    torch.cuda.synchronize()
+    masks = ft_relu_masks(twin._ft())
+    twin._ft().state = None
+    del twin
+    step = AttentionTrainStep(enc, dec, _adam(dec.parameters()), encoder_optimizer=_adam(enc.parameters()),
+                              graph=True, seed=5)
+    loss = float(step(x, t(caps, DEV), [L] * B))
+    torch.cuda.synchronize()
+    assert step.replayed == ["step"]
+    named = dict(enc.named_parameters())
+    trainable = {n for n, q in dec.named_parameters() if q.requires_grad}
+    gpu_enc = {k: named[_child_key(k)].grad.detach().double().cpu() for k in named_keys(params)}
+    gpu_dec = {k: dec.get_parameter(k).grad.detach().double().cpu() for k in trainable}
+    imgs, cp = x.cpu(), t(caps)
+    m64, pre64, m32 = {}, {}, {}
+    run = lambda dtype, **kw: finetune_train_step(params, p, trainable, imgs, cp, [L] * B, dtype=dtype, **kw)  # noqa
+    o64 = run(torch.float64, record=m64, pre=pre64)
+    o32 = run(torch.float32, record=m32)
+    o64_32 = run(torch.float64, masks=m32)
+    o64_gpu = run(torch.float64, masks=masks)
+    n_gpu, n_cpu = mask_flips(masks, m64), mask_flips(m32, m64)
+    worst = max([float(pre64[k][masks[k] != m64[k]].abs().max() / pre64[k].pow(2).mean().sqrt())
+                 for k in masks if (masks[k] != m64[k]).any()] or [0.0])
+    print(f"config 4: ReLU flips gpu {n_gpu} cpu32 {n_cpu}; worst flipped |z|/rms {worst:.2g}; loss gpu {loss:.6f} "
+          f"fp64 {float(o64_gpu['loss']):.6f} cpu32 {float(o32['loss']):.6f}")
+    assert n_gpu <= 2 * n_cpu + 2 and worst <= 3e-3, (n_gpu, n_cpu, worst)
+    el = abs(loss - float(o64_gpu["loss"]))
+    ec = abs(float(o32["loss"]) - float(o64_32["loss"]))
+    assert el <= 2 * ec + 1e-5, (el, ec)
+    for what, got, g64, g32, g64_32 in (("encoder", gpu_enc, o64_gpu["enc_raw"], o32["enc_raw"], o64_32["enc_raw"]),
+                                        ("decoder", gpu_dec, o64_gpu["dec_raw"], o32["dec_raw"], o64_32["dec_raw"])):
+        keys = list(g64)
+        cat = lambda d: torch.cat([d[k].detach().double().cpu().reshape(-1) for k in keys])  # noqa: E731
+        rows = {k: (rel_err(got[k], g64[k]), rel_err(g32[k], g64_32[k])) for k in keys}
+        agg = (rel_err(cat(got), cat(g64)), rel_err(cat(g32), cat(g64_32)))
+        _check_grads(rows, agg, f"config 4 {what} grads (branch-aligned)")
+
+
+def named_keys(params):
+    """Oracle names of the trainable encoder tensors (layer2-4 weights and BN affine)."""
+    return [k for k in params if k.startswith(("layer2.", "layer3.", "layer4.")) and "running" not in k]
+
+
+def test_config5_bert_bf16_step_b64():
+    """bench.py's config 5: bf16 encoder, BERT-branch decoder (M = 768 word features) with bf16 GEMM
+    operands, pipelined graphs, dup = 2. (1) the bf16 encoder's 7x7 map at B = 64 vs the fp64 oracle
+    (train-mode BN; bn3.weight x 0.1 for conditioning, see tests/test_gpu_bf16.py) within 6e-2;
+    (2) the decoder on those features (fused_loss_and_grads, the call the step makes) vs the fp32 oracle
+    BERT branch: loss rel. 2e-3, predictions / alphas rel. L2 1e-2, gradients rel. L2 3e-2 (1e-1 for
+    the cancellation-heavy enc_att / dec_att); (3) the step itself (AttentionTrainStep, pipelined graphs):
+    the same loss and gradients as (2), to fp32 summation noise."""
+    from capmi import decoder_fn as DF
+    from capmi.train_step import AttentionTrainStep
+    from oracle.resnet_ref import build_resnet101, encoder_attention_forward
+    from test_gpu_bert import _bert_decoder
+    torch.set_num_threads(_threads())
+    seed = 105
+    params = gen.resnet101_params(seed)
+    for k in params:
+        if k.endswith("bn3.weight"):
+            params[k] = params[k] * 0.1
+    enc = _encoder(params)
+    enc.set_compute_precision("bf16")
+    dec, p = _bert_decoder(512, 512, V, seed)
+    dec.set_compute_precision("bf16")
+    dec.fine_tune_embeddings(False)
+    dec.train()
+    x = t(gen.images(seed, B), DEV)
+    caps = gen.captions(seed, B, L, V)
+    twin = _encoder(params)
+    twin.set_compute_precision("bf16")
+    fmap = torch.empty(B, 7, 7, 2048, device=DEV)
+    with torch.no_grad():
+        twin.forward_into(x, fmap, pooled=False)
+    torch.cuda.synchronize()
+    # (1) encoder
+    r64 = build_resnet101(params).double().train()
+    with torch.no_grad():
+        y64 = encoder_attention_forward(r64, x.cpu().double())
+    e = rel_err(_pooled(fmap).view(B, 14, 14, 2048), y64)
+    print(f"config 5 bf16 encoder B=64: rel L2 vs fp64 {e:.3g}")
+    assert e < 6e-2, e
+    # (2) decoder on the same plan
+    emb = dec.bert_embedder(t(caps, DEV))
+    trainable = [n for n, q in dec.named_parameters() if q.requires_grad]
+    g2 = {n: torch.zeros_like(q) for n, q in dec.named_parameters() if q.requires_grad}
+    loss2, preds, alphas = DF.fused_loss_and_grads(dec, fmap, t(caps, DEV), [L] * B, 1.0, g2, dup=2)
+    torch.cuda.synchronize()
+    rloss, rpreds, ralphas, rraw, _, _, _ = R.train_step(p, set(trainable), _pooled(fmap), t(caps), [L] * B,
+                                                         embeddings=emb.cpu())
+    assert abs(float(loss2) - float(rloss)) <= 2e-3 * abs(float(rloss)), (float(loss2), float(rloss))
+    assert rel_err(preds.cpu(), rpreds) <= 1e-2
+    assert rel_err(alphas.cpu(), ralphas) <= 1e-2
+    for n in trainable:
+        got, want = g2[n].view_as(rraw[n]).cpu(), rraw[n]
+        if n == "attention.full_att.bias":
+            assert float(got.abs().max()) < 1e-5 and float(want.abs().max()) < 1e-5, n
+            continue
+        tol = 1e-1 if n.startswith(("attention.enc_att", "attention.dec_att")) else 3e-2
+        assert rel_err(got, want) <= tol, (n, rel_err(got, want))
+    # (3) the step the bench times, on the same weights and batch
+    step = AttentionTrainStep(enc, dec, _adam(dec.parameters()), alpha_c=1.0, pipeline=True, graph=True, seed=1)
+    assert step(x, t(caps, DEV), [L] * B) is None
+    loss3 = step.flush()
+    torch.cuda.synchronize()
+    assert abs(float(loss3) - float(loss2)) <= 1e-5 * abs(float(loss2))
+    for n in trainable:
+        assert rel_err(dec.get_parameter(n).grad, g2[n]) <= 1e-5, n
+    _ = (ALPHA_ATOL, LOGIT_ATOL, LOGIT_RTOL)

@@ -16,7 +16,7 @@ import pytest
 import torch
 
 import gen
-from helpers import assert_close, make_decoder, rel_err, t
+from helpers import assert_close, decoder_att_masks, make_decoder, rel_err, t
 from oracle import decoder_ref as R
 from test_gpu_decoder import ALPHA_ATOL, KINK_ROWS, LOGIT_ATOL, LOGIT_RTOL, _grad_check
 
@@ -30,17 +30,25 @@ def _threads():
     return int(env) if env.isdigit() and int(env) > 0 else min(16, os.cpu_count() or 1)
 
 
-def _check_grads(grads, rraw, trainable):
+def _check_grads(grads, rraw, trainable, aligned=False):
+    """tests/test_gpu_decoder.py's rule. ``aligned``: the oracle ran on the GPU's own attention-ReLU
+    decisions (helpers.decoder_att_masks), so no row is excused by the kink rule."""
     excused = {n: _grad_check(grads[n].view_as(rraw[n]), rraw[n], "grad " + n) for n in trainable}
     kinks = set().union(*(excused.get(n, set()) for n in KINK_ROWS))
+    if aligned:
+        assert not kinks, excused
+        return
     assert len(kinks) <= 2, excused
     assert excused.get("attention.dec_att.weight", set()) <= \
         excused.get("attention.enc_att.weight", set()) | excused.get("attention.enc_att.bias", set()), excused
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp32-x3"])
-def test_decoder_step_b64_matches_oracle(precision):
-    """fp32-x3 (the bench's decoder GEMMs, CAPMI_GEMM_SPLIT3) under the same tolerances as fp32."""
+@pytest.mark.parametrize("precision,dup", [("fp32", 1), ("fp32-x3", 1), ("fp32", 2), ("fp32-x3", 2)])
+def test_decoder_step_b64_matches_oracle(precision, dup):
+    """fp32-x3 (the bench's decoder GEMMs, CAPMI_GEMM_SPLIT3) under the same tolerances as fp32.
+    dup = 2: the plan the bench runs -- capmi decodes the 49 distinct rows of a 7x7 map, the oracle the
+    pooled 14x14 map the reference decodes (AdaptiveAvgPool2d(14) = 2x replicate, DESIGN.md 4.4);
+    logits, alphas (B, T, 196), loss and gradients under the same rule."""
     from capmi import decoder_fn as DF
     torch.set_num_threads(_threads())
     A, D, M, V, B, L, seed = 512, 512, 512, 8100, 64, 25, 47
@@ -48,17 +56,24 @@ def test_decoder_step_b64_matches_oracle(precision):
     dec.set_compute_precision(precision)
     dec.fine_tune_embeddings(False)  # the bench's (and the reference's default) configuration
     dec.train()
-    enc = gen.encoder_features(seed, B)
+    if dup == 1:
+        enc = t(gen.encoder_features(seed, B))
+        ref_enc = enc
+    else:
+        enc = t(gen.encoder_features(seed, B, P=49)).view(B, 7, 7, 2048)
+        ref_enc = enc.repeat_interleave(dup, 1).repeat_interleave(dup, 2).reshape(B, 196, 2048)
     caps = gen.captions(seed, B, L, V)
     trainable = [n for n, q in dec.named_parameters() if q.requires_grad]
     grads = {n: torch.zeros_like(q) for n, q in dec.named_parameters() if q.requires_grad}
-    loss, preds, alphas = DF.fused_loss_and_grads(dec, t(enc, DEV), t(caps, DEV), [L] * B, 1.0, grads)
+    loss, preds, alphas = DF.fused_loss_and_grads(dec, enc.to(DEV), t(caps, DEV), [L] * B, 1.0, grads, dup=dup)
     torch.cuda.synchronize()
-    rloss, rpreds, ralphas, rraw, _, _, _ = R.train_step(p, set(trainable), t(enc), t(caps), [L] * B)
+    assert tuple(alphas.shape) == (B, L - 1, 196)
+    am = decoder_att_masks(dup)
+    rloss, rpreds, ralphas, rraw, _, _, _ = R.train_step(p, set(trainable), ref_enc, t(caps), [L] * B, att_masks=am)
     assert_close(loss.view(()), rloss, 1e-5, 1e-6, "loss")
     assert_close(preds, rpreds, LOGIT_RTOL, LOGIT_ATOL, "predictions")
     assert_close(alphas, ralphas, 0.0, ALPHA_ATOL, "alphas")
-    _check_grads(grads, rraw, trainable)
+    _check_grads(grads, rraw, trainable, aligned=True)
 
 
 def _encoder(params):
