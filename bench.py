@@ -11,8 +11,14 @@ One step = the reference's training step (models/attention.py:386-430) on a resi
 synthetic batch of 64 (image 3x224x224, 25-token caption, V = 8100) per GPU: ResNet-101
 encoder forward (frozen, BatchNorm in train mode), 24-step soft-attention decoder
 forward + backward, CE + doubly-stochastic loss, (DP: gradient all-reduce over RCCL),
-clamp + Adam. fp32 throughout (the reference's precision). Weights: torch.manual_seed(0)
-random init of the reference architecture (no checkpoints offline).
+clamp + Adam. Arithmetic (defaults --conv x3 --dec auto): fp32 activations, statistics and
+optimizer state; the convs and the decoder GEMMs run "x3" -- every fp32 operand split exactly into
+three bf16 terms whose six significant cross products accumulate in fp32 on the bf16 matrix cores
+(error against fp64 at or below the fp32-MFMA kernel's: tests/test_gpu_x3.py, tests/test_gpu_finetune.py);
+``--conv native --dec fp32`` reproduces the plain fp32 MFMA arithmetic (v_mfma_f32_32x32x2_f32). The
+decoder runs on the 49 distinct rows of the 7x7 layer4 map, which AdaptiveAvgPool2d(14) only repeats
+(exact; ``config.decoder_rows`` in the line). Weights: torch.manual_seed(0) random init
+of the reference architecture (no checkpoints offline).
 
 Default launch: pipelined over two HIP streams, each replaying captured HIP graphs -- call k runs the frozen encoder of batch k
 beside the decoder step of batch k-1 (bit-identical to the sequential order; the K timed
@@ -529,6 +535,8 @@ def main():
                        "per_gpu_batch": B, "global_batch": B * N, "image_size": args.image_size,
                        "caption_len": args.caption_len, "decode_steps": args.caption_len - 1,
                        "vocab": args.vocab, "attention_dim": 512, "decoder_dim": 512, "embed_size": prm.embed_size,
+                       "decoder_rows": ("49 distinct (AdaptiveAvgPool 7->14 replicate; exact, DESIGN.md 4.4)"
+                                        if step._feat_layout(imgs)[1] > 1 else "196 pooled"),
                        "parallelism": f"dp{N}"},
             "dist": {"world_size": N, "backend": ctx.backend or "none",
                      "rank_ms_per_step": [round(x / args.steps * 1e3, 3) for x in rank_dts]},

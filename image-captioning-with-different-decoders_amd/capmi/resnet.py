@@ -258,18 +258,23 @@ class EncoderRunner:
         # conv1 stays on the fp32 MFMA kernel in the x3 mode: SPLIT3 measured 264 vs 261 us there (the
         # 7x7/2 im2col gather over the NHWC4 images bounds it, not the MFMA)
         split3 = False
-        smallk = not nchw and self.x3 and Kd <= _X3_SMALLK
+        # the x3 kernels address their A operand with 32-bit buffer offsets (< 2 GiB: fp32 for x3d /
+        # gemm_x3, three bf16 planes for x3p); a bigger per-GPU batch runs that conv on the fp32 MFMA
+        # kernel instead of failing in the planner (CAPMI_ERANGE)
+        a_elems = N * H * W * ci
+        x3 = self.x3 and a_elems * 4 < (1 << 31)
+        smallk = not nchw and x3 and Kd <= _X3_SMALLK
         # x3d (A fp32 split in-kernel, B planes by LDS-DMA, 256x128 tiles; tools/x3_ab.py at batch 64,
         # profiles/r02_x3_ab_x3d.md): the stride-2 convs, the first c1 of a stage (Cin = 2 Cout), the
         # layer4-sized grids except the plain c1, and the c3 of layer3 -- 4-39 us faster per launch than
         # gemm_x3 / the split pass + x3p there; elsewhere gemm_x3 or x3p stay ahead
-        x3d = (_X3D and not nchw and not smallk and self.x3 and ci % 32 == 0 and Kd % 32 == 0 and (
+        x3d = (_X3D and not nchw and not smallk and x3 and ci % 32 == 0 and Kd % 32 == 0 and (
             st == 2
             or (kh == 1 and in_ss is None and ci == 2 * co)
             or (rows <= 3136 and not (kh == 1 and in_ss is None))
             or (kh == 1 and in_ss is not None and co == 4 * ci and rows <= 12544)))
-        x3p = (not nchw and not smallk and not x3d and self.x3 and in_ss is not None and co >= 128
-               and ci % 32 == 0 and Kd >= 128 and rows >= 12544)
+        x3p = (not nchw and not smallk and not x3d and x3 and in_ss is not None and co >= 128
+               and ci % 32 == 0 and Kd >= 128 and rows >= 12544 and a_elems * 6 < (1 << 31))
         if isinstance(in_ss, _DeferredBN) and not x3p:
             in_ss = in_ss.now()  # only the x3p split pass takes the finalize fused
         if nchw:
@@ -328,13 +333,13 @@ class EncoderRunner:
                 launch()
             return Ho, Wo, rows
         elif kh == 1 and st == 1 and in_ss is None:
-            if self.x3 and Kd % 32 == 0:
+            if x3 and Kd % 32 == 0:
                 w = self._packed_x3(conv)
             prob = K.problem(rows, co, Kd, x, ci, w, Kd, out, co, **kw_)
             mode = CAPMI_A_KMAJOR
         else:
             sc, sh = in_ss if in_ss is not None else (None, None)
-            if self.x3 and Kd % 32 == 0 and ci % 32 == 0:
+            if x3 and Kd % 32 == 0 and ci % 32 == 0:
                 w = self._packed_x3(conv)
             prob = K.problem(rows, co, Kd, x, 0, w, Kd, out, co, conv=geo, in_scale=sc, in_shift=sh, **kw_)
             mode = CAPMI_A_CONV_NHWC

@@ -174,14 +174,17 @@ __global__ void __launch_bounds__(256 * DS_KG) dstep_gemm_kernel(const DsArgs a)
     }
     __syncthreads();
     if (tid == 0) {
-      const int old = __hip_atomic_fetch_add(a.count + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // acq_rel at agent scope: this split's parked partials (stored above, drained) are released
+      // before the count moves, and the last arriver acquires every other split's (the SC1 cache
+      // policy of the buffer ops stays as the performance hint, not the ordering guarantee)
+      const int old = __hip_atomic_fetch_add(a.count + tile, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       const int last = old == S - 1;
       if (last) __hip_atomic_store(a.count + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       last_flag = last;
     }
     __syncthreads();
     if (!last_flag || grp != 0) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every wave of the last arriver reads the others' partials
     const auto rt = rsrc_d(a.part + tb, (unsigned)(S * DS_ROWS * NT * 4));
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};

@@ -170,3 +170,58 @@ def test_dp_rccl_one_rank(fine_tune, graph):
     assert r[1] != "error", r[2]
     assert r[1] == 0.0, ("decoder grads", r[1])
     assert r[2] == 0.0, ("encoder grads", r[2])
+
+
+@pytest.mark.parametrize("captured", [False, True])
+def test_fc_bucket_cut_is_race_free(captured):
+    """The data-parallel step all-reduces the fc gradient bucket (fc.weight, fc.bias and their 256-B
+    padding) while the backward-through-time continues (eager: on_fc_grads callback; pipelined graphs:
+    AttentionTrainStep._capture_split cuts the decoder graph there). That is race-free only if nothing
+    after the cut reads or writes the bucket. Proof without a second GPU: the callback overwrites the
+    whole bucket with a sentinel; after the rest of the backward (eager, or the second graph's replay)
+    the sentinel must be intact and every other gradient bit-identical to a run without the cut."""
+    from capmi import decoder_fn as DF
+    from capmi.optim import Adam
+    from capmi.train_step import AttentionTrainStep
+    from helpers import make_decoder, t
+    import gen
+    V, B, L, seed = 8100, 8, 25, 61
+    dec, _ = make_decoder(512, 512, 512, V, seed, DEV)
+    dec.train()
+    dec.fine_tune_embeddings(False)
+    opt = Adam([q for q in dec.parameters() if q.requires_grad], lr=1e-4)
+    named = dict(dec.named_parameters())
+    head, rest = opt.grad_buckets({named["fc.weight"], named["fc.bias"]})
+    need = [n for n, q in named.items() if q.requires_grad]
+    grads = {n: named[n].grad for n in need}
+    enc = t(gen.encoder_features(seed, B, P=49), DEV).view(B, 7, 7, 2048)
+    caps = t(gen.captions(seed, B, L, V), DEV)
+    sentinel = 12345.0
+
+    def body(cut):
+        return DF.fused_loss_and_grads(dec, enc, caps, [L] * B, 1.0, grads, need=need, on_fc_grads=cut, dup=2)
+
+    body(None)
+    torch.cuda.synchronize()
+    want = [r.clone() for r in rest]
+
+    def fill():
+        for h in head:
+            h.fill_(sentinel)
+
+    for g_ in opt.grad_buffers():
+        g_.zero_()
+    if not captured:
+        body(fill)
+    else:
+        def cut_and_fill(cut):
+            return body(cut)
+        _, g1, g2 = AttentionTrainStep._capture_split(cut_and_fill)
+        g1.replay()
+        fill()
+        g2.replay()
+    torch.cuda.synchronize()
+    for h in head:
+        assert bool((h == sentinel).all()), "the backward after the cut touched the fc bucket"
+    for r, w in zip(rest, want):
+        assert torch.equal(r, w)

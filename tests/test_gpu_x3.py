@@ -242,3 +242,29 @@ def test_x3d_conv_stats(N, H, Cin, Cout, k, stride, pro):
     st = stats.double().cpu()[: 2 * ((rows + 63) // 64) * Cout].view(-1, Cout, 2)
     torch.testing.assert_close(st[..., 0].sum(0), o.sum(0), rtol=1e-5, atol=1e-3)
     torch.testing.assert_close(st[..., 1].sum(0), (o * o).sum(0), rtol=1e-5, atol=1e-3)
+
+
+def test_encoder_x3_oversize_batch_routes_to_fp32():
+    """A per-GPU batch whose conv input passes 2 GiB (layer1's 56x56x256 fp32 map at B = 672: 2.16e9 B)
+    exceeds the x3 kernels' 32-bit buffer offsets: those convs run the fp32 MFMA kernel instead of the
+    planner raising CAPMI_ERANGE (capmi.resnet.EncoderRunner._conv); the rest stay x3. The features
+    must match the all-fp32 encoder's to the two paths' fp32-level accuracy."""
+    import gen
+    from helpers import rel_err, t
+    from capmi.resnet import EncoderRunner, ResNet101
+    B = 672
+    net = ResNet101()
+    sd = net.state_dict()
+    for k_, v in gen.resnet101_params(79).items():
+        sd[k_] = t(v).clone()
+    net.load_state_dict(sd)
+    net = net.to(DEV).train()
+    x = t(gen.images(79, 8), DEV).repeat(B // 8, 1, 1, 1).contiguous()  # 0.4 GB of 224^2 images
+    r3, r1 = EncoderRunner(), EncoderRunner()
+    r3.x3 = True
+    with torch.no_grad():
+        y3 = r3.forward(net, x, out_hw=None)
+        y1 = r1.forward(net, x, out_hw=None)
+    torch.cuda.synchronize()
+    assert torch.isfinite(y3).all()
+    assert rel_err(y3, y1) < 5e-3, rel_err(y3, y1)
