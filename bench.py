@@ -29,10 +29,13 @@ graph instead.
 Rank 0 prints ONE JSON line. ``roofline`` is for the dominant kernel: the conv implicit-GEMM
 instantiation with the most time per step (the conv family is 86% of the step's FLOPs; the
 family aggregate is reported beside it). achieved = that kernel's algorithmic conv FLOPs /
-its summed launch time. The launch times come from a graph-node timing pass right after the
-timed region: the same step (same launch mode, same graphs structure) is captured again with
-timing events recorded as graph nodes (capmi_timing_event_record: hipEventRecordWithFlags(External))
-around every conv launch, on the launch stream, and --steps calls are replayed and read back one by one.
+its summed launch time. The launch times come from a timing pass right after the timed region:
+--steps more eager calls of the step, every conv GEMM with a pair of HIP events that receive its
+dispatch's own start / end timestamps (capmi_timing_arm -> hipExtLaunchKernel: the duration
+rocprofv3 reports for that dispatch), encoder and decoder on one stream -- the condition a rocprofv3
+kernel trace runs the bench in (its tracing serializes the two streams), so the committed trace
+summary of the same command gives the same per-launch average. ``roofline.in_pipeline`` repeats the
+pass with the timed region's two-stream pipelining: the same kernel slowed by the decoder's kernels.
 ``cpu_baseline`` times the CPU oracle (op-for-op restatement of the reference step) on the
 host cores, rank 0 at N = 1 only: the full batch (64 images) for at least one step.
 
@@ -122,62 +125,33 @@ def launch_ranks(args):
 
 
 class ConvTimer:
-    """Times every conv GEMM launch with HIP events on the launch stream, per kernel.
-
-    Eager launches (``enabled``): an event pair around the launch. Inside a graph capture:
-    the pair is recorded as graph nodes (external events), filed under the label of the graph
-    being captured (``on_capture``); after each replay ``harvest(labels)`` reads the pairs of
-    the graphs that ran (the caller synchronizes first)."""
+    """Times every conv GEMM launch of the timing pass, per kernel: each launch (eager) gets a pair of
+    HIP timing events that record its dispatch's own start and end timestamps
+    (capmi.kernels.timed_launch -> capmi_timing_arm -> hipExtLaunchKernel), i.e. the kernel duration
+    rocprofv3 reports for that dispatch -- no event packets between kernels, so no per-measurement
+    overhead. Launches under graph capture, or while disabled, run untimed."""
 
     def __init__(self):
-        self.events = []  # eager: (kernel key, flops, start event, end event)
+        self.events = []  # (kernel key, flops, start event, end event)
         self.enabled = False
-        self.graph = {}   # capture label -> [(key, flops, s, e)]
-        self.label = None
-        self.acc = {}     # key -> [launches, flops, ms] (harvested graph replays)
-
-    def on_capture(self, label):
-        self.label = label
-        self.graph[label] = []
 
     def __call__(self, tag, flops, launch, key):
-        if torch.cuda.is_current_stream_capturing():
-            if self.label is None:
-                launch()
-                return
-            from capmi.kernels import TimingEvent
-            s, e = TimingEvent(), TimingEvent()
-            s.record()
-            launch()
-            e.record()
-            self.graph[self.label].append((key, flops, s, e))
-            return
-        if not self.enabled:
+        if not self.enabled or torch.cuda.is_current_stream_capturing():
             launch()
             return
-        s = torch.cuda.Event(enable_timing=True)
-        e = torch.cuda.Event(enable_timing=True)
-        s.record()
-        launch()
-        e.record()
+        from capmi.kernels import TimingEvent, timed_launch
+        s, e = TimingEvent(), TimingEvent()
+        timed_launch(launch, s, e)
         self.events.append((key, flops, s, e))
 
-    def harvest(self, labels):
-        for lab in labels:
-            for key, f, s, e in self.graph.get(lab, ()):
-                ent = self.acc.setdefault(key, [0, 0.0, 0.0])
-                ent[0] += 1
-                ent[1] += f
-                ent[2] += s.elapsed_ms(e)
-
     def result(self):
-        """{kernel key: [launches, flops, ms]}."""
-        per = {k: list(v) for k, v in self.acc.items()}
+        """{kernel key: [launches, flops, ms]} (synchronize first)."""
+        per = {}
         for key, f, s, e in self.events:
             ent = per.setdefault(key, [0, 0.0, 0.0])
             ent[0] += 1
             ent[1] += f
-            ent[2] += s.elapsed_time(e)
+            ent[2] += s.elapsed_ms(e)
         return per
 
 
@@ -204,9 +178,26 @@ def _traffic(kernel, config="attention"):
     return None if ent is None else ent.get("hbm_bytes_per_launch")
 
 
+def _cgroup_cpus():
+    """CPUs this process's cgroup may use (cgroup v2 cpu.max quota / period), or None (no quota)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        return None
+
+
 def _host_threads():
-    """Threads for the CPU baseline: the box's CPU share for this process (OMP_NUM_THREADS is set
-    to it on the GPU boxes), else the CPUs this process may run on."""
+    """Threads for the CPU baseline: every CPU the box grants this process -- its cgroup CPU quota
+    (on the GPU boxes cpu.max = 1600000 100000: 16 CPUs of the 256 the node shows, one GPU's share;
+    OMP_NUM_THREADS is set to the same 16), else the CPUs in its affinity mask."""
+    q = _cgroup_cpus()
+    if q is not None:
+        try:
+            return min(q, len(os.sched_getaffinity(0)))
+        except AttributeError:
+            return q
     env = os.environ.get("OMP_NUM_THREADS")
     if env and env.isdigit() and int(env) > 0:
         return int(env)
@@ -239,6 +230,7 @@ def _oracle_loop(step_fn, B, seconds, desc, threads):
     dt = time.perf_counter() - t0
     return {"value": round(B * n / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
             "cpu_model": _cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "host_cpus_granted": _cgroup_cpus() or threads,
             "sample": f"{n} oracle train step(s) at B={B} ({desc}), torch CPU fp32, {threads} threads, {dt:.1f} s"}
 
 
@@ -348,30 +340,31 @@ def run_baseline_cpu(args, ctx):
     return time.perf_counter() - t0, float(loss.detach())
 
 
-def graph_timing_pass(args, make_step, imgs, caps, lens, timer, encoder):
-    """Re-capture the benchmarked step with timing events as graph nodes around every conv launch
-    (ConvTimer) and replay it ``args.steps`` times, reading the events back after each call: the
-    conv kernels' durations inside graph replays of the timed step's structure. Returns a
-    description, or raises when the runtime refuses event nodes."""
-    step2 = make_step(seed_off=99)
-    step2.capture_hook = timer.on_capture
+def timing_pass(args, make_step, imgs, caps, lens, timer, encoder, pipeline):
+    """Right after the timed region: --steps more calls of the step, launched eagerly so that every
+    conv GEMM can take a pair of dispatch-timestamp events (ConvTimer). ``pipeline`` False: encoder and
+    decoder on one stream, each kernel alone on the chip -- the condition a rocprofv3 kernel trace runs
+    the bench in (its tracing serializes the two streams: 1.3 % of dispatches overlap in
+    profiles/r03_bench_kernels.md), so these durations are the ones its summary reports. True: the timed
+    region's pipelining (the previous batch's decoder beside the encoder), i.e. the durations the convs
+    take inside the timed step, decoder interference included."""
+    step2 = make_step(seed_off=99, graph=False, pipeline=pipeline)
     encoder._runner.conv_hook = timer
-    pipe = step2.pipeline
-    step2(imgs, caps, lens)          # captures (events as nodes) + first replay
-    if not pipe:
+    step2(imgs, caps, lens)  # warm (pipelined: fills the pipeline with the first encoder pass), untimed
+    if not pipeline:
         step2.flush()
     torch.cuda.synchronize()
+    timer.enabled = True
     for _ in range(args.steps):
         step2(imgs, caps, lens)
-        torch.cuda.synchronize()
-        timer.harvest(step2.replayed)
+    timer.enabled = False
     step2.flush()
     torch.cuda.synchronize()
     encoder._runner.conv_hook = None
-    return (f"HIP events recorded as graph nodes around each conv launch on its stream, {args.steps} replays of "
-            "a re-capture of the timed step (" + ("pipelined: the decoder graph of the previous batch replaying "
-                                                  "beside the encoder graph, as in the timed region)" if pipe else
-                                                  "one graph per step, as in the timed region)"))
+    return (f"HIP events holding each conv GEMM dispatch's own start/end timestamps (hipExtLaunchKernel; what "
+            f"rocprofv3 reports as its duration), {args.steps} eager calls of the step right after the timed region, "
+            + ("pipelined as the timed region (the previous batch's decoder beside the encoder)" if pipeline else
+               "encoder and decoder on one stream (each kernel alone on the chip, as under a rocprofv3 kernel trace)"))
 
 
 def main():
@@ -432,12 +425,13 @@ def main():
         enc_opt.set_clip(5.0)
     pipe = not args.sequential and not ft
 
-    def make_step(seed_off=0):
-        return AttentionTrainStep(encoder, decoder, opt, ctx, alpha_c=1.0, graph=not args.eager,
-                                  seed=77 + seed_off + ctx.rank, pipeline=pipe, encoder_optimizer=enc_opt)
+    def make_step(seed_off=0, graph=not args.eager, pipeline=pipe):
+        return AttentionTrainStep(encoder, decoder, opt, ctx, alpha_c=1.0, graph=graph,
+                                  seed=77 + seed_off + ctx.rank, pipeline=pipeline, encoder_optimizer=enc_opt)
 
     step = make_step()
     timer = ConvTimer()
+    timer_pipe = None
     encoder._runner.conv_hook = None if args.no_roofline or not args.eager else timer
     B = args.batch
     imgs, caps, lens = synthetic_batch(B, args.caption_len, args.vocab, dev, seed=1234 + ctx.rank,
@@ -471,10 +465,15 @@ def main():
     timing = None
     if not args.no_roofline:
         if args.eager:
-            timing = "HIP events around each conv launch on its stream, inside the timed (eager) steps"
+            timing = ("HIP events holding each conv GEMM dispatch's own start/end timestamps (hipExtLaunchKernel), "
+                      "inside the timed (eager) steps")
         else:
-            timing = graph_timing_pass(args, make_step, imgs, caps, lens, timer, encoder)
+            timing = timing_pass(args, make_step, imgs, caps, lens, timer, encoder, pipeline=False)
             K.sk_check()
+            if pipe:
+                timer_pipe = ConvTimer()
+                timing_pass(args, make_step, imgs, caps, lens, timer_pipe, encoder, pipeline=True)
+                K.sk_check()
 
     N = ctx.world
     value = N * B * args.steps / dt
@@ -504,6 +503,13 @@ def main():
                                 "conv_ms_per_step": round(fam_ms / args.steps, 3),
                                 "conv_gflop_per_image": round(per_img / 1e9, 3)},
                 "timing": timing}
+        if timer_pipe is not None:
+            pp = timer_pipe.result().get(key)
+            if pp:
+                # the same kernel's launches inside the pipelined step (decoder kernels sharing the CUs)
+                roof["in_pipeline"] = {"avg_launch_us": round(pp[2] * 1e3 / pp[0], 2),
+                                       "achieved": round(pp[1] / (pp[2] * 1e-3) / 1e12, 3),
+                                       "frac": round(pp[1] / (pp[2] * 1e-3) / 1e12 / peak, 4)}
     cpu = None
     if ctx.rank == 0 and N == 1 and not args.no_cpu_baseline:
         cpu = (cpu_baseline_finetune if ft else cpu_baseline)(args, args.cpu_seconds)

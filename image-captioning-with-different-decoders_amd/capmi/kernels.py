@@ -689,3 +689,15 @@ class TimingEvent:
             lib.capmi_timing_event_destroy(self.h)
         except Exception:  # noqa: BLE001  (interpreter shutdown)
             pass
+
+
+def timed_launch(launch, start, stop):
+    """Run ``launch`` (one capmi GEMM call, eager) with its kernel's dispatch start / end recorded
+    into the TimingEvents ``start`` / ``stop`` (capmi_timing_arm: hipExtLaunchKernel, the AQL
+    packet's own timestamps -- the duration rocprofv3 reports for that dispatch)."""
+    call("capmi_timing_arm", start.h, stop.h)
+    try:
+        launch()
+    finally:
+        if lib.capmi_timing_disarm():
+            raise CapmiError("timed_launch: the call launched no GEMM kernel")

@@ -1,5 +1,6 @@
 // Shared device helpers for libcapmi (gfx950 only).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -16,6 +17,25 @@
 #define CAPMI_REQUIRE(cond, code) \
   do {                            \
     if (!(cond)) return (code);   \
+  } while (0)
+
+// Kernel timing for bench.py's roofline (capmi_timing_arm, timing.hip): the next GEMM launch on this
+// host thread takes these two events and records into them the dispatch's own start / end timestamps
+// (hipExtLaunchKernel: the AQL packet's times, the ones rocprofv3 reports as the kernel duration),
+// then the pair is disarmed. Unarmed, CAPMI_KLAUNCH is hipLaunchKernelGGL.
+struct CapmiArmedEvents {
+  hipEvent_t start, stop;
+};
+extern thread_local CapmiArmedEvents g_capmi_armed;
+#define CAPMI_KLAUNCH(kernel, grid, block, shmem, stream, ...)                                          \
+  do {                                                                                                 \
+    if (g_capmi_armed.start != nullptr) {                                                              \
+      const CapmiArmedEvents ev__ = g_capmi_armed;                                                     \
+      g_capmi_armed = CapmiArmedEvents{nullptr, nullptr};                                              \
+      hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, ev__.start, ev__.stop, 0, __VA_ARGS__); \
+    } else {                                                                                           \
+      hipLaunchKernelGGL(kernel, grid, block, shmem, stream, __VA_ARGS__);                             \
+    }                                                                                                  \
   } while (0)
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }

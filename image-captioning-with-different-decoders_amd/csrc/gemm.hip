@@ -350,10 +350,10 @@ __global__ void __launch_bounds__(256) gemm_kernel(const GemmArgs args) {
 template <int BM, int BN, int WM, int WN, int AMODE, int BMODE>
 static int launch_t(const GemmArgs& a, bool vec, int blocks, hipStream_t s) {
   if (vec)
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AMODE, BMODE, true>), dim3(blocks), dim3(256), 0,
+    CAPMI_KLAUNCH((gemm_kernel<BM, BN, WM, WN, AMODE, BMODE, true>), dim3(blocks), dim3(256), 0,
                        s, a);
   else
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AMODE, BMODE, false>), dim3(blocks), dim3(256),
+    CAPMI_KLAUNCH((gemm_kernel<BM, BN, WM, WN, AMODE, BMODE, false>), dim3(blocks), dim3(256),
                        0, s, a);
   CAPMI_LAUNCH_CHECK();
   return 0;

@@ -323,14 +323,14 @@ void launch_bf16(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
   const bool sk = a.sk_workers > 0;
   if (amode == 2) {
     if (sk)
-      hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, 2, true>), g, b, 0, s, a);
+      CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 2, true>), g, b, 0, s, a);
     else
-      hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, 2, false>), g, b, 0, s, a);
+      CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 2, false>), g, b, 0, s, a);
   } else {
     if (sk)
-      hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, 0, true>), g, b, 0, s, a);
+      CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 0, true>), g, b, 0, s, a);
     else
-      hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, 0, false>), g, b, 0, s, a);
+      CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 0, false>), g, b, 0, s, a);
   }
 }
 

@@ -789,21 +789,21 @@ template <int BM, int BN, bool SK, int TERMS>
 void launch_nts(const GemmArgs& a, int amode, int bmode, bool pro, int blocks, hipStream_t s) {
   const dim3 g(blocks), b(256);
   if (TERMS == 3 && amode == 2 && pro)  // conv with the BN-apply + ReLU prologue
-    hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, TERMS == 3 ? 2 : 0, 0, SK, TERMS, TERMS == 3>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nts_kernel<BM, BN, TERMS == 3 ? 2 : 0, 0, SK, TERMS, TERMS == 3>), g, b, 0, s, a);
   else if (TERMS == 3 && amode == 2)  // conv (no prologue: the data gradients' dY)
-    hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, TERMS == 3 ? 2 : 0, 0, SK, TERMS>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nts_kernel<BM, BN, TERMS == 3 ? 2 : 0, 0, SK, TERMS>), g, b, 0, s, a);
   else if (TERMS == 3 && amode == 4)  // conv1 on the NHWC4 images
-    hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, TERMS == 3 ? 4 : 0, 0, SK, TERMS>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nts_kernel<BM, BN, TERMS == 3 ? 4 : 0, 0, SK, TERMS>), g, b, 0, s, a);
   else if (TERMS == 3 && bmode == 2 && pro)  // conv weight gradient, BN prologue on the im2col B
-    hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, 1, TERMS == 3 ? 2 : 1, SK, TERMS, TERMS == 3>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nts_kernel<BM, BN, 1, TERMS == 3 ? 2 : 1, SK, TERMS, TERMS == 3>), g, b, 0, s, a);
   else if (TERMS == 3 && bmode == 2)
-    hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, 1, TERMS == 3 ? 2 : 1, SK, TERMS>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nts_kernel<BM, BN, 1, TERMS == 3 ? 2 : 1, SK, TERMS>), g, b, 0, s, a);
   else if (amode == 0 && bmode == 0)
-    hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, 0, 0, SK, TERMS>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nts_kernel<BM, BN, 0, 0, SK, TERMS>), g, b, 0, s, a);
   else if (amode == 0 && bmode == 1)
-    hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, 0, 1, SK, TERMS>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nts_kernel<BM, BN, 0, 1, SK, TERMS>), g, b, 0, s, a);
   else
-    hipLaunchKernelGGL((gemm_nts_kernel<BM, BN, 1, 1, SK, TERMS>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nts_kernel<BM, BN, 1, 1, SK, TERMS>), g, b, 0, s, a);
 }
 
 template <int AMODE, bool PRO, bool SK>
@@ -816,26 +816,26 @@ template <bool SK>
 void launch_nt8(const GemmArgs& a, int amode, bool pro, int blocks, hipStream_t s) {
   const dim3 g(blocks), b(512);
   if (amode == 4)
-    hipLaunchKernelGGL((gemm_nt8_kernel<4, false, SK>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nt8_kernel<4, false, SK>), g, b, 0, s, a);
   else if (amode == 0)
-    hipLaunchKernelGGL((gemm_nt8_kernel<0, false, SK>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nt8_kernel<0, false, SK>), g, b, 0, s, a);
   else if (pro)
-    hipLaunchKernelGGL((gemm_nt8_kernel<2, true, SK>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nt8_kernel<2, true, SK>), g, b, 0, s, a);
   else
-    hipLaunchKernelGGL((gemm_nt8_kernel<2, false, SK>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nt8_kernel<2, false, SK>), g, b, 0, s, a);
 }
 
 template <int BM, int BN, bool SK>
 void launch_sk_bf16(const GemmArgs& a, int amode, bool pro, int blocks, hipStream_t s) {
   const dim3 g(blocks), b(256);
   if (amode == 4)
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 4, 0, false, SK, true>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nt_kernel<BM, BN, 4, 0, false, SK, true>), g, b, 0, s, a);
   else if (amode == 0)
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 0, 0, false, SK, true>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nt_kernel<BM, BN, 0, 0, false, SK, true>), g, b, 0, s, a);
   else if (pro)
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 2, 0, true, SK, true>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nt_kernel<BM, BN, 2, 0, true, SK, true>), g, b, 0, s, a);
   else
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 2, 0, false, SK, true>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nt_kernel<BM, BN, 2, 0, false, SK, true>), g, b, 0, s, a);
 }
 
 template <int BM, int BN, bool SK>
@@ -843,24 +843,24 @@ void launch_sk(const GemmArgs& a, int amode, int bmode, bool pro, int blocks, hi
   const dim3 g(blocks), b(256);
   if (bmode == 2) {  // weight gradient: A = dY stored as k rows, B = implicit im2col k rows
     if (pro)
-      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 1, 2, true, SK>), g, b, 0, s, a);
+      CAPMI_KLAUNCH((gemm_nt_kernel<BM, BN, 1, 2, true, SK>), g, b, 0, s, a);
     else
-      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 1, 2, false, SK>), g, b, 0, s, a);
+      CAPMI_KLAUNCH((gemm_nt_kernel<BM, BN, 1, 2, false, SK>), g, b, 0, s, a);
   } else if (bmode == 1) {
     if (amode == 1)
-      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 1, 1, false, SK>), g, b, 0, s, a);
+      CAPMI_KLAUNCH((gemm_nt_kernel<BM, BN, 1, 1, false, SK>), g, b, 0, s, a);
     else
-      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 0, 1, false, SK>), g, b, 0, s, a);
+      CAPMI_KLAUNCH((gemm_nt_kernel<BM, BN, 0, 1, false, SK>), g, b, 0, s, a);
   } else if (amode == 1) {
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 1, 0, false, SK>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nt_kernel<BM, BN, 1, 0, false, SK>), g, b, 0, s, a);
   } else if (amode == 4) {
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 4, 0, false, SK>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nt_kernel<BM, BN, 4, 0, false, SK>), g, b, 0, s, a);
   } else if (amode == 0) {
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 0, 0, false, SK>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nt_kernel<BM, BN, 0, 0, false, SK>), g, b, 0, s, a);
   } else if (pro) {
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 2, 0, true, SK>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nt_kernel<BM, BN, 2, 0, true, SK>), g, b, 0, s, a);
   } else {
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, 2, 0, false, SK>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_nt_kernel<BM, BN, 2, 0, false, SK>), g, b, 0, s, a);
   }
 }
 

@@ -429,11 +429,11 @@ void launch_x3(const GemmArgs& a, int amode, bool pro, int blocks, hipStream_t s
   const dim3 g(blocks), b(XNT);
   if (amode == 2) {
     if (pro)
-      hipLaunchKernelGGL((gemm_x3_kernel<BN, 2, true, SK>), g, b, 0, s, a);
+      CAPMI_KLAUNCH((gemm_x3_kernel<BN, 2, true, SK>), g, b, 0, s, a);
     else
-      hipLaunchKernelGGL((gemm_x3_kernel<BN, 2, false, SK>), g, b, 0, s, a);
+      CAPMI_KLAUNCH((gemm_x3_kernel<BN, 2, false, SK>), g, b, 0, s, a);
   } else {
-    hipLaunchKernelGGL((gemm_x3_kernel<BN, 0, false, SK>), g, b, 0, s, a);
+    CAPMI_KLAUNCH((gemm_x3_kernel<BN, 0, false, SK>), g, b, 0, s, a);
   }
 }
 

@@ -562,7 +562,7 @@ int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
   const bool sk = a.sk_workers > 0;
   const bool pro = a.p[0].in_scale != nullptr;
   CAPMI_REQUIRE(!pro || amode == 2, CAPMI_EINVAL);
-#define X3D_GO(M, S, PR) hipLaunchKernelGGL((gemm_x3p_kernel<M, S, 32, true, PR>), g, b, 0, s, a)
+#define X3D_GO(M, S, PR) CAPMI_KLAUNCH((gemm_x3p_kernel<M, S, 32, true, PR>), g, b, 0, s, a)
   if (amode == 2) {
     if (pro) {
       if (sk) X3D_GO(2, true, true); else X3D_GO(2, false, true);
@@ -583,7 +583,7 @@ int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_
   // the two-workgroup form runs data-parallel grids only (its 128-VGPR budget has no room for
   // the stream-K hand-off)
   CAPMI_REQUIRE(bk == 32 || (bk == 16 && !sk), CAPMI_EINVAL);
-#define X3P_GO(M, S, BK) hipLaunchKernelGGL((gemm_x3p_kernel<M, S, BK>), g, b, 0, s, a)
+#define X3P_GO(M, S, BK) CAPMI_KLAUNCH((gemm_x3p_kernel<M, S, BK>), g, b, 0, s, a)
   if (bk == 16) {
     if (amode == 2)
       X3P_GO(2, false, 16);

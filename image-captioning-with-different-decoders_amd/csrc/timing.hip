@@ -6,6 +6,23 @@
 // 0: hipEventRecordWithFlags(External) first; 1: it was refused once, go straight to the node
 static int g_record_mode = 0;
 
+thread_local CapmiArmedEvents g_capmi_armed = {nullptr, nullptr};
+
+// the next GEMM launch of this host thread records its dispatch start / end into (start, stop)
+// (CAPMI_KLAUNCH, common.h); eager launches only (a stream under capture refuses it)
+extern "C" int capmi_timing_arm(void* start, void* stop) {
+  CAPMI_REQUIRE(start != nullptr && stop != nullptr, CAPMI_EINVAL);
+  g_capmi_armed = CapmiArmedEvents{reinterpret_cast<hipEvent_t>(start), reinterpret_cast<hipEvent_t>(stop)};
+  return 0;
+}
+
+// drops an armed pair no launch consumed (a launch refused by its planner); returns 1 if one was left
+extern "C" int capmi_timing_disarm(void) {
+  const int left = g_capmi_armed.start != nullptr ? 1 : 0;
+  g_capmi_armed = CapmiArmedEvents{nullptr, nullptr};
+  return left;
+}
+
 extern "C" int capmi_timing_event_create(void** event) {
   CAPMI_REQUIRE(event != nullptr, CAPMI_EINVAL);
   hipEvent_t e = nullptr;

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 15
+#define CAPMI_ABI_VERSION 16
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -520,6 +520,12 @@ int capmi_timing_event_create(void** event);
 int capmi_timing_event_destroy(void* event);
 int capmi_timing_event_record(void* event, void* stream);
 int capmi_timing_elapsed_ms(void* start, void* end, float* ms);
+/* ABI 16: the next GEMM launch of the calling host thread (any capmi_gemm* entry point, eager, not
+ * under capture) records its dispatch's own start / end timestamps into the two timing events
+ * (hipExtLaunchKernel: the kernel duration rocprofv3 reports); capmi_timing_disarm drops a pair no
+ * launch consumed and returns 1 if there was one. */
+int capmi_timing_arm(void* start, void* stop);
+int capmi_timing_disarm(void);
 
 const char* capmi_strerror(int code);
 int capmi_abi_version(void);
