@@ -29,16 +29,24 @@
 namespace {
 
 constexpr int XBK = 32;       // fp32 k per k-tile
+#ifndef X3_M16
+#define X3_M16 1
+#endif
 #ifndef X3_SWZ
-#define X3_SWZ 0
+#define X3_SWZ X3_M16
 #endif
 // LDS row stride (bf16 elements). X3_SWZ (default): 64-B rows with x3p's 16-B chunk swizzle (chunk c
 // of row r at c ^ ((r / 4) % 4)): the 8-B split stores of a wave (8 rows x 64 B) and the 16-lane
 // ds_read_b128 groups both hit 64 distinct banks. Else 80-B padded rows (the reads conflict-free,
 // the split stores 2-3-way conflicted: PMC lds_conflict 29 %, profiles/r02_pmc_sq.txt).
 constexpr int XSB = X3_SWZ ? XBK : XBK + 8;
+// X3_M16 (round 3, default): the MFMAs are v_mfma_f32_16x16x32_bf16 (one per 32-deep k-tile and
+// 16 x 16 block; the chip holds a higher clock under them than under 32x32x16: gemm_x3p.hip), read
+// as lane l -> row l % 16, chunk l / 16, conflict-free on the [0, 2, 3, 1][(row >> 2) & 3] chunk
+// swizzle of 64-B rows (the split stores stay conflict-free: 16 lanes = two whole rows)
 __device__ __forceinline__ int xoff(int row, int chunk) {  // bf16 offset of 8-element chunk `chunk` of `row`
-  return row * XSB + ((X3_SWZ ? (chunk ^ ((row >> 2) & 3)) : chunk) << 3);
+  const int sw = X3_M16 ? ((0x1320 >> (4 * ((row >> 2) & 3))) & 3) : ((row >> 2) & 3);
+  return row * XSB + ((X3_SWZ ? (chunk ^ sw) : chunk) << 3);
 }
 constexpr int XNT = 512;
 typedef unsigned u32x4_x __attribute__((ext_vector_type(4)));
@@ -84,12 +92,19 @@ gemm_x3_kernel(const GemmArgs args) {
   (void)NB;
 
   f32x16 acc[TN];
+  constexpr int TN16 = WN / 16;      // 16x16x32: 2 x TN16 blocks per wave
+  typedef float f32x4_x __attribute__((ext_vector_type(4)));
+  f32x4_x acc4[2][TN16];
 
   auto mainloop = [&](const capmi_gemm_problem& P, int m0, int n0, int k_lo, int k_hi) {
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < TN16; ++j) acc4[i][j] = f32x4_x{0.f, 0.f, 0.f, 0.f};
     const int nkt = (k_hi - k_lo) / XBK;
     if (nkt <= 0) return;
     const int M = P.M, N = P.N;
@@ -213,6 +228,35 @@ gemm_x3_kernel(const GemmArgs args) {
         if (b_lds[i] >= 0) *reinterpret_cast<u32x4_x*>(&Bs[buf][0][b_lds[i]]) = st.b[i];
     };
     auto compute = [&](int buf) {
+      if constexpr (X3_M16) {
+        const int c = lane >> 4, rl = lane & 15;
+        bf16x8_x a[2][3], b[TN16][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int ao = xoff(wm0 + 16 * i + rl, c);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) a[i][p] = *reinterpret_cast<const bf16x8_x*>(&As[buf][p][ao]);
+        }
+#pragma unroll
+        for (int j = 0; j < TN16; ++j) {
+          const int bo = xoff(wn0 + 16 * j + rl, c);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) b[j][p] = *reinterpret_cast<const bf16x8_x*>(&Bs[buf][p][bo]);
+        }
+        // smallest terms first into the fp32 accumulator
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < TN16; ++j) {
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][1], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][2], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[j][0], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][1], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][0], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][0], acc4[i][j], 0, 0, 0);
+          }
+        return;
+      }
 #pragma unroll
       for (int g = 0; g < XBK / 16; ++g) {
         bf16x8_x a[3], b[3][TN];
@@ -272,46 +316,85 @@ gemm_x3_kernel(const GemmArgs args) {
     const float beta = P.beta;
     const int relu = P.relu;
     const long long ldc = P.ldc, c_r1 = P.c_r1, c_s2 = P.c_s2;
-    float csum[TN], csq[TN];
+    // per-lane column sums over this wave's 32 rows: TN columns per lane (32x32x16: lane column
+    // 32 j + lane % 32) or TN16 (16x16x32: column 16 j + lane % 16); scol(j) is the wave-local column
+    constexpr int NCOL = X3_M16 ? TN16 : TN;
+    float csum[NCOL], csq[NCOL];
+    auto scol = [&](int j) { return X3_M16 ? 16 * j + (lane & 15) : 32 * j + lr; };
+    if constexpr (X3_M16) {
+      const int rq = lane >> 4;
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      csum[j] = 0.f;
-      csq[j] = 0.f;
-      const int col = n0 + wn0 + 32 * j + lr;
-      const bool cok = col < N;
-      float bias = 0.f;
-      if (cok) {
-        if (P.bias) bias += P.bias[col];
-        if (P.bias2) bias += P.bias2[col];
+      for (int j = 0; j < TN16; ++j) {
+        csum[j] = 0.f;
+        csq[j] = 0.f;
+        const int col = n0 + wn0 + scol(j);
+        const bool cok = col < N;
+        float bias = 0.f;
+        if (cok) {
+          if (P.bias) bias += P.bias[col];
+          if (P.bias2) bias += P.bias2[col];
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = m0 + wm0 + 16 * i + 4 * rq + r;
+            if (cok && row < M) {
+              float* cp = C + remap(row, c_r1, ldc, c_s2) + col;
+              float v = fmaf(acc4[i][j][r], alpha, bias);
+              if (beta != 0.f) v = fmaf(beta, *cp, v);
+              if (relu) v = fmaxf(v, 0.f);
+              *cp = v;
+              csum[j] += v;
+              csq[j] = fmaf(v, v, csq[j]);
+            }
+          }
       }
+    } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (cok && row < M) {
-          float* cp = C + remap(row, c_r1, ldc, c_s2) + col;
-          float v = fmaf(acc[j][r], alpha, bias);
-          if (beta != 0.f) v = fmaf(beta, *cp, v);
-          if (relu) v = fmaxf(v, 0.f);
-          *cp = v;
-          csum[j] += v;
-          csq[j] = fmaf(v, v, csq[j]);
+      for (int j = 0; j < TN; ++j) {
+        csum[j] = 0.f;
+        csq[j] = 0.f;
+        const int col = n0 + wn0 + 32 * j + lr;
+        const bool cok = col < N;
+        float bias = 0.f;
+        if (cok) {
+          if (P.bias) bias += P.bias[col];
+          if (P.bias2) bias += P.bias2[col];
+        }
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm0 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (cok && row < M) {
+            float* cp = C + remap(row, c_r1, ldc, c_s2) + col;
+            float v = fmaf(acc[j][r], alpha, bias);
+            if (beta != 0.f) v = fmaf(beta, *cp, v);
+            if (relu) v = fmaxf(v, 0.f);
+            *cp = v;
+            csum[j] += v;
+            csq[j] = fmaf(v, v, csq[j]);
+          }
         }
       }
     }
     float* __restrict__ stats = P.stats;
     if (stats != nullptr) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
+      for (int j = 0; j < NCOL; ++j) {
+        if (X3_M16) {
+          csum[j] += __shfl_xor(csum[j], 16, 64);
+          csq[j] += __shfl_xor(csq[j], 16, 64);
+        }
         csum[j] += __shfl_xor(csum[j], 32, 64);
         csq[j] += __shfl_xor(csq[j], 32, 64);
       }
       // wave rows 2s and 2s+1 share the tile's 64-row slice s
       float* red = reinterpret_cast<float*>(&As[0][0][0]);  // the k loop ended with a barrier
-      if (lh == 0) {
+      if (X3_M16 ? (lane >> 4) == 0 : lh == 0) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          red[(wid * 2 + 0) * WN + 32 * j + lr] = csum[j];
-          red[(wid * 2 + 1) * WN + 32 * j + lr] = csq[j];
+        for (int j = 0; j < NCOL; ++j) {
+          red[(wid * 2 + 0) * WN + scol(j)] = csum[j];
+          red[(wid * 2 + 1) * WN + scol(j)] = csq[j];
         }
       }
       __syncthreads();
@@ -374,6 +457,14 @@ gemm_x3_kernel(const GemmArgs args) {
     if (ke < nkt) {
       const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + (long long)blockIdx.x * PART, 0,
                                                         PART * 4, 0x00020000);
+      if constexpr (X3_M16) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < TN16; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_x, acc4[i][j]), rs,
+                                                   ((i * TN16 + j) * XNT + tid) * 16, 0, kSc1x);
+      } else {
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -385,6 +476,7 @@ gemm_x3_kernel(const GemmArgs args) {
           v.w = __float_as_uint(acc[j][4 * q + 3]);
           __builtin_amdgcn_raw_buffer_store_b128(v, rs, ((j * 4 + q) * XNT + tid) * 16, 0, kSc1x);
         }
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) __hip_atomic_store(flags + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -407,6 +499,14 @@ gemm_x3_kernel(const GemmArgs args) {
         __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + b2 * PART, 0, PART * 4, 0x00020000);
+        if constexpr (X3_M16) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < TN16; ++j)
+              acc4[i][j] += __builtin_bit_cast(
+                  f32x4_x, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i * TN16 + j) * XNT + tid) * 16, 0, kSc1x));
+        } else {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -417,6 +517,7 @@ gemm_x3_kernel(const GemmArgs args) {
             acc[j][4 * q + 2] += __uint_as_float(v.z);
             acc[j][4 * q + 3] += __uint_as_float(v.w);
           }
+        }
         if (ub + w2 * U / G <= tb) break;
       }
     }

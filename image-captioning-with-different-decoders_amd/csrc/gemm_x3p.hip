@@ -25,6 +25,7 @@ namespace {
 constexpr int PBM = 256, PBN = 128, PNT = 512;
 typedef unsigned u32x4_p __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_p __attribute__((ext_vector_type(8)));
+typedef float f32x4_p __attribute__((ext_vector_type(4)));
 constexpr unsigned kOOBp = 0x80000000u;
 constexpr int kSc1p = 16;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -49,6 +50,24 @@ struct X3pGeo {
   static constexpr int WPE = PBK == 16 ? 4 : 2;     // waves per SIMD: two workgroups per CU at BK = 16
 };
 
+#ifndef X3P_M16
+#define X3P_M16 1
+#endif
+// MFMA shape (round 3): 32-deep k-tiles run v_mfma_f32_16x16x32_bf16 (X3P_M16, default) -- the same
+// cycles per FLOP as 32x32x16, but MI355X holds a higher clock under a 16x16x32 stream (random data:
+// ~1.12-1.15x the FLOP/s, MI355X_MICROARCH.md 'DVFS give-back' (7)); 16-deep k-tiles keep 32x32x16.
+// LDS chunk swizzle of row r (physical 16-B slot of logical k-chunk c = c ^ swz(r)): for the 16x16x32
+// reads (lane l: row l % 16, chunk l / 16) the slot pattern [0, 2, 3, 1][(r >> 2) & 3] makes every
+// 16-lane group of ds_read_b128 hit 64 distinct banks; the 32x32x16 reads (lane l: row l % 32, chunk
+// 2g + l / 32) use (r / SWZ) % CPR.
+template <int PBK>
+__device__ __forceinline__ int swz(int r) {
+  if constexpr (PBK == 32 && X3P_M16)
+    return (0x1320 >> (4 * ((r >> 2) & 3))) & 3;
+  else
+    return (r / X3pGeo<PBK>::SWZ) % X3pGeo<PBK>::CPR;
+}
+
 // ASPLIT ("x3d"): A is the fp32 operand itself (dense, or the NHWC conv input with the optional BN-apply
 // + ReLU prologue PRO), loaded to registers one k-tile ahead and split into the three swizzled LDS
 // planes after the k-tile's MFMAs; B stays LDS-DMA. It replaces gemm_x3 (both operands through
@@ -70,7 +89,9 @@ gemm_x3p_kernel(const GemmArgs args) {
   // DMA lane geometry: row lane / CPR of an RPB-row block, slot lane % CPR
   const int drow = lane / CPR, dslot = lane % CPR;
 
-  f32x16 acc[2][2];
+  constexpr bool M16 = PBK == 32 && X3P_M16;
+  f32x16 acc[2][2];     // 32x32x16: wave tile 2 x 2 blocks of 32 x 32
+  f32x4_p acc4[4][4];   // 16x16x32: wave tile 4 x 4 blocks of 16 x 16
 
   auto mainloop = [&](const capmi_gemm_problem& P, int m0, int n0, int k_lo, int k_hi) {
 #pragma unroll
@@ -79,6 +100,10 @@ gemm_x3p_kernel(const GemmArgs args) {
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc4[i][j] = f32x4_p{0.f, 0.f, 0.f, 0.f};
     const int nkt = (k_hi - k_lo) / PBK;
     if (nkt <= 0) return;
     const int M = P.M, N = P.N;
@@ -103,7 +128,7 @@ gemm_x3p_kernel(const GemmArgs args) {
     for (int i = 0; i < NAB; ++i) {
       const int r = (NAB * wid + i) * RPB + drow;
       const int row = m0 + r;
-      a_ch[i] = dslot ^ ((r / SWZ) % CPR);
+      a_ch[i] = dslot ^ swz<PBK>(r);
       a_ok[i] = row < M;
       if (AMODE == 0) {
         a_base[i] = (unsigned)(((long long)(a_ok[i] ? row : 0) * P.lda + a_ch[i] * 8) * 2);
@@ -120,7 +145,7 @@ gemm_x3p_kernel(const GemmArgs args) {
     }
     const bool bw = wid < NBB;  // this wave stages B row block wid
     const int br = (wid % NBB) * RPB + drow;
-    const int b_ch = dslot ^ ((br / SWZ) % CPR);
+    const int b_ch = dslot ^ swz<PBK>(br);
     const bool b_ok = bw && n0 + br < N;
     const unsigned b_base = (unsigned)(((long long)(b_ok ? n0 + br : 0) * P.ldb + b_ch * 8) * 2);
     // x3d: four fp32 float4 slots per thread, slot i = row (tid + 512 i) / 8, k 4 ((tid + 512 i) % 8)
@@ -136,7 +161,7 @@ gemm_x3p_kernel(const GemmArgs args) {
         const int r = (tid + 512 * i) >> 3;
         const int row = m0 + r;
         s_ok[i] = row < M;
-        s_lds[i] = r * PROWB + (((aq >> 1) ^ ((r / SWZ) % CPR)) << 4) + (aq & 1) * 8;
+        s_lds[i] = r * PROWB + (((aq >> 1) ^ swz<PBK>(r)) << 4) + (aq & 1) * 8;
         if (AMODE == 0) {
           s_base[i] = (unsigned)(((long long)(s_ok[i] ? row : 0) * P.lda + aq * 4) * 4);
           s_ih0[i] = s_iw0[i] = 0;
@@ -241,16 +266,16 @@ gemm_x3p_kernel(const GemmArgs args) {
               boff == kOOBp ? kOOBp : boff + p * pB2, 0, 0, 0);
       }
     };
-    // x3d: the registers of the k-tile loaded by the last issue() -> (prologue) -> three planes
-    auto store_a = [&](int buf) {
+    // x3d: fp32 A registers of one k-tile -> (prologue) -> three planes
+    auto store_a_from = [&](int buf, const float4 (&ar)[NSA], float4 sc, float4 sh, unsigned msk) {
       if (!ASPLIT) return;
       unsigned char* base = lds + buf * PBUF;
 #pragma unroll
       for (int i = 0; i < NSA; ++i) {
-        float4 v = areg[i];
-        if (PRO) v = make_float4(fmaxf(fmaf(v.x, a_sc.x, a_sh.x), 0.f), fmaxf(fmaf(v.y, a_sc.y, a_sh.y), 0.f),
-                                 fmaxf(fmaf(v.z, a_sc.z, a_sh.z), 0.f), fmaxf(fmaf(v.w, a_sc.w, a_sh.w), 0.f));
-        if (!((a_msk >> i) & 1u)) v = make_float4(0.f, 0.f, 0.f, 0.f);  // padding taps: zeros AFTER the BN
+        float4 v = ar[i];
+        if (PRO) v = make_float4(fmaxf(fmaf(v.x, sc.x, sh.x), 0.f), fmaxf(fmaf(v.y, sc.y, sh.y), 0.f),
+                                 fmaxf(fmaf(v.z, sc.z, sh.z), 0.f), fmaxf(fmaf(v.w, sc.w, sh.w), 0.f));
+        if (!((msk >> i) & 1u)) v = make_float4(0.f, 0.f, 0.f, 0.f);  // padding taps: zeros AFTER the BN
         const float e[4] = {v.x, v.y, v.z, v.w};
         unsigned short h[3][4];
 #pragma unroll
@@ -272,6 +297,8 @@ gemm_x3p_kernel(const GemmArgs args) {
         }
       }
     };
+    // x3d: the registers of the k-tile loaded by the last issue()
+    auto store_a = [&](int buf) { store_a_from(buf, areg, a_sc, a_sh, a_msk); };
 #ifndef X3D_MID
 #define X3D_MID 0
 #endif
@@ -279,6 +306,45 @@ gemm_x3p_kernel(const GemmArgs args) {
     auto compute = [&](int buf, int nbuf) {
       const unsigned char* A_ = lds + buf * PBUF;
       const unsigned char* B_ = A_ + PA_BYTES;
+      if constexpr (M16) {
+        // 16x16x32: lane l reads row (l % 16) of each 16-row block, k-chunk l / 16 (8 k of the 32);
+        // all 24 fragments of the k-tile up front, then 16 blocks x 6 products
+        bf16x8_p a[4][3], b[4][3];
+        const int c = lane >> 4, rl = lane & 15;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = wm0 + 16 * i + rl;
+          const int o = r * PROWB + ((c ^ swz<PBK>(r)) << 4);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) a[i][p] = *reinterpret_cast<const bf16x8_p*>(A_ + p * PBM * PROWB + o);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = wn0 + 16 * j + rl;
+          const int o = r * PROWB + ((c ^ swz<PBK>(r)) << 4);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) b[j][p] = *reinterpret_cast<const bf16x8_p*>(B_ + p * PBN * PROWB + o);
+        }
+        // smallest terms first into each fp32 accumulator
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][1], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][2], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[j][0], acc4[i][j], 0, 0, 0);
+          }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][1], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][0], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][0], acc4[i][j], 0, 0, 0);
+          }
+        (void)nbuf;
+        return;
+      }
       // every fragment of the k-tile is requested up front (2 x 12 ds_read_b128): the second
       // chunk's reads land while the first chunk's 24 MFMAs run
       bf16x8_p a[PBK / 16][2][3], b[PBK / 16][2][3];
@@ -288,7 +354,7 @@ gemm_x3p_kernel(const GemmArgs args) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int r = wm0 + 32 * i + lr;
-          const int o = r * PROWB + ((c ^ ((r / SWZ) % CPR)) << 4);
+          const int o = r * PROWB + ((c ^ swz<PBK>(r)) << 4);
 #if X3P_SKIP & 2  // timing-only: no LDS reads
 #pragma unroll
           for (int p = 0; p < 3; ++p) a[g][i][p] = bf16x8_p{} + (__bf16)(float)(o + p);
@@ -300,7 +366,7 @@ gemm_x3p_kernel(const GemmArgs args) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int r = wn0 + 32 * j + lr;
-          const int o = r * PROWB + ((c ^ ((r / SWZ) % CPR)) << 4);
+          const int o = r * PROWB + ((c ^ swz<PBK>(r)) << 4);
 #if X3P_SKIP & 2
 #pragma unroll
           for (int p = 0; p < 3; ++p) b[g][j][p] = bf16x8_p{} + (__bf16)(float)(o - p);
@@ -336,6 +402,116 @@ gemm_x3p_kernel(const GemmArgs args) {
       }
       (void)nbuf;
     };
+#ifndef X3D_DEEP
+#define X3D_DEEP 0
+#endif
+    if constexpr (ASPLIT && X3D_DEEP && !X3D_MID) {
+      // x3d with A TWO k-tiles ahead (round 3): the fp32 A of k-tile t sits in register slot t & 1
+      // (loaded in iteration t - 2), B goes by LDS-DMA one k-tile ahead as before, and so do the
+      // prologue's scale / shift (one register set). One k-tile of MFMAs (1536 cycles per SIMD) does
+      // not cover an HBM-latency load, so the one-deep form drained vmcnt(0) on A every k-tile. Per
+      // iteration the vector-memory instructions are issued in the order [B DMA + scale / shift of
+      // t + 1][the NSA A loads of t + 2], so `s_waitcnt vmcnt(NSA)` after the MFMAs retires exactly
+      // everything of t + 1 (loads return in order) and leaves A(t + 2) in flight. Every load is
+      // issued unconditionally (out-of-range offsets read zeros), so the count never changes.
+      static_assert(NSA == 4, "x3d deep pipeline: vmcnt immediate");
+      const auto rsc = rsrc_p(PRO ? (const void*)P.in_scale : P.A, PRO ? (unsigned)(cCin * 4) : 0u);
+      const auto rsh = rsrc_p(PRO ? (const void*)P.in_shift : P.A, PRO ? (unsigned)(cCin * 4) : 0u);
+      // channel walk of the scale / shift loads (one k-tile behind the A walk c_ci / c_kh / c_kw)
+      int b_ci = c_ci, b_tap = c_kh * cKW + c_kw;
+      const int taps = cKW * P.cKH;
+      auto load_a = [&](int kt, float4 (&ar)[NSA], unsigned& msk) {
+        const int k = k_lo + kt * PBK;
+        const bool kok = k < k_hi;
+        msk = 0;
+#pragma unroll
+        for (int i = 0; i < NSA; ++i) {
+          unsigned off;
+          bool ok;
+          if (AMODE == 0) {
+            ok = s_ok[i] && kok;
+            off = s_base[i] + (unsigned)k * 4;
+          } else {
+            const int ih = s_ih0[i] + c_kh, iw = s_iw0[i] + c_kw;
+            ok = s_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
+            off = ((s_base[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + aq * 4)) * 4u;
+          }
+          ar[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off : kOOBp, 0, 0));
+          msk |= (unsigned)ok << i;
+        }
+        if (AMODE == 2 && ++c_kw == cKW) {  // (PBK = 32: one k-tile per (slice, tap))
+          c_kw = 0;
+          if (++c_kh == P.cKH) {
+            c_kh = 0;
+            c_ci += 32;
+          }
+        }
+      };
+      auto issue_b = [&](int kt, int buf) {
+        const int k = k_lo + kt * PBK;
+        const bool kok = k < k_hi;
+        if constexpr (PRO) {
+          const unsigned o = kok ? (unsigned)(b_ci + aq * 4) * 4u : kOOBp;
+          a_sc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsc, o, 0, 0));
+          a_sh = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsh, o, 0, 0));
+          if (++b_tap == taps) {
+            b_tap = 0;
+            b_ci += 32;
+          }
+        }
+        unsigned char* base = lds + buf * PBUF;
+        if (bw) {
+          const unsigned boff = b_ok && kok ? b_base + (unsigned)k * 2 : kOOBp;
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * RPB * PROWB), 16,
+                boff == kOOBp ? kOOBp : boff + p * pB2, 0, 0, 0);
+        }
+      };
+      float4 ar0[NSA], ar1[NSA];
+      unsigned m0_ = 0, m1_ = 0;
+      issue_b(0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      load_a(0, ar0, m0_);
+      load_a(1, ar1, m1_);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // B(0), scale / shift(0), A(0)
+      store_a_from(0, ar0, a_sc, a_sh, m0_);
+      __syncthreads();
+      // iteration kt: B + scale / shift (kt + 1) -> buffer (kt + 1) & 1, A(kt + 2) -> the slot A(kt) left,
+      // MFMAs of kt, then A(kt + 1) from the other slot into LDS; unrolled by two (static slots)
+      int kt = 0;
+      for (; kt + 1 < nkt; kt += 2) {
+        issue_b(kt + 1, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        load_a(kt + 2, ar0, m0_);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(0, 1);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        store_a_from(1, ar1, a_sc, a_sh, m1_);
+        __syncthreads();
+        issue_b(kt + 2, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        load_a(kt + 3, ar1, m1_);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(1, 0);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        store_a_from(0, ar0, a_sc, a_sh, m0_);
+        __syncthreads();
+      }
+      if (kt < nkt) {  // odd k-tile count: the last one (its successors are out of range: zeros)
+        issue_b(kt + 1, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        load_a(kt + 2, ar0, m0_);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(0, 1);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        store_a_from(1, ar1, a_sc, a_sh, m1_);
+        __syncthreads();
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the out-of-range A loads: nothing left in flight
+      return;
+    }
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     store_a(0);
@@ -361,6 +537,60 @@ gemm_x3p_kernel(const GemmArgs args) {
     const float beta = P.beta;
     const int relu = P.relu;
     const long long ldc = P.ldc, c_r1 = P.c_r1, c_s2 = P.c_s2;
+    if constexpr (M16) {
+      // 16x16 blocks: lane l holds rows 4 (l / 16) .. + 3 of column l % 16 of each block
+      const int cl = lane & 15, rq = lane >> 4;
+      float csum4[4], csq4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        csum4[j] = 0.f;
+        csq4[j] = 0.f;
+        const int col = n0 + wn0 + 16 * j + cl;
+        const bool cok = col < N;
+        float bias = 0.f;
+        if (cok) {
+          if (P.bias) bias += P.bias[col];
+          if (P.bias2) bias += P.bias2[col];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = m0 + wm0 + 16 * i + 4 * rq + r;
+            if (cok && row < M) {
+              float* cp = C + remap(row, c_r1, ldc, c_s2) + col;
+              float v = fmaf(acc4[i][j][r], alpha, bias);
+              if (beta != 0.f) v = fmaf(beta, *cp, v);
+              if (relu) v = fmaxf(v, 0.f);
+              *cp = v;
+              csum4[j] += v;
+              csq4[j] = fmaf(v, v, csq4[j]);
+            }
+          }
+      }
+      float* __restrict__ stats = P.stats;
+      if (stats != nullptr) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          csum4[j] += __shfl_xor(csum4[j], 16, 64);
+          csq4[j] += __shfl_xor(csq4[j], 16, 64);
+          csum4[j] += __shfl_xor(csum4[j], 32, 64);
+          csq4[j] += __shfl_xor(csq4[j], 32, 64);
+        }
+        if (rq == 0) {  // the wave's 64 rows are one 64-row slice
+          const long long sl = (m0 + wm0) >> 6;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int col = n0 + wn0 + 16 * j + cl;
+            if (col < N && m0 + wm0 < M) {
+              stats[(sl * N + col) * 2 + 0] = csum4[j];
+              stats[(sl * N + col) * 2 + 1] = csq4[j];
+            }
+          }
+        }
+      }
+      return;
+    }
     float csum[2], csq[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -468,6 +698,14 @@ gemm_x3p_kernel(const GemmArgs args) {
     if (ke < nkt) {
       const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + (long long)blockIdx.x * PART, 0,
                                                         PART * 4, 0x00020000);
+      if constexpr (M16) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_p, acc4[i][j]), rs,
+                                                   ((i * 4 + j) * PNT + tid) * 16, 0, kSc1p);
+      } else {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -481,6 +719,7 @@ gemm_x3p_kernel(const GemmArgs args) {
             v.w = __float_as_uint(acc[i][j][4 * q + 3]);
             __builtin_amdgcn_raw_buffer_store_b128(v, rs, (((i * 2 + j) * 4 + q) * PNT + tid) * 16, 0, kSc1p);
           }
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) __hip_atomic_store(flags + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -503,6 +742,14 @@ gemm_x3p_kernel(const GemmArgs args) {
         __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + b2 * PART, 0, PART * 4, 0x00020000);
+        if constexpr (M16) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc4[i][j] += __builtin_bit_cast(
+                  f32x4_p, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i * 4 + j) * PNT + tid) * 16, 0, kSc1p));
+        } else {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -516,6 +763,7 @@ gemm_x3p_kernel(const GemmArgs args) {
               acc[i][j][4 * q + 2] += __uint_as_float(v.z);
               acc[i][j][4 * q + 3] += __uint_as_float(v.w);
             }
+        }
         if (ub + w2 * U / G <= tb) break;
       }
     }
