@@ -10,7 +10,7 @@ import torch
 
 from ._lib import DstepEpi, DstepSeg
 from ._lib import (CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_GEMM_BF16_IO, CAPMI_GEMM_X3, CAPMI_GEMM_X3P,
-                   CAPMI_GEMM_SPLIT3, CAPMI_GEMM_X3D,
+                   CAPMI_GEMM_SPLIT3, CAPMI_GEMM_X3D, CAPMI_GEMM_X3S,
                    CAPMI_COLSUM_GROUPS, CAPMI_TILE_128, CAPMI_TILE_64,
                    CAPMI_TILE_128x64, CAPMI_TILE_AUTO, GemmProblem, call, lib)
 
@@ -191,6 +191,25 @@ def gemm_x3d(prob, amode, workspace):
     _cuda(workspace, dtype=torch.int32)
     call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3D,
          ptr(workspace), workspace.numel() * 4, stream())
+
+
+def gemm_x3s(prob, amode):
+    """CAPMI_GEMM_X3S: the K = 64 convs (dense rows, or a 1x1 conv input with the optional BN prologue) x
+    B = three bf16 planes (split3_bf16), store-only epilogue; persistent, no workspace."""
+    call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3S,
+         None, 0, stream())
+
+
+def gemm_x3s_ok(prob, amode):
+    """True when CAPMI_GEMM_X3S takes this problem (its planner accepts it)."""
+    v = [ctypes.c_int(0) for _ in range(5)]
+    return lib.capmi_gemm_sk_plan(ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3S,
+                                  *[ctypes.byref(x) for x in v]) == 0
+
+
+def gemm_x3s_kernel_name(prob, amode):
+    ncb = {64: 1, 128: 2, 256: 4}[prob.N]
+    return f"gemm_x3s_kernel<{ncb}, {'true' if prob.in_scale else 'false'}>"
 
 
 def gemm_x3d_kernel_name(prob, amode):

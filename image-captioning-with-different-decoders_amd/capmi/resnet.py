@@ -147,6 +147,8 @@ def pool_dup(H, W, out_hw):
 _X3_SMALLK = int(os.environ.get("CAPMI_X3_SMALLK", "0"))
 # x3 mode: route the shapes where it measured fastest to the x3d kernel (CAPMI_X3D=0: off, A/B)
 _X3D = os.environ.get("CAPMI_X3D", "1") != "0"
+# x3 mode: layer1's K = 64 1x1 convs on the short-k streaming kernel (CAPMI_X3S=0: off, A/B)
+_X3S = os.environ.get("CAPMI_X3S", "1") != "0"
 # train-mode BN finalize fused into the consumer pass where it fits (capmi_bn_finalize_apply), opt-in
 # with CAPMI_BN_FUSE=1: measured slower than the separate finalize launch (headline 5558 -> 5458,
 # bf16 config 10559 -> 9732 img/s)
@@ -275,8 +277,26 @@ class EncoderRunner:
             or (kh == 1 and in_ss is not None and co == 4 * ci and rows <= 12544)))
         x3p = (not nchw and not smallk and not x3d and x3 and in_ss is not None and co >= 128
                and ci % 32 == 0 and Kd >= 128 and rows >= 12544 and a_elems * 6 < (1 << 31))
+        # x3s (round 3): layer1's K = 64 1x1 convs (layer1.0 conv1 / downsample on the pooled stem, every
+        # layer1 conv3 on relu(bn2(y2))) on the short-k streaming kernel (gemm_x3s.hip: weight in VGPRs,
+        # persistent 64-row tiles, two workgroups per CU)
+        x3s = (_X3S and x3 and not nchw and Kd == 64 and kh == 1 and st == 1 and pd == 0 and co in (64, 128, 256))
         if isinstance(in_ss, _DeferredBN) and not x3p:
             in_ss = in_ss.now()  # only the x3p split pass takes the finalize fused
+        if x3s:
+            w3 = self._packed_x3(conv)
+            if in_ss is None:
+                prob, mode = K.problem(rows, co, Kd, x, ci, w3, Kd, out, co, **kw_), CAPMI_A_KMAJOR
+            else:
+                prob = K.problem(rows, co, Kd, x, 0, w3, Kd, out, co, conv=geo, in_scale=in_ss[0],
+                                 in_shift=in_ss[1], **kw_)
+                mode = CAPMI_A_CONV_NHWC
+            launch = lambda: K.gemm_x3s(prob, mode)  # noqa: E731
+            if self.conv_hook is not None:
+                self.conv_hook(tag, 2.0 * rows * co * Kd, launch, K.gemm_x3s_kernel_name(prob, mode))
+            else:
+                launch()
+            return Ho, Wo, rows
         if nchw:
             # conv1: the NCHW images are re-laid out once as NHWC with 4 channels (one float4 per
             # pixel); the implicit GEMM then runs over k = (kh, kw, c4), the 4th channel zero

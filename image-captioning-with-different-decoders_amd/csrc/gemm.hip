@@ -688,6 +688,7 @@ int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gemm
 int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total,
              int& bk);
 int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total);
+int x3s_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long& lda, int& tiles, int& grid);
 }  // namespace
 
 extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, int flags,
@@ -717,6 +718,18 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
     if (bn) *bn = 128;
     if (stream_k) *stream_k = sk ? 1 : 0;
     if (generic) *generic = 32;
+    return 0;
+  }
+  if (flags == CAPMI_GEMM_X3S) {
+    long long lda = 0;
+    int tiles = 0, grid = 0;
+    const int rc = x3s_plan(prob, amode, bmode, lda, tiles, grid);
+    if (rc) return rc;
+    if (threads) *threads = 256;
+    if (bm) *bm = 64;
+    if (bn) *bn = prob->N;
+    if (stream_k) *stream_k = 0;
+    if (generic) *generic = grid;  // CAPMI_GEMM_X3S: the persistent grid
     return 0;
   }
   if (flags == CAPMI_GEMM_X3) {
@@ -823,6 +836,7 @@ int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gemm
   a.p[0] = p;
   a.tiles_m[0] = (int)cdiv(p.M, 128);
   a.tiles_n[0] = (int)cdiv(p.N, bn);
+  a.plain_epi = plain_epilogue(p, bn);
   total = (long long)a.tiles_m[0] * a.tiles_n[0];
   a.tiles_begin[1] = (int)total;
   const long long slots = sk_cus();
@@ -875,6 +889,7 @@ int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
     }();
     a.tile_cols_first = col;
   }
+  a.plain_epi = plain_epilogue(p, 128);
   total = (long long)a.tiles_m[0] * a.tiles_n[0];
   a.tiles_begin[1] = (int)total;
   const long long slots2 = 2LL * sk_cus();
@@ -942,6 +957,7 @@ int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
   a.p[0] = p;
   a.tiles_m[0] = (int)cdiv(p.M, 256);
   a.tiles_n[0] = (int)cdiv(p.N, 128);
+  a.plain_epi = plain_epilogue(p, 128);
   total = (long long)a.tiles_m[0] * a.tiles_n[0];
   a.tiles_begin[1] = (int)total;
   const long long slots = sk_cus();
@@ -972,6 +988,43 @@ int gemm_x3d(const capmi_gemm_problem* prob, int amode, int bmode, void* workspa
   a.sk_flags = static_cast<int*>(workspace);
   a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
   return gemm_x3d_launch(a, amode, a.sk_workers, s);
+}
+
+// CAPMI_GEMM_X3S (gemm_x3s.hip): K = 64, N in {64, 128, 256}, dense rows or a 1x1 / stride-1 conv input
+// (optional prologue), store-only epilogue; grid = two persistent workgroups per CU over 64-row tiles
+int x3s_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long& lda, int& tiles, int& grid) {
+  CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
+  const capmi_gemm_problem& p = *prob;
+  CAPMI_REQUIRE(bmode == CAPMI_B_NMAJOR_W && (amode == CAPMI_A_KMAJOR || amode == CAPMI_A_CONV_NHWC), CAPMI_EINVAL);
+  CAPMI_REQUIRE(p.A && p.B && p.C && p.M >= 0 && p.K == 64 && (p.N == 64 || p.N == 128 || p.N == 256), CAPMI_EINVAL);
+  CAPMI_REQUIRE(plain_epilogue(p, 64) && p.a_r1 <= 0 && (p.in_scale == nullptr) == (p.in_shift == nullptr),
+                CAPMI_EINVAL);
+  if (amode == CAPMI_A_CONV_NHWC) {
+    CAPMI_REQUIRE(p.cKH == 1 && p.cKW == 1 && p.cStride == 1 && p.cPad == 0 && p.cCin == 64 && p.cHo == p.cH &&
+                      p.cWo == p.cW && p.M == p.cN * p.cHo * p.cWo,
+                  CAPMI_EINVAL);
+    lda = p.cCin;
+  } else {
+    CAPMI_REQUIRE(p.in_scale == nullptr, CAPMI_EINVAL);
+    lda = p.lda;
+  }
+  CAPMI_REQUIRE(aligned16(p.A) && aligned16(p.B) && lda % 4 == 0 && lda >= 64 && p.ldb % 8 == 0 && p.ldb >= 64,
+                CAPMI_EALIGN);
+  CAPMI_REQUIRE(p.in_scale == nullptr || (aligned16(p.in_scale) && aligned16(p.in_shift)), CAPMI_EALIGN);
+  CAPMI_REQUIRE((reinterpret_cast<uintptr_t>(p.stats) & 7u) == 0, CAPMI_EALIGN);
+  CAPMI_REQUIRE((long long)p.M * lda * 4 < (1LL << 31) && 3LL * p.N * p.ldb * 2 < (1LL << 31), CAPMI_ERANGE);
+  tiles = (int)cdiv(p.M, 64);
+  grid = (int)std::max<long long>(1, std::min<long long>(tiles, 2LL * cu_count()));
+  return 0;
+}
+
+int gemm_x3s(const capmi_gemm_problem* prob, int amode, int bmode, hipStream_t s) {
+  long long lda = 0;
+  int tiles = 0, grid = 0;
+  const int rc = x3s_plan(prob, amode, bmode, lda, tiles, grid);
+  if (rc) return rc;
+  if (prob->M == 0) return 0;
+  return gemm_x3s_launch(*prob, lda, tiles, grid, s);
 }
 
 int gemm_x3(const capmi_gemm_problem* prob, int amode, int bmode, int tile, void* workspace, long long ws_bytes,
@@ -1007,6 +1060,7 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   if (flags == CAPMI_GEMM_X3) return gemm_x3(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3P) return gemm_x3p(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3D) return gemm_x3d(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
+  if (flags == CAPMI_GEMM_X3S) return gemm_x3s(prob, amode, bmode, as_stream(stream));
   int terms = flag_terms(flags);
   CAPMI_REQUIRE(terms >= 0, CAPMI_EINVAL);
   CAPMI_REQUIRE(terms_mode_ok(terms, amode, bmode), CAPMI_EINVAL);

@@ -20,10 +20,27 @@ struct GemmArgs {
   float* sk_part;        // [workers][BM*BN] parked k-prefix partials
   int* sk_flags;         // [workers + 1], zero between launches; [workers] = spin-timeout flag
   int tile_cols_first;   // x3p: tile t = (tm, tn) as tm = t % tiles_m, tn = t / tiles_m (column-major)
+  // x3 kernels (gemm_x3 / x3p / x3d): the store-only epilogue applies (plain_epilogue() below): C = A.B
+  // stored through one buffer descriptor with per-row 32-bit offsets computed once per tile -- no
+  // per-element 64-bit address, bounds branch, alpha / bias / beta / relu (round 3)
+  int plain_epi;
 };
 
 __device__ __forceinline__ long long remap(long long r, long long r1, long long ld, long long s2) {
   return r1 > 0 ? (r % r1) * ld + (r / r1) * s2 : r * ld;
+}
+
+// Host: does problem p take the store-only epilogue of the x3 kernels with BN-wide column tiles?
+// (C = A.B exactly: no alpha / bias / beta / relu / row remap; whole column tiles; C addressable with
+// 32-bit byte offsets; rows past M read zeros in A, so their accumulators add nothing to the BN sums)
+inline int plain_epilogue(const capmi_gemm_problem& p, int bn) {
+  static const bool off = [] {  // CAPMI_X3_PLAIN_EPI=0: the general epilogue everywhere (A/B arm)
+    const char* e = getenv("CAPMI_X3_PLAIN_EPI");
+    return e && e[0] == '0';
+  }();
+  return !off && p.alpha == 1.f && p.alpha_ptr == nullptr && p.bias == nullptr && p.bias2 == nullptr && p.beta == 0.f &&
+         !p.relu && p.c_r1 <= 0 && p.ksplit == 1 && p.N % bn == 0 && p.ldc >= p.N &&
+         (long long)p.M * p.ldc * 4 < (1LL << 31);
 }
 
 // v2 kernel: A K-major dense / NHWC conv / NHWC4 conv1 / M-major (k rows), B = W[N][K] or k rows;
@@ -41,6 +58,9 @@ int gemm_x3_launch(const GemmArgs& a, int amode, int bn, int blocks, hipStream_t
 int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_t s);
 // x3p with A fp32 split in-kernel ("x3d": register-staged A + optional conv BN prologue, LDS-DMA B)
 int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s);
+// short-k streaming x3 GEMM (gemm_x3s.hip): K = 64, N in {64, 128, 256}, dense rows of lda floats
+// (optional BN prologue), store-only epilogue; persistent grid over 64-row tiles
+int gemm_x3s_launch(const capmi_gemm_problem& p, long long lda, int tiles, int grid, hipStream_t s);
 // resident workgroups per CU of the NT kernel for a tile shape (LDS / register bound)
 // (terms 3: three bf16 LDS planes per operand, 60 KB for 64x64 and >= 90 KB for the larger tiles)
 inline int gemm_nt_wg_per_cu(int bm, int bn, int terms = 0) {

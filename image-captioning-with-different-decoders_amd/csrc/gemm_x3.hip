@@ -323,6 +323,34 @@ gemm_x3_kernel(const GemmArgs args) {
     auto scol = [&](int j) { return X3_M16 ? 16 * j + (lane & 15) : 32 * j + lr; };
     if constexpr (X3_M16) {
       const int rq = lane >> 4;
+      if (args.plain_epi) {
+        // store-only form (host: plain_epilogue): row offsets once per tile, column block as an
+        // immediate offset; rows past M are dropped by the descriptor (their accumulators are 0)
+        const auto rc = rsrc_x(C, (unsigned)((long long)M * ldc * 4));
+        unsigned roff[2][4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = m0 + wm0 + 16 * i + 4 * rq + r;
+            roff[i][r] = row < M ? (unsigned)row * (unsigned)ldc * 4u : kOOBx;
+          }
+        const unsigned cb = (unsigned)(n0 + wn0 + (lane & 15)) * 4u;
+#pragma unroll
+        for (int j = 0; j < TN16; ++j) {
+          csum[j] = 0.f;
+          csq[j] = 0.f;
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = acc4[i][j][r];
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, roff[i][r] + cb + 64u * j, 0, 0);
+              csum[j] += v;
+              csq[j] = fmaf(v, v, csq[j]);
+            }
+        }
+      } else
 #pragma unroll
       for (int j = 0; j < TN16; ++j) {
         csum[j] = 0.f;

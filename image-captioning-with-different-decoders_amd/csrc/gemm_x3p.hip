@@ -541,6 +541,34 @@ gemm_x3p_kernel(const GemmArgs args) {
       // 16x16 blocks: lane l holds rows 4 (l / 16) .. + 3 of column l % 16 of each block
       const int cl = lane & 15, rq = lane >> 4;
       float csum4[4], csq4[4];
+      if (args.plain_epi) {
+        // store-only form (host: plain_epilogue): 16 row offsets per lane computed once, the 64 stores
+        // take the column block as an immediate offset; rows past M are dropped by the descriptor
+        const auto rc = rsrc_p(C, (unsigned)((long long)M * ldc * 4));
+        unsigned roff[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = m0 + wm0 + 16 * i + 4 * rq + r;
+            roff[i][r] = row < M ? (unsigned)row * (unsigned)ldc * 4u : kOOBp;
+          }
+        const unsigned cb = (unsigned)(n0 + wn0 + cl) * 4u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          csum4[j] = 0.f;
+          csq4[j] = 0.f;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = acc4[i][j][r];
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, roff[i][r] + cb + 64u * j, 0, 0);
+              csum4[j] += v;
+              csq4[j] = fmaf(v, v, csq4[j]);
+            }
+        }
+      } else
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         csum4[j] = 0.f;

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 16
+#define CAPMI_ABI_VERSION 17
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -138,6 +138,13 @@ int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int t
  * split into the three bf16 planes in-kernel while B (pre-split, x3p k order) is LDS-DMA staged;
  * 256x128 tiles, k-tiles of 32, one workgroup per CU, stream-K as capmi_gemm_sk. */
 #define CAPMI_GEMM_X3D 32
+/* CAPMI_GEMM_X3S (alone, ABI 17): the CAPMI_GEMM_X3 arithmetic for the short-k convs (layer1's K = 64):
+ * K == 64, N in {64, 128, 256}; A fp32 dense rows (CAPMI_A_KMAJOR, lda % 4 == 0) or a 1x1 / stride-1 /
+ * unpadded NHWC conv input with Cin == 64 (CAPMI_A_CONV_NHWC, optional BN-apply + ReLU prologue); B the
+ * three bf16 planes of capmi_split3_bf16 (ldb % 8 == 0); C = A.B only (alpha 1, no bias / beta / relu /
+ * remap / ksplit) with the optional `stats`. Persistent 256-thread workgroups (two per CU) stream 64-row
+ * tiles with the weight held in registers; the workspace is not used (may be NULL). */
+#define CAPMI_GEMM_X3S 64
 /* CAPMI_GEMM_SPLIT3 (alone): fp32 A and B, both split exactly into three bf16 terms when staged to
  * LDS (the CAPMI_GEMM_X3 arithmetic with no pre-split operand: fp32-accurate on the bf16 matrix
  * cores). Dense modes only: CAPMI_A_KMAJOR x CAPMI_B_NMAJOR_W / CAPMI_B_KROWS and CAPMI_A_MMAJOR x

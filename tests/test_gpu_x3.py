@@ -268,3 +268,45 @@ def test_encoder_x3_oversize_batch_routes_to_fp32():
     torch.cuda.synchronize()
     assert torch.isfinite(y3).all()
     assert rel_err(y3, y1) < 5e-3, rel_err(y3, y1)
+
+
+@pytest.mark.parametrize("N,H,Cout,pro,lda", [
+    (2, 56, 256, True, 0), (2, 56, 64, False, 0), (1, 11, 256, True, 0), (3, 7, 128, False, 80),
+    (1, 9, 64, True, 0), (64, 56, 256, True, 0), (64, 56, 64, False, 64)])
+def test_x3s_short_k(N, H, Cout, pro, lda):
+    """The short-k streaming kernel (CAPMI_GEMM_X3S, layer1's K = 64 convs): the 1x1 conv of
+    relu(x*s+b) (or dense rows of stride lda) vs fp64 under the x3 rule, the BN statistics of the
+    stored output, and nothing written past row M (NaN sentinel rows after C)."""
+    K = _K()
+    Cin = 64
+    rows = N * H * H
+    x = rnd(rows, max(lda, Cin), seed=31)
+    w = rnd(Cout, Cin, seed=32) * (2.0 / Cin) ** 0.5
+    s, b = rnd(Cin, seed=33) + 1.0, rnd(Cin, seed=34)
+    xin = torch.relu(torch.addcmul(b, x[:, :Cin], s)) if pro else x[:, :Cin]
+    stats = torch.zeros(2 * K.stat_tiles(rows) * Cout, device=DEV)
+    buf = torch.full((rows + 64, Cout), float("nan"), device=DEV)
+    out = buf[:rows]
+    xd = x.to(DEV).contiguous()
+    if lda:
+        prob, mode = K.problem(rows, Cout, Cin, xd, lda, split3(w.to(DEV)), Cin, out, Cout, stats=stats), 0
+    else:
+        geo = dict(N=N, H=H, W=H, Cin=Cin, KH=1, KW=1, stride=1, pad=0, Ho=H, Wo=H)
+        prob = K.problem(rows, Cout, Cin, xd, 0, split3(w.to(DEV)), Cin, out, Cout, conv=geo, stats=stats,
+                         in_scale=s.to(DEV) if pro else None, in_shift=b.to(DEV) if pro else None)
+        mode = 2
+    assert K.gemm_x3s_ok(prob, mode)
+    K.gemm_x3s(prob, mode)
+    torch.cuda.synchronize()
+    ref = xin.double() @ w.double().T
+    ref_abs = xin.double().abs() @ w.double().abs().T
+    r3, _ = _errs(out, ref, ref_abs)
+    assert r3 <= 1.0, r3
+    assert bool(torch.isnan(buf[rows:]).all()), "x3s wrote past row M"
+    o = out.double().cpu()
+    st = stats.double().cpu().view(-1, Cout, 2)
+    torch.testing.assert_close(st[..., 0].sum(0), o.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(st[..., 1].sum(0), (o * o).sum(0), rtol=1e-5, atol=1e-3)
+    # each 64-row slice's statistics are that slice's sums (what bn_finalize reads)
+    sl = torch.nn.functional.pad(o, (0, 0, 0, (-rows) % 64)).view(-1, 64, Cout)
+    torch.testing.assert_close(st[..., 0], sl.sum(1), rtol=1e-5, atol=1e-4)

@@ -76,7 +76,7 @@ def test_gemm_sk_plan_on_host():
     assert rc == 0 and (bm, bn, generic, nt) == (128, 128, 0, 512)
     assert plan(64)[1][4] == 256
     assert plan(256, flags=1)[1][4] == 256
-    assert plan(256, flags=64)[0] == 1001  # unknown flag
+    assert plan(256, flags=128)[0] == 1001  # unknown flag
     assert plan(256, flags=1 | 16)[0] == 1001  # flags do not combine
     # CAPMI_GEMM_SPLIT3 (16) on a conv: the 256-thread split-staged kernel, two workgroups per CU
     # for 64x64 (stream-K sized for that)
@@ -93,6 +93,28 @@ def test_gemm_sk_plan_on_host():
     rc, (bm, bn, sk, generic, nt) = plan(256, flags=8, M=200704)
     assert rc == 0 and (bm, bn, generic, nt) == (256, 128, 16, 512) and sk == 0
     assert plan(256, flags=8, Cin=20)[0] == 1001  # Cin % 32 != 0
+    # CAPMI_GEMM_X3S (64, ABI 17): K = 64 only -- the 3x3 conv above is rejected; a 1x1 layer1 conv3 with
+    # the BN prologue (M = 200704, N = 256) gets 64-row tiles, 256 threads, no stream-K, the persistent
+    # grid (two workgroups per CU) in `generic`
+    assert plan(256, flags=64)[0] == 1001
+
+    def x3s_plan(N, M=200704, alpha=1.0, beta=0.0):
+        p = GemmProblem()
+        p.M, p.N, p.K, p.ksplit = M, N, 64, 1
+        p.A = p.B = p.C = p.in_scale = p.in_shift = 256
+        p.ldb, p.ldc, p.alpha, p.beta = 64, N, alpha, beta
+        p.cN, p.cH, p.cW, p.cCin, p.cKH, p.cKW = M // 3136, 56, 56, 64, 1, 1
+        p.cStride, p.cPad, p.cHo, p.cWo = 1, 0, 56, 56
+        v = [c_int(0) for _ in range(5)]
+        rc = lib.capmi_gemm_sk_plan(ctypes.byref(p), 2, 0, 3, 64, *[ctypes.byref(x) for x in v])
+        return rc, tuple(x.value for x in v)
+
+    rc, (bm, bn, sk, grid, nt) = x3s_plan(256)
+    assert rc == 0 and (bm, bn, sk, nt) == (64, 256, 0, 256) and grid == 512  # 256 CUs with no GPU attached
+    assert x3s_plan(64)[0] == 0 and x3s_plan(64)[1][1] == 64
+    assert x3s_plan(512)[0] == 1001  # N outside {64, 128, 256}
+    assert x3s_plan(256, beta=1.0)[0] == 1001  # not the store-only epilogue
+    assert x3s_plan(256, M=3136)[1][3] == 49  # one image: grid = tiles when fewer than two per CU
 
     def wgrad_plan(Cout, Cin, k):
         # dW[Cout, (kh, kw, ci)] over k = 64*14*14 output pixels (A_MMAJOR x B_CONV_NHWC)

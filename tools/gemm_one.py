@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--nopro", action="store_true", help="drop the BN-apply+ReLU prologue (1x1: dense A)")
     ap.add_argument("--x3", action="store_true", help="fp32-accurate three-term bf16 split GEMM (CAPMI_GEMM_X3)")
     ap.add_argument("--x3p", action="store_true", help="x3 with the A operand pre-split too (CAPMI_GEMM_X3P)")
+    ap.add_argument("--x3d", action="store_true", help="x3 with the fp32 A split in-kernel, B by LDS-DMA (CAPMI_GEMM_X3D)")
+    ap.add_argument("--x3s", action="store_true", help="short-k streaming x3 kernel (gemm_x3s.hip)")
     a = ap.parse_args()
     dev = "cuda"
     ci, H, W, co, k, pro, *st = SHAPES[a.shape]
@@ -79,6 +81,18 @@ def main():
             prob, mode = K.problem(M, co, Kd, xp, 0, w3, Kd, y, co, conv=geo, stats=stats), CAPMI_A_CONV_NHWC
         print("x3p kernel:", K.gemm_x3p_kernel_name(prob, mode))
         run = lambda: K.gemm_x3p(prob, mode, ws)  # noqa: E731
+    elif a.x3d:
+        w3 = torch.empty(3 * w.numel(), device=dev, dtype=torch.bfloat16)
+        K.split3_bf16(K.conv_weight_order_x3p(w, k, k, ci).contiguous(), w3)
+        prob.B = w3.data_ptr()
+        print("x3d kernel:", K.gemm_x3d_kernel_name(prob, mode))
+        run = lambda: K.gemm_x3d(prob, mode, ws)  # noqa: E731
+    elif a.x3s:
+        w3 = torch.empty(3 * w.numel(), device=dev, dtype=torch.bfloat16)
+        K.split3_bf16(w, w3)
+        prob.B = w3.data_ptr()
+        print("x3s kernel:", K.gemm_x3s_kernel_name(prob, mode))
+        run = lambda: K.gemm_x3s(prob, mode)  # noqa: E731
     elif a.x3:
         w3 = torch.empty(3 * w.numel(), device=dev, dtype=torch.bfloat16)
         K.split3_bf16(w, w3)

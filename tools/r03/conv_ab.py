@@ -20,6 +20,8 @@ def routed(tag, rows, Cin, Cout, k, st, pro):
     """The kernel EncoderRunner._conv picks for this shape in the x3 mode (resnet.py)."""
     kd = k * k * Cin
     in_ss = pro
+    if kd == 64 and k == 1 and st == 1 and Cout in (64, 128, 256) and os.environ.get("CAPMI_X3S", "1") != "0":
+        return "x3s"
     if Cin % 32 == 0 and kd % 32 == 0 and (st == 2 or (k == 1 and not in_ss and Cin == 2 * Cout)
                                            or (rows <= 3136 and not (k == 1 and not in_ss))
                                            or (k == 1 and in_ss and Cout == 4 * Cin and rows <= 12544)):
@@ -32,7 +34,7 @@ def routed(tag, rows, Cin, Cout, k, st, pro):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--arms", default="x3,x3d,x3p")
+    ap.add_argument("--arms", default="x3,x3d,x3p,x3s")
     ap.add_argument("--only", default="")
     a = ap.parse_args()
     arms_on = a.arms.split(",")
@@ -65,11 +67,16 @@ def main():
             K.split3_bf16(w, w3)
             p3 = K.problem(rows, Cout, Kd, x, Cin if dense else 0, w3, Kd, out, Cout, **kw)
             fns["x3"] = lambda: K.gemm_x3(p3, mode, ws)
+        w3s = torch.empty(3 * w.numel(), device=dev, dtype=torch.bfloat16)
+        K.split3_bf16(w, w3s)
         w3d = torch.empty(3 * w.numel(), device=dev, dtype=torch.bfloat16)
         K.split3_bf16(K.conv_weight_order_x3p(w, k, k, Cin).contiguous(), w3d)
         if "x3d" in arms_on and Cin % 32 == 0:
             pd = K.problem(rows, Cout, Kd, x, Cin if dense else 0, w3d, Kd, out, Cout, **kw)
             fns["x3d"] = lambda: K.gemm_x3d(pd, mode, ws)
+        if "x3s" in arms_on and Kd == 64 and k == 1 and st == 1 and Cout in (64, 128, 256):
+            ps = K.problem(rows, Cout, Kd, x, Cin if dense else 0, w3s, Kd, out, Cout, **kw)
+            fns["x3s"] = lambda: K.gemm_x3s(ps, mode)
         if "x3p" in arms_on and Cin % 32 == 0 and Kd >= 128:
             xp = torch.empty(3 * x.numel(), device=dev, dtype=torch.bfloat16)
             if k == 1 and st == 1:
