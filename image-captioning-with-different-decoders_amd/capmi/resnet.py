@@ -149,6 +149,24 @@ _X3_SMALLK = int(os.environ.get("CAPMI_X3_SMALLK", "0"))
 _X3D = os.environ.get("CAPMI_X3D", "1") != "0"
 # x3 mode: layer1's K = 64 1x1 convs on the short-k streaming kernel (CAPMI_X3S=0: off, A/B)
 _X3S = os.environ.get("CAPMI_X3S", "1") != "0"
+# x3 mode, opt-in (CAPMI_X3_TAIL=1): a bottleneck tail relu(bn3(y3) + identity) whose output feeds the next
+# block's conv1 (a plain gemm_x3 1x1) is computed in that GEMM's A staging, which also stores the block
+# output -- bit-identical, but measured slower than the separate capmi_bn_add_relu pass (5959 vs 6138 img/s,
+# same box: the GEMM's second column tile re-reads both tail operands and its A staging doubles)
+_X3_TAIL = os.environ.get("CAPMI_X3_TAIL", "0") == "1"
+
+
+class _Tail:
+    """A deferred bottleneck tail out = relu(y*s + b + res') with res' = res*rs + rb (downsample BN) or
+    res: the arguments of capmi_bn_add_relu, run as the next conv1's fused prologue or, when that conv
+    cannot take it, materialised just before it (``now``)."""
+
+    def __init__(self, y, s, b, res, out, rows, C, rs=None, rb=None):
+        self.y, self.s, self.b, self.res, self.out, self.rows, self.C, self.rs, self.rb = y, s, b, res, out, rows, C, rs, rb
+
+    def now(self):
+        K.bn_add_relu(self.y, self.s, self.b, self.res, self.out, self.rows, self.C, res_scale=self.rs,
+                      res_shift=self.rb)
 # train-mode BN finalize fused into the consumer pass where it fits (capmi_bn_finalize_apply), opt-in
 # with CAPMI_BN_FUSE=1: measured slower than the separate finalize launch (headline 5558 -> 5458,
 # bf16 config 10559 -> 9732 img/s; DESIGN.md 4.7)
@@ -247,7 +265,7 @@ class EncoderRunner:
             return _DeferredBN(self, ws, bn, rows)
         return self._bn(ws, bn, rows, train)
 
-    def _conv(self, tag, x, conv, out, N, H, W, train, in_ss=None, nchw=False):
+    def _conv(self, tag, x, conv, out, N, H, W, train, in_ss=None, nchw=False, tail=None):
         co, ci, kh, kw = conv.weight.shape
         st, pd = conv.stride[0], conv.padding[0]
         Ho, Wo = (H + 2 * pd - kh) // st + 1, (W + 2 * pd - kw) // st + 1
@@ -283,6 +301,10 @@ class EncoderRunner:
         x3s = (_X3S and x3 and not nchw and Kd == 64 and kh == 1 and st == 1 and pd == 0 and co in (64, 128, 256))
         if isinstance(in_ss, _DeferredBN) and not x3p:
             in_ss = in_ss.now()  # only the x3p split pass takes the finalize fused
+        if tail is not None and not (x3 and not x3s and not x3d and not x3p and not smallk and not nchw and kh == 1
+                                     and st == 1 and in_ss is None and Kd % 32 == 0 and Kd == ci):
+            tail.now()  # this conv cannot take the fused tail: the block output first
+            tail = None
         if x3s:
             w3 = self._packed_x3(conv)
             if in_ss is None:
@@ -355,7 +377,11 @@ class EncoderRunner:
         elif kh == 1 and st == 1 and in_ss is None:
             if x3 and Kd % 32 == 0:
                 w = self._packed_x3(conv)
-            prob = K.problem(rows, co, Kd, x, ci, w, Kd, out, co, **kw_)
+            if tail is not None:  # x (= tail.out) is written by this GEMM from the tail's operands
+                prob = K.problem(rows, co, Kd, tail.y, ci, w, Kd, out, co, in_scale=tail.s, in_shift=tail.b,
+                                 in_res=tail.res, in_res_scale=tail.rs, in_res_shift=tail.rb, in_out=tail.out, **kw_)
+            else:
+                prob = K.problem(rows, co, Kd, x, ci, w, Kd, out, co, **kw_)
             mode = CAPMI_A_KMAJOR
         else:
             sc, sh = in_ss if in_ss is not None else (None, None)
@@ -532,12 +558,20 @@ class EncoderRunner:
         bns = []
         direct = out_hw is None and out is not None
         n4 = len(net.layer4)
+        tail = None  # the previous block's deferred tail (its output x not yet written)
         for li in range(1, 5):
-            for bi, blk in enumerate(getattr(net, f"layer{li}")):
+            layer = getattr(net, f"layer{li}")
+            for bi, blk in enumerate(layer):
                 if direct and li == 4 and bi == n4 - 1:
                     xo = out  # the last block's output is the result
                 tag = f"layer{li}.{bi}"
-                _, _, r1 = self._conv(tag + ".conv1", x, blk.conv1, ws["y1"], N, H, W, train)
+                if tail is not None and blk.downsample is not None:
+                    tail.now()  # (never: only a block followed by one of its own layer defers)
+                    tail = None
+                _, _, r1 = self._conv(tag + ".conv1", x, blk.conv1, ws["y1"], N, H, W, train, tail=tail)
+                tail = None
+                # this block's tail may ride in the next block's conv1 (same layer: no downsample reads x)
+                defer = self.x3 and _X3_TAIL and bi + 1 < len(layer)
                 # (layer3/4: the finalize of bn1 / bn2 rides in the consumer's pass, _bn_defer)
                 ss1 = self._bn_defer(ws, blk.bn1, r1, train)
                 H2, W2, r2 = self._conv(tag + ".conv2", ws["y1"], blk.conv2, ws["y2"], N, H, W, train, in_ss=ss1)
@@ -548,14 +582,17 @@ class EncoderRunner:
                     s3, b3 = self._bn(ws, blk.bn3, r3, train)  # (the downsample conv reuses the stats buffer)
                     self._conv(tag + ".downsample", x, blk.downsample[0], ws["yd"], N, H, W, train)
                     sd, bd = self._bn(ws, blk.downsample[1], r3, train)
-                    K.bn_add_relu(ws["y3"], s3, b3, ws["yd"], xo, r3, Cout, res_scale=sd, res_shift=bd)
+                    tail = _Tail(ws["y3"], s3, b3, ws["yd"], xo, r3, Cout, rs=sd, rb=bd)
                     bns.append(blk.downsample[1])
                 else:
                     d3 = self._bn_defer(ws, blk.bn3, r3, train)
                     if isinstance(d3, _DeferredBN):
                         d3.apply(CAPMI_BNFA_ADD_RELU, ws["y3"], xo, res=x)
                     else:
-                        K.bn_add_relu(ws["y3"], d3[0], d3[1], x, xo, r3, Cout)
+                        tail = _Tail(ws["y3"], d3[0], d3[1], x, xo, r3, Cout)
+                if tail is not None and not defer:
+                    tail.now()
+                    tail = None
                 bns += [blk.bn1, blk.bn2, blk.bn3]
                 x, xo = xo, x
                 H, W, Cx = H2, W2, Cout

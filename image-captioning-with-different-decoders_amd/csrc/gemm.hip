@@ -398,6 +398,9 @@ int gemm_plan(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, 
   CAPMI_REQUIRE(bmode != 2 || amode == 1, CAPMI_EINVAL);
   CAPMI_REQUIRE(tile >= CAPMI_TILE_128 && tile <= CAPMI_TILE_128_W8, CAPMI_EINVAL);
   CAPMI_REQUIRE(amode != 4 || bmode == 0, CAPMI_EINVAL);
+  for (int i = 0; i < nprob; ++i)  // the fused bottleneck tail is a CAPMI_GEMM_X3 form only (ABI 18)
+    CAPMI_REQUIRE(!probs[i].in_res && !probs[i].in_out && !probs[i].in_res_scale && !probs[i].in_res_shift,
+                  CAPMI_EINVAL);
   GemmArgs& a = g.a;
   memset(&a, 0, sizeof(a));
   a.nprob = nprob;
@@ -817,11 +820,19 @@ int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gemm
   const capmi_gemm_problem& p = *prob;
   CAPMI_REQUIRE(bmode == CAPMI_B_NMAJOR_W && (amode == CAPMI_A_KMAJOR || amode == CAPMI_A_CONV_NHWC), CAPMI_EINVAL);
   CAPMI_REQUIRE(p.A && p.B && p.C && p.M >= 0 && p.N > 0 && p.K > 0 && p.K % 32 == 0 && p.ksplit == 1, CAPMI_EINVAL);
-  CAPMI_REQUIRE(amode == CAPMI_A_CONV_NHWC || (!p.in_scale && !p.in_shift), CAPMI_EINVAL);
+  // dense A takes a prologue only as the fused bottleneck tail (in_res + in_out, ABI 18)
+  const bool tail = p.in_res != nullptr;
+  CAPMI_REQUIRE(amode == CAPMI_A_CONV_NHWC || tail || (!p.in_scale && !p.in_shift), CAPMI_EINVAL);
+  CAPMI_REQUIRE(!tail || (amode == CAPMI_A_KMAJOR && p.in_scale && p.in_out && p.lda == p.K), CAPMI_EINVAL);
+  CAPMI_REQUIRE(tail || (!p.in_out && !p.in_res_scale && !p.in_res_shift), CAPMI_EINVAL);
+  CAPMI_REQUIRE((p.in_res_scale == nullptr) == (p.in_res_shift == nullptr), CAPMI_EINVAL);
   CAPMI_REQUIRE((p.in_scale == nullptr) == (p.in_shift == nullptr), CAPMI_EINVAL);
   CAPMI_REQUIRE(p.stats == nullptr || p.c_r1 <= 0, CAPMI_EINVAL);
   CAPMI_REQUIRE(aligned16(p.A) && aligned16(p.B) && p.ldb % 8 == 0 && p.ldb >= p.K, CAPMI_EALIGN);
   CAPMI_REQUIRE(p.in_scale == nullptr || (aligned16(p.in_scale) && aligned16(p.in_shift)), CAPMI_EALIGN);
+  CAPMI_REQUIRE(!tail || (aligned16(p.in_res) && aligned16(p.in_out) &&
+                          (p.in_res_scale == nullptr || (aligned16(p.in_res_scale) && aligned16(p.in_res_shift)))),
+                CAPMI_EALIGN);
   CAPMI_REQUIRE(3LL * p.N * p.ldb * 2 < (1LL << 31), CAPMI_ERANGE);
   if (amode == CAPMI_A_CONV_NHWC) {
     CAPMI_REQUIRE(p.cCin % 32 == 0 && p.K == p.cKH * p.cKW * p.cCin && p.M == p.cN * p.cHo * p.cWo, CAPMI_EINVAL);
@@ -1056,6 +1067,9 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
                                 void* workspace, long long ws_bytes, void* stream) {
   GemmPlan g;
   bool sk = false;
+  CAPMI_REQUIRE(prob == nullptr || flags == CAPMI_GEMM_X3 ||
+                    (!prob->in_res && !prob->in_out && !prob->in_res_scale && !prob->in_res_shift),
+                CAPMI_EINVAL);  // the fused bottleneck tail: CAPMI_GEMM_X3 only
   if (flags == CAPMI_GEMM_BF16_IO) return gemm_bf16_io(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3) return gemm_x3(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3P) return gemm_x3p(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 17
+#define CAPMI_ABI_VERSION 18
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -78,6 +78,16 @@ typedef struct capmi_gemm_problem {
   int cN, cH, cW, cCin, cKH, cKW, cStride, cPad, cHo, cWo;
   const float* in_scale; /* NULL or [Cin]: A element := relu(x*in_scale[ci] + in_shift[ci]) in-bounds (BN-apply+ReLU prologue) */
   const float* in_shift;
+  /* ABI 18, CAPMI_GEMM_X3 with CAPMI_A_KMAJOR only (the fused bottleneck tail, models/encoder.py:88-91
+   * via torchvision's Bottleneck.forward "out += identity; out = relu(out)"): when in_res is set, A
+   * element (m, k) := relu(fma(A, in_scale[k], in_shift[k]) + r), r = in_res[m][k] (lda-strided) or
+   * fma(in_res, in_res_scale[k], in_res_shift[k]) (downsample BN) -- the capmi_bn_add_relu formula, bit
+   * for bit -- and the workgroups of the first column tile also store it to in_out[m][k] (the block
+   * output, the next tail's residual); in_scale, in_shift and in_out are then required. NULL: unused. */
+  const float* in_res;
+  const float* in_res_scale;
+  const float* in_res_shift;
+  float* in_out;
 } capmi_gemm_problem;
 
 int capmi_gemm(const capmi_gemm_problem* problems, int nprob, int amode, int bmode, int tile,

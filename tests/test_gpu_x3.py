@@ -310,3 +310,65 @@ def test_x3s_short_k(N, H, Cout, pro, lda):
     # each 64-row slice's statistics are that slice's sums (what bn_finalize reads)
     sl = torch.nn.functional.pad(o, (0, 0, 0, (-rows) % 64)).view(-1, 64, Cout)
     torch.testing.assert_close(st[..., 0], sl.sum(1), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("M,C,N,rbn", [(12544, 1024, 256, False), (12544, 1024, 256, True), (50176, 512, 128, False),
+                                       (200704, 256, 64, True), (777, 256, 64, False), (3136, 2048, 512, False)])
+def test_x3_fused_tail_bit_identical(M, C, N, rbn):
+    """gemm_x3 dense with the fused bottleneck tail (in_res, ABI 18) == capmi_bn_add_relu followed by the
+    plain gemm_x3, bit for bit: the block output it stores (in_out), the GEMM output and the BN statistics;
+    stream-K (M = 12544) and data-parallel grids, a ragged M, and the downsample-BN residual (rbn)."""
+    K = _K()
+    y, res = rnd(M, C, seed=41).to(DEV), rnd(M, C, seed=42).to(DEV)
+    s, b = (rnd(C, seed=43) + 1.0).to(DEV), rnd(C, seed=44).to(DEV)
+    rs, rb = ((rnd(C, seed=45) + 1.0).to(DEV), rnd(C, seed=46).to(DEV)) if rbn else (None, None)
+    w3 = split3((rnd(N, C, seed=47) * (2.0 / C) ** 0.5).to(DEV))
+    ws = K.gemm_workspace(DEV)
+    # reference: the separate tail pass, then the plain GEMM on its output
+    x_ref = torch.empty(M, C, device=DEV)
+    K.bn_add_relu(y, s, b, res, x_ref, M, C, res_scale=rs, res_shift=rb)
+    c_ref = torch.empty(M, N, device=DEV)
+    st_ref = torch.zeros(2 * K.stat_tiles(M) * N, device=DEV)
+    K.gemm_x3(K.problem(M, N, C, x_ref, C, w3, C, c_ref, N, stats=st_ref), 0, ws)
+    # fused
+    x_f = torch.full((M, C), float("nan"), device=DEV)
+    c_f = torch.empty(M, N, device=DEV)
+    st_f = torch.zeros(2 * K.stat_tiles(M) * N, device=DEV)
+    K.gemm_x3(K.problem(M, N, C, y, C, w3, C, c_f, N, stats=st_f, in_scale=s, in_shift=b, in_res=res,
+                        in_res_scale=rs, in_res_shift=rb, in_out=x_f), 0, ws)
+    torch.cuda.synchronize()
+    K.sk_check([ws])
+    assert torch.equal(x_f, x_ref)
+    assert torch.equal(c_f, c_ref)
+    assert torch.equal(st_f, st_ref)
+
+
+def test_encoder_x3_fused_tails_bit_identical():
+    """The x3 train-mode encoder with its bottleneck tails fused into the next conv1 (CAPMI_X3_TAIL default)
+    equals the one with separate capmi_bn_add_relu passes bit for bit (features and BN running stats)."""
+    import gen
+    from helpers import t
+    from capmi import resnet as R
+    net = R.ResNet101()
+    sd = net.state_dict()
+    for k_, v in gen.resnet101_params(81).items():
+        sd[k_] = t(v).clone()
+    net.load_state_dict(sd)
+    net = net.to(DEV).train()
+    x = t(gen.images(81, 4), DEV).contiguous()
+    outs = []
+    for fused in (True, False):
+        old = R._X3_TAIL
+        R._X3_TAIL = fused
+        try:
+            net.load_state_dict(sd)
+            r = R.EncoderRunner()
+            r.x3 = True
+            with torch.no_grad():
+                y = r.forward(net, x, out_hw=(14, 14))
+            torch.cuda.synchronize()
+            outs.append((y.cpu(), net.layer3[5].bn3.running_var.cpu().clone()))
+        finally:
+            R._X3_TAIL = old
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
