@@ -121,17 +121,19 @@ def gemm_sk(prob, amode, workspace, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W
          workspace.numel() * 4, stream())
 
 
-def problem_bf16(M, N, K, A, lda, B, ldb, C, ldc, *, stats=None, conv=None):
+def problem_bf16(M, N, K, A, lda, B, ldb, C, ldc, *, stats=None, conv=None, in_scale=None, in_shift=None):
     """capmi_gemm_problem over bf16 A / B / C (CAPMI_GEMM_BF16_IO): plain conv or dense GEMM,
-    fp32 BN statistics of the stored (bf16) output."""
+    fp32 BN statistics of the stored (bf16) output; in_scale / in_shift (fp32 [Cin]): the input's
+    BN-apply + ReLU in the A staging (bf16 RNE, capmi_bn_relu_bf16's arithmetic; round 3)."""
     _cuda(A, B, C, dtype=torch.bfloat16)
-    _cuda(stats)
+    _cuda(stats, in_scale, in_shift)
     p = GemmProblem()
     p.M, p.N, p.K, p.ksplit = int(M), int(N), int(K), 1
     p.A, p.lda, p.B, p.ldb = ptr(A), int(lda), ptr(B), int(ldb)
     p.C, p.ldc = ptr(C), int(ldc)
     p.alpha, p.beta = 1.0, 0.0
     p.stats = ptr(stats)
+    p.in_scale, p.in_shift = ptr(in_scale), ptr(in_shift)
     if conv is not None:
         p.cN, p.cH, p.cW, p.cCin = conv["N"], conv["H"], conv["W"], conv["Cin"]
         p.cKH, p.cKW, p.cStride, p.cPad = conv["KH"], conv["KW"], conv["stride"], conv["pad"]
@@ -221,14 +223,14 @@ def gemm_x3d_kernel_name(prob, amode):
     call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3D,
          *[ctypes.byref(x) for x in v])
     b = lambda x: "true" if x else "false"  # noqa: E731
-    return f"gemm_x3p_kernel<{amode}, {b(v[2].value)}, 32, true, {b(bool(prob.in_scale))}>"
+    return f"gemm_x3p_kernel<{amode}, {b(v[2].value)}, 32, true, {b(bool(prob.in_scale))}, 128>"
 
 
 def gemm_x3p_kernel_name(prob, amode):
     v = [ctypes.c_int(0) for _ in range(5)]
     call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3P,
          *[ctypes.byref(x) for x in v])
-    return f"gemm_x3p_kernel<{amode}, {'true' if v[2].value else 'false'}, {v[3].value}, false, false>"
+    return f"gemm_x3p_kernel<{amode}, {'true' if v[2].value else 'false'}, {v[3].value}, false, false, {v[1].value}>"
 
 
 def gemm_x3_kernel_name(prob, amode, tile=CAPMI_TILE_AUTO):

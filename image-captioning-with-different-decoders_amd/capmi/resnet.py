@@ -147,6 +147,11 @@ def pool_dup(H, W, out_hw):
 _X3_SMALLK = int(os.environ.get("CAPMI_X3_SMALLK", "0"))
 # x3 mode: route the shapes where it measured fastest to the x3d kernel (CAPMI_X3D=0: off, A/B)
 _X3D = os.environ.get("CAPMI_X3D", "1") != "0"
+# bf16 encoder, opt-in: the conv input's BN-apply + ReLU in the consumer GEMM's A staging instead of a
+# capmi_bn_relu_bf16 pass (bit mask: 1 = conv2's input, 2 = conv3's input). Bit-identical, measured slower on
+# config 5 (same box: 10224 img/s with the passes, 10124 with conv3's folded, 9744 with both): at bf16 MFMA
+# rates the per-element unpack / fma / max / pack VALU in the staging costs more than the pass it saves
+_BF16_FOLD = int(os.environ.get("CAPMI_BF16_FOLD", "0"))
 # x3 mode: layer1's K = 64 1x1 convs on the short-k streaming kernel (CAPMI_X3S=0: off, A/B)
 _X3S = os.environ.get("CAPMI_X3S", "1") != "0"
 # x3 mode, opt-in (CAPMI_X3_TAIL=1): a bottleneck tail relu(bn3(y3) + identity) whose output feeds the next
@@ -442,8 +447,9 @@ class EncoderRunner:
             self.packed.cache[key] = ent
         return ent[2]
 
-    def _conv_bf16(self, tag, x, conv, out, N, H, W, train):
-        """bf16 NHWC x -> bf16 NHWC out (CAPMI_GEMM_BF16_IO), BN statistics into ws['stats']."""
+    def _conv_bf16(self, tag, x, conv, out, N, H, W, train, in_ss=None):
+        """bf16 NHWC x -> bf16 NHWC out (CAPMI_GEMM_BF16_IO), BN statistics into ws['stats']; in_ss = (scale,
+        shift): the input's BN-apply + ReLU in the GEMM's A staging (round 3) instead of a materialising pass."""
         co, ci, kh, kw = conv.weight.shape
         st, pd = conv.stride[0], conv.padding[0]
         Ho, Wo = (H + 2 * pd - kh) // st + 1, (W + 2 * pd - kw) // st + 1
@@ -451,11 +457,13 @@ class EncoderRunner:
         Kd = ci * kh * kw
         w = self._packed_bf16(conv)
         stats = self._ws["stats"] if train else None
+        sc, sh = in_ss if in_ss is not None else (None, None)
         if kh == 1 and st == 1:
-            prob, mode = K.problem_bf16(rows, co, Kd, x, ci, w, Kd, out, co, stats=stats), AK
+            prob, mode = K.problem_bf16(rows, co, Kd, x, ci, w, Kd, out, co, stats=stats, in_scale=sc, in_shift=sh), AK
         else:
             geo = dict(N=N, H=H, W=W, Cin=ci, KH=kh, KW=kw, stride=st, pad=pd, Ho=Ho, Wo=Wo)
-            prob, mode = K.problem_bf16(rows, co, Kd, x, 0, w, Kd, out, co, stats=stats, conv=geo), AC
+            prob, mode = K.problem_bf16(rows, co, Kd, x, 0, w, Kd, out, co, stats=stats, conv=geo, in_scale=sc,
+                                        in_shift=sh), AC
         launch = lambda: K.gemm_bf16(prob, mode, self._ws["sk"], K.TILE_AUTO)  # noqa: E731
         if self.conv_hook is not None:
             # the launch capmi_gemm_sk_ex makes for CAPMI_GEMM_BF16_IO (gemm.hip: gemm_bf16_io)
@@ -464,15 +472,18 @@ class EncoderRunner:
             slots = 2 * torch.cuda.get_device_properties(x.device).multi_processor_count
             rounds = -(-tiles // slots)
             sk = Kd // 64 >= 4 and tiles / (rounds * slots) < 0.9
-            key = f"gemm_bf16_kernel<128, {bn_}, {mode}, {'true' if sk else 'false'}>"
+            key = (f"gemm_bf16_kernel<128, {bn_}, {mode}, {'true' if sk else 'false'}, "
+                   f"{'true' if in_ss is not None else 'false'}>")
             self.conv_hook(tag, 2.0 * rows * co * Kd, launch, key)
         else:
             launch()
         return Ho, Wo, rows
 
-    def _bn_relu_bf16(self, ws, bn, rows, train, y):
+    def _bn_relu_bf16(self, ws, bn, rows, train, y, fold=False):
         """relu(bn(y)) in place on a bf16 conv output (the next conv's input), the BN finalize fused in
-        where it fits."""
+        where it fits. fold: return (scale, shift) for the consumer GEMM's prologue instead (round 3)."""
+        if fold:
+            return self._bn(ws, bn, rows, train)
         d = self._bn_defer(ws, bn, rows, train)
         if isinstance(d, _DeferredBN):
             d.apply(CAPMI_BNFA_RELU_BF16, y, y)
@@ -504,10 +515,10 @@ class EncoderRunner:
             for bi, blk in enumerate(getattr(net, f"layer{li}")):
                 tag = f"layer{li}.{bi}"
                 _, _, r1 = self._conv_bf16(tag + ".conv1", x, blk.conv1, bf["y1"], N, H, W, train)
-                self._bn_relu_bf16(ws, blk.bn1, r1, train, bf["y1"])
-                H2, W2, r2 = self._conv_bf16(tag + ".conv2", bf["y1"], blk.conv2, bf["y2"], N, H, W, train)
-                self._bn_relu_bf16(ws, blk.bn2, r2, train, bf["y2"])
-                _, _, r3 = self._conv_bf16(tag + ".conv3", bf["y2"], blk.conv3, bf["y3"], N, H2, W2, train)
+                ss1 = self._bn_relu_bf16(ws, blk.bn1, r1, train, bf["y1"], fold=_BF16_FOLD & 1)
+                H2, W2, r2 = self._conv_bf16(tag + ".conv2", bf["y1"], blk.conv2, bf["y2"], N, H, W, train, in_ss=ss1)
+                ss2 = self._bn_relu_bf16(ws, blk.bn2, r2, train, bf["y2"], fold=_BF16_FOLD & 2)
+                _, _, r3 = self._conv_bf16(tag + ".conv3", bf["y2"], blk.conv3, bf["y3"], N, H2, W2, train, in_ss=ss2)
                 Cout = blk.conv3.out_channels
                 if blk.downsample is not None:
                     s3, b3 = self._bn(ws, blk.bn3, r3, train)  # (the downsample conv reuses the stats buffer)

@@ -689,7 +689,7 @@ bool terms_mode_ok(int terms, int amode, int bmode) {
 int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, GemmArgs& a, int& bn, bool& sk,
             long long& total);
 int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total,
-             int& bk);
+             int& bk, int& bn);
 int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total);
 int x3s_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long& lda, int& tiles, int& grid);
 }  // namespace
@@ -701,12 +701,12 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
   if (flags == CAPMI_GEMM_X3P) {
     GemmArgs a;
     long long total = 0;
-    int bk = 32;
-    const int rc = x3p_plan(prob, amode, bmode, a, sk, total, bk);
+    int bk = 32, xbn = 128;
+    const int rc = x3p_plan(prob, amode, bmode, a, sk, total, bk, xbn);
     if (rc) return rc;
     if (threads) *threads = 512;
     if (bm) *bm = 256;
-    if (bn) *bn = 128;
+    if (bn) *bn = xbn;
     if (stream_k) *stream_k = sk ? 1 : 0;
     if (generic) *generic = bk;  // CAPMI_GEMM_X3P: the k-tile depth
     return 0;
@@ -772,9 +772,13 @@ int gemm_bf16_io(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
   const capmi_gemm_problem& p = *prob;
   CAPMI_REQUIRE(bmode == CAPMI_B_NMAJOR_W && (amode == CAPMI_A_KMAJOR || amode == CAPMI_A_CONV_NHWC), CAPMI_EINVAL);
   CAPMI_REQUIRE(p.A && p.B && p.C && p.M >= 0 && p.N > 0 && p.K > 0 && p.K % 64 == 0, CAPMI_EINVAL);
-  CAPMI_REQUIRE(p.ksplit == 1 && !p.in_scale && !p.in_shift && !p.bias && !p.bias2 && !p.alpha_ptr &&
-                    p.alpha == 1.f && p.beta == 0.f && !p.relu && p.a_r1 <= 0 && p.c_r1 <= 0,
+  CAPMI_REQUIRE(p.ksplit == 1 && !p.bias && !p.bias2 && !p.alpha_ptr && p.alpha == 1.f && p.beta == 0.f &&
+                    !p.relu && p.a_r1 <= 0 && p.c_r1 <= 0,
                 CAPMI_EINVAL);
+  // the BN-apply + ReLU prologue (round 3): dense rows with lda == K (the channel is k) or a conv
+  CAPMI_REQUIRE((p.in_scale == nullptr) == (p.in_shift == nullptr), CAPMI_EINVAL);
+  CAPMI_REQUIRE(p.in_scale == nullptr || amode == CAPMI_A_CONV_NHWC || p.lda == p.K, CAPMI_EINVAL);
+  CAPMI_REQUIRE(p.in_scale == nullptr || (aligned16(p.in_scale) && aligned16(p.in_shift)), CAPMI_EALIGN);
   CAPMI_REQUIRE(aligned16(p.A) && aligned16(p.B) && p.ldb % 8 == 0 && p.ldb >= p.K && p.ldc >= p.N, CAPMI_EALIGN);
   CAPMI_REQUIRE((long long)p.N * p.ldb * 2 < (1LL << 31), CAPMI_ERANGE);
   if (amode == CAPMI_A_CONV_NHWC) {
@@ -872,7 +876,7 @@ bool x3p_force32() {
 // round; otherwise BK = 32, one workgroup per CU, stream-K when the tile count leaves the chip
 // under-filled (l3 c3, 392 tiles: 49 us stream-K vs 102 us as one 2-per-CU round).
 int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total,
-             int& bk) {
+             int& bk, int& bn) {
   CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
   const capmi_gemm_problem& p = *prob;
   CAPMI_REQUIRE(bmode == CAPMI_B_NMAJOR_W && (amode == CAPMI_A_KMAJOR || amode == CAPMI_A_CONV_NHWC), CAPMI_EINVAL);
@@ -891,8 +895,9 @@ int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
   memset(&a, 0, sizeof(a));
   a.nprob = 1;
   a.p[0] = p;
+  bn = p.N <= 64 ? 64 : 128;  // 256 x 64 tiles for the N = 64 convs (layer1's 3x3)
   a.tiles_m[0] = (int)cdiv(p.M, 256);
-  a.tiles_n[0] = (int)cdiv(p.N, 128);
+  a.tiles_n[0] = (int)cdiv(p.N, bn);
   {  // A/B knob: CAPMI_X3P_ORDER=col walks tiles column-major (an XCD's contiguous range shares B)
     static const int col = [] {
       const char* e = getenv("CAPMI_X3P_ORDER");
@@ -900,7 +905,7 @@ int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
     }();
     a.tile_cols_first = col;
   }
-  a.plain_epi = plain_epilogue(p, 128);
+  a.plain_epi = plain_epilogue(p, bn);
   total = (long long)a.tiles_m[0] * a.tiles_n[0];
   a.tiles_begin[1] = (int)total;
   const long long slots2 = 2LL * sk_cus();
@@ -923,11 +928,11 @@ int gemm_x3p(const capmi_gemm_problem* prob, int amode, int bmode, void* workspa
   GemmArgs a;
   bool sk = false;
   long long total = 0;
-  int bk = 32;
-  const int rc = x3p_plan(prob, amode, bmode, a, sk, total, bk);
+  int bk = 32, bn = 128;
+  const int rc = x3p_plan(prob, amode, bmode, a, sk, total, bk, bn);
   if (rc) return rc;
   if (prob->M == 0) return 0;
-  if (!sk || workspace == nullptr) return gemm_x3p_launch(a, amode, bk, (int)total, s);
+  if (!sk || workspace == nullptr) return gemm_x3p_launch(a, amode, bk, (int)total, s, bn);
   CAPMI_REQUIRE(aligned16(workspace), CAPMI_EINVAL);
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
   const int cus = cu_count();
@@ -939,7 +944,7 @@ int gemm_x3p(const capmi_gemm_problem* prob, int amode, int bmode, void* workspa
   a.sk_groups = sk_xcd_groups() && a.sk_workers % 8 == 0 && total >= 64 ? 8 : 1;
   a.sk_flags = static_cast<int*>(workspace);
   a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
-  return gemm_x3p_launch(a, amode, bk, a.sk_workers, s);
+  return gemm_x3p_launch(a, amode, bk, a.sk_workers, s, bn);
 }
 
 // CAPMI_GEMM_X3D: fp32 A (+ BN prologue for convs) split in-kernel x three-plane B in the x3p k order

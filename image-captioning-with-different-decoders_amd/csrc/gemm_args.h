@@ -55,7 +55,7 @@ int gemm_x3_launch(const GemmArgs& a, int amode, int bn, int blocks, hipStream_t
 // x3 with both operands pre-split (gemm_x3p.hip): 256x128 tiles, 512 threads, amode 0 / 2; k-tile depth
 // bk (16: two workgroups per CU, data-parallel grids only; 32: one, stream-K capable) is the unit
 // of GemmArgs::sk_nkt for it
-int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_t s);
+int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_t s, int bn = 128);
 // x3p with A fp32 split in-kernel ("x3d": register-staged A + optional conv BN prologue, LDS-DMA B)
 int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s);
 // short-k streaming x3 GEMM (gemm_x3s.hip): K = 64, N in {64, 128, 256}, dense rows of lda floats

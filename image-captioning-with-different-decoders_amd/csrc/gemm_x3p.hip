@@ -22,7 +22,7 @@
 
 namespace {
 
-constexpr int PBM = 256, PBN = 128, PNT = 512;
+constexpr int PBM = 256, PNT = 512;
 typedef unsigned u32x4_p __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_p __attribute__((ext_vector_type(8)));
 typedef float f32x4_p __attribute__((ext_vector_type(4)));
@@ -36,7 +36,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_p(const void* p, unsigned
 
 // BK = 32: 72 KiB per LDS buffer, one workgroup per CU; BK = 16: 36 KiB, two workgroups per CU (their
 // barriers and DMA waits fall at different times, so one's MFMAs cover the other's stalls)
-template <int PBK>
+template <int PBK, int PBN = 128>
 struct X3pGeo {
   static constexpr int PROWB = PBK * 2;             // bytes per LDS row
   static constexpr int CPR = PBK / 8;               // 16-B chunks per row
@@ -72,38 +72,42 @@ __device__ __forceinline__ int swz(int r) {
 // + ReLU prologue PRO), loaded to registers one k-tile ahead and split into the three swizzled LDS
 // planes after the k-tile's MFMAs; B stays LDS-DMA. It replaces gemm_x3 (both operands through
 // registers) and the separate split pass of x3p (BK = 32 only).
-template <int AMODE, bool SK, int PBK, bool ASPLIT = false, bool PRO = false>
+// PBN (round 3): 128, or 64 for the N = 64 convs (layer1's 3x3): the wave tile is 64 x PBN/2
+template <int AMODE, bool SK, int PBK, bool ASPLIT = false, bool PRO = false, int PBN = 128>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(X3pGeo<PBK>::WPE)))
 gemm_x3p_kernel(const GemmArgs args) {
   static_assert(!ASPLIT || PBK == 32, "x3d: 32-deep k-tiles");
   static_assert(!PRO || (ASPLIT && AMODE == 2), "prologue: x3d conv");
-  using G_ = X3pGeo<PBK>;
+  static_assert(PBN == 128 || PBN == 64, "column tile");
+  using G_ = X3pGeo<PBK, PBN>;
+  constexpr int JN = PBN / 32;    // 16x16x32: 16-column blocks per wave
+  constexpr int JN32 = PBN / 64;  // 32x32x16: 32-column blocks per wave
   constexpr int PROWB = G_::PROWB, CPR = G_::CPR, RPB = G_::RPB, SWZ = G_::SWZ;
   constexpr int PA_BYTES = G_::PA_BYTES, PBUF = G_::PBUF, NAB = G_::NAB, NBB = G_::NBB;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * PBUF];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases in SGPRs
-  const int wm0 = (wid >> 1) * 64, wn0 = (wid & 1) * 64;
+  const int wm0 = (wid >> 1) * 64, wn0 = (wid & 1) * (PBN / 2);
   const int lr = lane & 31, lh = lane >> 5;
   // DMA lane geometry: row lane / CPR of an RPB-row block, slot lane % CPR
   const int drow = lane / CPR, dslot = lane % CPR;
 
   constexpr bool M16 = PBK == 32 && X3P_M16;
-  f32x16 acc[2][2];     // 32x32x16: wave tile 2 x 2 blocks of 32 x 32
-  f32x4_p acc4[4][4];   // 16x16x32: wave tile 4 x 4 blocks of 16 x 16
+  f32x16 acc[2][JN32];  // 32x32x16: wave tile 2 x JN32 blocks of 32 x 32
+  f32x4_p acc4[4][JN];  // 16x16x32: wave tile 4 x JN blocks of 16 x 16
 
   auto mainloop = [&](const capmi_gemm_problem& P, int m0, int n0, int k_lo, int k_hi) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < JN32; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc4[i][j] = f32x4_p{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < JN; ++j) acc4[i][j] = f32x4_p{0.f, 0.f, 0.f, 0.f};
     const int nkt = (k_hi - k_lo) / PBK;
     if (nkt <= 0) return;
     const int M = P.M, N = P.N;
@@ -309,7 +313,7 @@ gemm_x3p_kernel(const GemmArgs args) {
       if constexpr (M16) {
         // 16x16x32: lane l reads row (l % 16) of each 16-row block, k-chunk l / 16 (8 k of the 32);
         // all 24 fragments of the k-tile up front, then 16 blocks x 6 products
-        bf16x8_p a[4][3], b[4][3];
+        bf16x8_p a[4][3], b[JN][3];
         const int c = lane >> 4, rl = lane & 15;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -319,7 +323,7 @@ gemm_x3p_kernel(const GemmArgs args) {
           for (int p = 0; p < 3; ++p) a[i][p] = *reinterpret_cast<const bf16x8_p*>(A_ + p * PBM * PROWB + o);
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < JN; ++j) {
           const int r = wn0 + 16 * j + rl;
           const int o = r * PROWB + ((c ^ swz<PBK>(r)) << 4);
 #pragma unroll
@@ -329,7 +333,7 @@ gemm_x3p_kernel(const GemmArgs args) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < JN; ++j) {
             acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][1], acc4[i][j], 0, 0, 0);
             acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][2], acc4[i][j], 0, 0, 0);
             acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[j][0], acc4[i][j], 0, 0, 0);
@@ -337,7 +341,7 @@ gemm_x3p_kernel(const GemmArgs args) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < JN; ++j) {
             acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][1], acc4[i][j], 0, 0, 0);
             acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][0], acc4[i][j], 0, 0, 0);
             acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][0], acc4[i][j], 0, 0, 0);
@@ -347,7 +351,7 @@ gemm_x3p_kernel(const GemmArgs args) {
       }
       // every fragment of the k-tile is requested up front (2 x 12 ds_read_b128): the second
       // chunk's reads land while the first chunk's 24 MFMAs run
-      bf16x8_p a[PBK / 16][2][3], b[PBK / 16][2][3];
+      bf16x8_p a[PBK / 16][2][3], b[PBK / 16][JN32][3];
 #pragma unroll
       for (int g = 0; g < PBK / 16; ++g) {
         const int c = 2 * g + lh;  // logical 16-B chunk (8 k) this lane reads
@@ -364,7 +368,7 @@ gemm_x3p_kernel(const GemmArgs args) {
 #endif
         }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < JN32; ++j) {
           const int r = wn0 + 32 * j + lr;
           const int o = r * PROWB + ((c ^ swz<PBK>(r)) << 4);
 #if X3P_SKIP & 2
@@ -382,7 +386,7 @@ gemm_x3p_kernel(const GemmArgs args) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
+          for (int j = 0; j < JN32; ++j) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[g][i][1], b[g][j][1], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[g][i][0], b[g][j][2], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[g][i][2], b[g][j][0], acc[i][j], 0, 0, 0);
@@ -390,7 +394,7 @@ gemm_x3p_kernel(const GemmArgs args) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
+          for (int j = 0; j < JN32; ++j) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[g][i][0], b[g][j][1], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[g][i][1], b[g][j][0], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[g][i][0], b[g][j][0], acc[i][j], 0, 0, 0);
@@ -540,7 +544,7 @@ gemm_x3p_kernel(const GemmArgs args) {
     if constexpr (M16) {
       // 16x16 blocks: lane l holds rows 4 (l / 16) .. + 3 of column l % 16 of each block
       const int cl = lane & 15, rq = lane >> 4;
-      float csum4[4], csq4[4];
+      float csum4[JN], csq4[JN];
       if (args.plain_epi) {
         // store-only form (host: plain_epilogue): 16 row offsets per lane computed once, the 64 stores
         // take the column block as an immediate offset; rows past M are dropped by the descriptor
@@ -555,7 +559,7 @@ gemm_x3p_kernel(const GemmArgs args) {
           }
         const unsigned cb = (unsigned)(n0 + wn0 + cl) * 4u;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < JN; ++j) {
           csum4[j] = 0.f;
           csq4[j] = 0.f;
 #pragma unroll
@@ -570,7 +574,7 @@ gemm_x3p_kernel(const GemmArgs args) {
         }
       } else
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < JN; ++j) {
         csum4[j] = 0.f;
         csq4[j] = 0.f;
         const int col = n0 + wn0 + 16 * j + cl;
@@ -599,7 +603,7 @@ gemm_x3p_kernel(const GemmArgs args) {
       float* __restrict__ stats = P.stats;
       if (stats != nullptr) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < JN; ++j) {
           csum4[j] += __shfl_xor(csum4[j], 16, 64);
           csq4[j] += __shfl_xor(csq4[j], 16, 64);
           csum4[j] += __shfl_xor(csum4[j], 32, 64);
@@ -608,7 +612,7 @@ gemm_x3p_kernel(const GemmArgs args) {
         if (rq == 0) {  // the wave's 64 rows are one 64-row slice
           const long long sl = (m0 + wm0) >> 6;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < JN; ++j) {
             const int col = n0 + wn0 + 16 * j + cl;
             if (col < N && m0 + wm0 < M) {
               stats[(sl * N + col) * 2 + 0] = csum4[j];
@@ -619,9 +623,9 @@ gemm_x3p_kernel(const GemmArgs args) {
       }
       return;
     }
-    float csum[2], csq[2];
+    float csum[JN32], csq[JN32];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < JN32; ++j) {
       csum[j] = 0.f;
       csq[j] = 0.f;
       const int col = n0 + wn0 + 32 * j + lr;
@@ -650,14 +654,14 @@ gemm_x3p_kernel(const GemmArgs args) {
     float* __restrict__ stats = P.stats;
     if (stats != nullptr) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < JN32; ++j) {
         csum[j] += __shfl_xor(csum[j], 32, 64);
         csq[j] += __shfl_xor(csq[j], 32, 64);
       }
       if (lh == 0) {  // the wave's 64 rows are one 64-row slice
         const long long sl = (m0 + wm0) >> 6;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < JN32; ++j) {
           const int col = n0 + wn0 + 32 * j + lr;
           if (col < N && m0 + wm0 < M) {
             stats[(sl * N + col) * 2 + 0] = csum[j];
@@ -730,14 +734,14 @@ gemm_x3p_kernel(const GemmArgs args) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < JN; ++j)
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_p, acc4[i][j]), rs,
-                                                   ((i * 4 + j) * PNT + tid) * 16, 0, kSc1p);
+                                                   ((i * JN + j) * PNT + tid) * 16, 0, kSc1p);
       } else {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < JN32; ++j)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             u32x4_p v;
@@ -745,7 +749,7 @@ gemm_x3p_kernel(const GemmArgs args) {
             v.y = __float_as_uint(acc[i][j][4 * q + 1]);
             v.z = __float_as_uint(acc[i][j][4 * q + 2]);
             v.w = __float_as_uint(acc[i][j][4 * q + 3]);
-            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (((i * 2 + j) * 4 + q) * PNT + tid) * 16, 0, kSc1p);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (((i * JN32 + j) * 4 + q) * PNT + tid) * 16, 0, kSc1p);
           }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -774,18 +778,18 @@ gemm_x3p_kernel(const GemmArgs args) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < JN; ++j)
               acc4[i][j] += __builtin_bit_cast(
-                  f32x4_p, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i * 4 + j) * PNT + tid) * 16, 0, kSc1p));
+                  f32x4_p, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i * JN + j) * PNT + tid) * 16, 0, kSc1p));
         } else {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < JN32; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const u32x4_p v =
-                  __builtin_amdgcn_raw_buffer_load_b128(rs, (((i * 2 + j) * 4 + q) * PNT + tid) * 16, 0, kSc1p);
+                  __builtin_amdgcn_raw_buffer_load_b128(rs, (((i * JN32 + j) * 4 + q) * PNT + tid) * 16, 0, kSc1p);
               acc[i][j][4 * q + 0] += __uint_as_float(v.x);
               acc[i][j][4 * q + 1] += __uint_as_float(v.y);
               acc[i][j][4 * q + 2] += __uint_as_float(v.z);
@@ -853,12 +857,26 @@ int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
   return 0;
 }
 
-int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_t s) {
+int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_t s, int bn) {
   const dim3 g(blocks), b(PNT);
   const bool sk = a.sk_workers > 0;
   // the two-workgroup form runs data-parallel grids only (its 128-VGPR budget has no room for
   // the stream-K hand-off)
   CAPMI_REQUIRE(bk == 32 || (bk == 16 && !sk), CAPMI_EINVAL);
+  CAPMI_REQUIRE(bn == 128 || bn == 64, CAPMI_EINVAL);
+  if (bn == 64) {  // the N = 64 convs (layer1's 3x3)
+#define X3P_GO64(M, S, BK) CAPMI_KLAUNCH((gemm_x3p_kernel<M, S, BK, false, false, 64>), g, b, 0, s, a)
+    if (bk == 16) {
+      if (amode == 2) X3P_GO64(2, false, 16); else X3P_GO64(0, false, 16);
+    } else if (amode == 2) {
+      if (sk) X3P_GO64(2, true, 32); else X3P_GO64(2, false, 32);
+    } else {
+      if (sk) X3P_GO64(0, true, 32); else X3P_GO64(0, false, 32);
+    }
+#undef X3P_GO64
+    CAPMI_LAUNCH_CHECK();
+    return 0;
+  }
 #define X3P_GO(M, S, BK) CAPMI_KLAUNCH((gemm_x3p_kernel<M, S, BK>), g, b, 0, s, a)
   if (bk == 16) {
     if (amode == 2)

@@ -121,8 +121,10 @@ int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int t
  * leading dimensions in elements), v_mfma_f32_32x32x16_bf16 with fp32 accumulation, C rounded to bf16
  * (RNE) once, `stats` fp32 from the stored values. A = CAPMI_A_KMAJOR (lda % 8 == 0) or
  * CAPMI_A_CONV_NHWC (Cin % 64 == 0) x B = W[N][K] (CAPMI_B_NMAJOR_W, ldb % 8 == 0); K % 64 == 0;
- * alpha 1, beta 0, no bias / relu / prologue / ksplit (the bf16 encoder materialises the conv
- * input with capmi_bn_relu_bf16). Tile 128x128, or 128x64 for CAPMI_TILE_128x64 / N <= 64. */
+ * alpha 1, beta 0, no bias / relu / ksplit. Optional BN-apply + ReLU prologue (in_scale / in_shift fp32
+ * [Cin]; CAPMI_A_KMAJOR needs lda == K): each A element becomes relu(fma(a, scale, shift)) rounded to bf16
+ * (RNE), capmi_bn_relu_bf16's arithmetic bit for bit, padding taps zero after it (round 3: the bf16
+ * encoder no longer materialises conv3's input). Tile 128x128, or 128x64 for CAPMI_TILE_128x64 / N <= 64. */
 #define CAPMI_GEMM_BF16_IO 2
 /* CAPMI_GEMM_X3 (alone): fp32-accurate GEMM on the bf16 matrix cores. A is fp32 (CAPMI_A_KMAJOR,
  * lda % 4 == 0, or CAPMI_A_CONV_NHWC, Cin % 32 == 0, with the optional BN-apply + ReLU prologue);

@@ -162,7 +162,9 @@ def test_bn_relu_split3_exact():
     (4, 14, 256, 256, 3, 1, True), (4, 28, 128, 128, 3, 2, True), (2, 56, 64, 256, 1, 1, True),
     (3, 14, 256, 1024, 1, 1, True), (2, 7, 512, 2048, 1, 1, False), (64, 14, 256, 256, 3, 1, True),
     (1, 9, 64, 128, 3, 1, True), (64, 7, 512, 512, 3, 1, True), (64, 28, 128, 128, 3, 1, True),
-    (64, 14, 256, 1024, 1, 1, True), (64, 56, 128, 128, 3, 2, True)])
+    (64, 14, 256, 1024, 1, 1, True), (64, 56, 128, 128, 3, 2, True),
+    # N = 64 (256 x 64 tiles, round 3): layer1's 3x3 at batch 64 (data-parallel, two per CU), stream-K, ragged
+    (64, 56, 64, 64, 3, 1, True), (2, 56, 64, 64, 3, 1, True), (1, 9, 64, 64, 3, 1, True)])
 def test_x3p_conv_stats(N, H, Cin, Cout, k, stride, pro):
     """Both operands pre-split (CAPMI_GEMM_X3P): the conv of relu(x*s+b) (split pass) vs fp64, and
     the BN statistics; ragged M (tiles of 256 rows), stream-K and data-parallel grids."""

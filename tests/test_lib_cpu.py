@@ -94,6 +94,7 @@ def test_gemm_sk_plan_on_host():
     rc, (bm, bn, sk, generic, nt) = plan(256, flags=8, M=200704)
     assert rc == 0 and (bm, bn, generic, nt) == (256, 128, 16, 512) and sk == 0
     assert plan(256, flags=8, Cin=20)[0] == 1001  # Cin % 32 != 0
+    assert plan(64, flags=8)[1][1] == 64  # N = 64: 256 x 64 tiles (round 3)
     # CAPMI_GEMM_X3S (64, ABI 17): K = 64 only -- the 3x3 conv above is rejected; a 1x1 layer1 conv3 with
     # the BN prologue (M = 200704, N = 256) gets 64-row tiles, 256 threads, no stream-K, the persistent
     # grid (two workgroups per CU) in `generic`
