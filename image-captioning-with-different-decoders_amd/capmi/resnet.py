@@ -303,7 +303,8 @@ class EncoderRunner:
         # x3s (round 3): layer1's K = 64 1x1 convs (layer1.0 conv1 / downsample on the pooled stem, every
         # layer1 conv3 on relu(bn2(y2))) on the short-k streaming kernel (gemm_x3s.hip: weight in VGPRs,
         # persistent 64-row tiles, two workgroups per CU)
-        x3s = (_X3S and x3 and not nchw and Kd == 64 and kh == 1 and st == 1 and pd == 0 and co in (64, 128, 256))
+        x3s = (_X3S and x3 and not nchw and Kd == 64 and kh == 1 and st == 1 and pd == 0 and co in (64, 128, 256)
+               and rows * co * 4 < (1 << 31))  # (its store-only epilogue addresses C with 32-bit offsets)
         if isinstance(in_ss, _DeferredBN) and not x3p:
             in_ss = in_ss.now()  # only the x3p split pass takes the finalize fused
         if tail is not None and not (x3 and not x3s and not x3d and not x3p and not smallk and not nchw and kh == 1
@@ -613,7 +614,7 @@ class EncoderRunner:
             if nbt:
                 torch._foreach_add_(nbt, 1)
         if out_hw is None:
-            return x if direct else x.view(N, H, W, Cx).clone()
+            return x if direct else x[: N * H * W * Cx].view(N, H, W, Cx).clone()
         OH, OW = out_hw
         if out is None:
             out = torch.empty(N, OH, OW, Cx, device=imgs.device, dtype=torch.float32)

@@ -72,7 +72,8 @@ def test_encoder_surface():
     assert all(p.requires_grad for p in list(enc.resnet.children())[5].parameters())
 
 
-@pytest.mark.parametrize("rows,C,rbn", [(12544, 1024, False), (3137, 256, True), (5, 12, False), (1, 4, True)])
+@pytest.mark.parametrize("rows,C,rbn", [(12544, 1024, False), (3137, 256, True), (5, 12, False), (1, 4, True),
+                                         (200704, 256, True), (3136, 2048, False), (777, 2048, True)])
 def test_bn_add_relu_elementwise(rows, C, rbn):
     """out = relu(y*s + b + (res*rs + rb | res)) elementwise vs torch fp32 (same fma order up to
     contraction: 1 ulp), ragged sizes (n4 not a multiple of the 512 float4 a block covers)."""

@@ -140,10 +140,11 @@ def test_encoder_x3_matches_oracle(B, H):
     assert e_gpu <= 2 * e_cpu + 1e-6, (e_gpu, e_cpu)
 
 
-def test_bn_relu_split3_exact():
-    """The split planes of relu(y*s+b) sum exactly (fp64) to the fp32 value torch computes."""
+@pytest.mark.parametrize("rows,C", [(1000, 96), (12544, 256), (3137, 1024), (5, 12), (777, 2048)])
+def test_bn_relu_split3_exact(rows, C):
+    """The split planes of relu(y*s+b) sum exactly (fp64) to the fp32 value torch computes (any C: the
+    grid keeps one channel group per thread)."""
     K = _K()
-    rows, C = 1000, 96
     y, s, b = rnd(rows, C, seed=8) * 3, rnd(C, seed=9) + 1.5, rnd(C, seed=10)
     out = torch.empty(3 * rows * C, device=DEV, dtype=torch.bfloat16)
     K.bn_relu_split3(y.to(DEV), s.to(DEV), b.to(DEV), rows, C, out)
