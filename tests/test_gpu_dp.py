@@ -19,6 +19,7 @@ import torch
 import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
+DEV = "cuda"
 
 
 def _free_port():
