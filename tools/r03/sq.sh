@@ -18,4 +18,4 @@ for c in ${CASES:-l3c3:x3d l3c2:x3p l3c1:x3 l1c3:x3 l1c2:x3}; do
     n=$((n+1))
   done
 done
-cd $R && python tools/pmc_table.py gpurun_out/pmcx3 > gpurun_out/sq_table.txt
+cd $R && python tools/pmc_table.py gpurun_out/pmcx3 > gpurun_out/sq_table.txt && rm -rf gpurun_out/pmcx3
