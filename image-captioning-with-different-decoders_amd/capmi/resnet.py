@@ -672,7 +672,9 @@ _FT_DGRAD_X3D = os.environ.get("CAPMI_FT_DGRAD_X3D", "1") != "0"
 _FT_PACK_X3 = os.environ.get("CAPMI_FT_PACK_X3", "1") != "0"
 # 1x1 dgrads read the weight itself as k rows (CAPMI_B_KROWS) instead of a per-step transposed pack
 _FT_DGRAD1_KROWS = os.environ.get("CAPMI_FT_DGRAD1_KROWS", "0") != "0"
-_FT_DGRAD1_X3D = os.environ.get("CAPMI_FT_DGRAD1_X3D", "0") != "0"  # 1x1 dgrads: neutral (1666 both), off
+# 1x1 dgrads on x3d: neutral in round 2 (1666 both); with the store-only / beta epilogue
+# 1676-1680 -> 1711-1716 img/s (two pairs, one box): on
+_FT_DGRAD1_X3D = os.environ.get("CAPMI_FT_DGRAD1_X3D", "1") != "0"
 
 
 class FineTuneRunner:

@@ -1013,8 +1013,11 @@ int x3s_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long& ld
   const capmi_gemm_problem& p = *prob;
   CAPMI_REQUIRE(bmode == CAPMI_B_NMAJOR_W && (amode == CAPMI_A_KMAJOR || amode == CAPMI_A_CONV_NHWC), CAPMI_EINVAL);
   CAPMI_REQUIRE(p.A && p.B && p.C && p.M >= 0 && p.K == 64 && (p.N == 64 || p.N == 128 || p.N == 256), CAPMI_EINVAL);
-  CAPMI_REQUIRE(plain_epilogue(p, 64) && p.a_r1 <= 0 && (p.in_scale == nullptr) == (p.in_shift == nullptr),
+  // the store-only epilogue is x3s's only form (independent of the CAPMI_X3_PLAIN_EPI A/B switch)
+  CAPMI_REQUIRE(p.alpha == 1.f && p.alpha_ptr == nullptr && p.bias == nullptr && p.bias2 == nullptr && p.beta == 0.f &&
+                    !p.relu && p.c_r1 <= 0 && p.ksplit == 1 && p.ldc >= p.N && (long long)p.M * p.ldc * 4 < (1LL << 31),
                 CAPMI_EINVAL);
+  CAPMI_REQUIRE(p.a_r1 <= 0 && (p.in_scale == nullptr) == (p.in_shift == nullptr), CAPMI_EINVAL);
   if (amode == CAPMI_A_CONV_NHWC) {
     CAPMI_REQUIRE(p.cKH == 1 && p.cKW == 1 && p.cStride == 1 && p.cPad == 0 && p.cCin == 64 && p.cHo == p.cH &&
                       p.cWo == p.cW && p.M == p.cN * p.cHo * p.cWo,

@@ -31,16 +31,19 @@ __device__ __forceinline__ long long remap(long long r, long long r1, long long 
 }
 
 // Host: does problem p take the store-only epilogue of the x3 kernels with BN-wide column tiles?
-// (C = A.B exactly: no alpha / bias / beta / relu / row remap; whole column tiles; C addressable with
+// (C = A.B (+ beta C) exactly: no alpha / bias / relu / row remap; whole column tiles; C addressable with
 // 32-bit byte offsets; rows past M read zeros in A, so their accumulators add nothing to the BN sums)
 inline int plain_epilogue(const capmi_gemm_problem& p, int bn) {
   static const bool off = [] {  // CAPMI_X3_PLAIN_EPI=0: the general epilogue everywhere (A/B arm)
     const char* e = getenv("CAPMI_X3_PLAIN_EPI");
     return e && e[0] == '0';
   }();
-  return !off && p.alpha == 1.f && p.alpha_ptr == nullptr && p.bias == nullptr && p.bias2 == nullptr && p.beta == 0.f &&
-         !p.relu && p.c_r1 <= 0 && p.ksplit == 1 && p.N % bn == 0 && p.ldc >= p.N &&
-         (long long)p.M * p.ldc * 4 < (1LL << 31);
+  // 1: C = A.B; 2: C = A.B + beta C (read-modify-write through the same offsets; the fine-tune 1x1 data
+  // gradients accumulate into the block input's gradient)
+  const bool ok = !off && p.alpha == 1.f && p.alpha_ptr == nullptr && p.bias == nullptr && p.bias2 == nullptr &&
+                  !p.relu && p.c_r1 <= 0 && p.ksplit == 1 && p.N % bn == 0 && p.ldc >= p.N &&
+                  (long long)p.M * p.ldc * 4 < (1LL << 31);
+  return ok ? (p.beta == 0.f ? 1 : 2) : 0;
 }
 
 // v2 kernel: A K-major dense / NHWC conv / NHWC4 conv1 / M-major (k rows), B = W[N][K] or k rows;

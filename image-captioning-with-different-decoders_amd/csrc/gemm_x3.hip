@@ -380,7 +380,9 @@ gemm_x3_kernel(const GemmArgs args) {
           for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float v = acc4[i][j][r];
+              float v = acc4[i][j][r];
+              if (args.plain_epi == 2)  // + beta C (the general epilogue's fmaf(beta, C, v), bit for bit)
+                v = fmaf(beta, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rc, roff[i][r] + cb + 64u * j, 0, 0)), v);
               __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, roff[i][r] + cb + 64u * j, 0, 0);
               csum[j] += v;
               csq[j] = fmaf(v, v, csq[j]);
