@@ -346,8 +346,10 @@ class EncoderRunner:
             split3 = True
         elif x3d:
             w3 = self._packed_x3(conv, tap_inner=True)
-            if kh == 1 and st == 1 and in_ss is None:
-                prob, mode = K.problem(rows, co, Kd, x, ci, w3, Kd, out, co, **kw_), CAPMI_A_KMAJOR
+            if kh == 1 and st == 1 and pd == 0:  # 1x1: dense rows, the BN prologue (if any) per k = channel
+                sc, sh = in_ss if in_ss is not None else (None, None)
+                prob = K.problem(rows, co, Kd, x, ci, w3, Kd, out, co, in_scale=sc, in_shift=sh, **kw_)
+                mode = CAPMI_A_KMAJOR
             else:
                 sc, sh = in_ss if in_ss is not None else (None, None)
                 prob = K.problem(rows, co, Kd, x, 0, w3, Kd, out, co, conv=geo, in_scale=sc, in_shift=sh, **kw_)

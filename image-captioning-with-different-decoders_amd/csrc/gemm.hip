@@ -955,7 +955,8 @@ int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
   const capmi_gemm_problem& p = *prob;
   CAPMI_REQUIRE(bmode == CAPMI_B_NMAJOR_W && (amode == CAPMI_A_KMAJOR || amode == CAPMI_A_CONV_NHWC), CAPMI_EINVAL);
   CAPMI_REQUIRE(p.A && p.B && p.C && p.M >= 0 && p.N > 0 && p.K > 0 && p.K % 32 == 0 && p.ksplit == 1, CAPMI_EINVAL);
-  CAPMI_REQUIRE(amode == CAPMI_A_CONV_NHWC || (!p.in_scale && !p.in_shift), CAPMI_EINVAL);
+  // dense rows take the prologue when k is the channel (a 1x1 conv's input: lda == K)
+  CAPMI_REQUIRE(amode == CAPMI_A_CONV_NHWC || (!p.in_scale && !p.in_shift) || p.lda == p.K, CAPMI_EINVAL);
   CAPMI_REQUIRE((p.in_scale == nullptr) == (p.in_shift == nullptr), CAPMI_EINVAL);
   CAPMI_REQUIRE(p.a_r1 <= 0 && (p.stats == nullptr || p.c_r1 <= 0), CAPMI_EINVAL);
   CAPMI_REQUIRE(aligned16(p.A) && aligned16(p.B) && p.ldb % 8 == 0 && p.ldb >= p.K, CAPMI_EALIGN);

@@ -77,7 +77,7 @@ template <int AMODE, bool SK, int PBK, bool ASPLIT = false, bool PRO = false, in
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(X3pGeo<PBK>::WPE)))
 gemm_x3p_kernel(const GemmArgs args) {
   static_assert(!ASPLIT || PBK == 32, "x3d: 32-deep k-tiles");
-  static_assert(!PRO || (ASPLIT && AMODE == 2), "prologue: x3d conv");
+  static_assert(!PRO || ASPLIT, "prologue: x3d (conv, or dense rows whose k is the channel: 1x1 convs)");
   static_assert(PBN == 128 || PBN == 64, "column tile");
   using G_ = X3pGeo<PBK, PBN>;
   constexpr int JN = PBN / 32;    // 16x16x32: 16-column blocks per wave
@@ -211,8 +211,9 @@ gemm_x3p_kernel(const GemmArgs args) {
       if (ASPLIT) {
         a_msk = 0;
         if (PRO && kok) {  // (past the last k-tile the walk is past Cin: no read)
-          a_sc = *reinterpret_cast<const float4*>(P.in_scale + c_ci + aq * 4);
-          a_sh = *reinterpret_cast<const float4*>(P.in_shift + c_ci + aq * 4);
+          const int ch = (AMODE == 2 ? c_ci : k) + aq * 4;  // dense rows (1x1 conv): the channel is k
+          a_sc = *reinterpret_cast<const float4*>(P.in_scale + ch);
+          a_sh = *reinterpret_cast<const float4*>(P.in_shift + ch);
         }
 #pragma unroll
         for (int i = 0; i < NSA; ++i) {
@@ -419,6 +420,7 @@ gemm_x3p_kernel(const GemmArgs args) {
       // everything of t + 1 (loads return in order) and leaves A(t + 2) in flight. Every load is
       // issued unconditionally (out-of-range offsets read zeros), so the count never changes.
       static_assert(NSA == 4, "x3d deep pipeline: vmcnt immediate");
+      static_assert(!PRO || AMODE == 2, "x3d deep pipeline: the prologue walks the conv channels");
       const auto rsc = rsrc_p(PRO ? (const void*)P.in_scale : P.A, PRO ? (unsigned)(cCin * 4) : 0u);
       const auto rsh = rsrc_p(PRO ? (const void*)P.in_shift : P.A, PRO ? (unsigned)(cCin * 4) : 0u);
       // channel walk of the scale / shift loads (one k-tile behind the A walk c_ci / c_kh / c_kw)
@@ -843,7 +845,6 @@ int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
   const dim3 g(blocks), b(PNT);
   const bool sk = a.sk_workers > 0;
   const bool pro = a.p[0].in_scale != nullptr;
-  CAPMI_REQUIRE(!pro || amode == 2, CAPMI_EINVAL);
 #define X3D_GO(M, S, PR) CAPMI_KLAUNCH((gemm_x3p_kernel<M, S, 32, true, PR>), g, b, 0, s, a)
   if (amode == 2) {
     if (pro) {
@@ -851,6 +852,8 @@ int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
     } else {
       if (sk) X3D_GO(2, true, false); else X3D_GO(2, false, false);
     }
+  } else if (pro) {  // 1x1 conv as dense rows with the BN prologue (round 3: no im2col address VALU)
+    if (sk) X3D_GO(0, true, true); else X3D_GO(0, false, true);
   } else {
     if (sk) X3D_GO(0, true, false); else X3D_GO(0, false, false);
   }

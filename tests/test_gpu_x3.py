@@ -375,3 +375,30 @@ def test_encoder_x3_fused_tails_bit_identical():
             R._X3_TAIL = old
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout", [(64, 14, 256, 1024), (3, 7, 512, 2048), (1, 9, 64, 128)])
+def test_x3d_dense_prologue_equals_conv_form(N, H, Cin, Cout):
+    """x3d on a 1x1 conv's input as dense rows with the BN prologue (k = channel; round 3) == the same
+    conv through the implicit-im2col form, bit for bit (output and BN statistics)."""
+    K = _K()
+    rows = N * H * H
+    x = rnd(rows, Cin, seed=51).to(DEV)
+    s, b = (rnd(Cin, seed=52) + 1.0).to(DEV), rnd(Cin, seed=53).to(DEV)
+    w3 = split3((rnd(Cout, Cin, seed=54) * (2.0 / Cin) ** 0.5).to(DEV))
+    ws = K.gemm_workspace(DEV)
+    geo = dict(N=N, H=H, W=H, Cin=Cin, KH=1, KW=1, stride=1, pad=0, Ho=H, Wo=H)
+    outs = []
+    for dense in (True, False):
+        out = torch.empty(rows, Cout, device=DEV)
+        st = torch.zeros(2 * K.stat_tiles(rows) * Cout, device=DEV)
+        if dense:
+            prob = K.problem(rows, Cout, Cin, x, Cin, w3, Cin, out, Cout, stats=st, in_scale=s, in_shift=b)
+        else:
+            prob = K.problem(rows, Cout, Cin, x, 0, w3, Cin, out, Cout, stats=st, conv=geo, in_scale=s, in_shift=b)
+        K.gemm_x3d(prob, 0 if dense else 2, ws)
+        outs.append((out, st))
+    torch.cuda.synchronize()
+    K.sk_check([ws])
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])

@@ -72,8 +72,13 @@ def main():
         w3d = torch.empty(3 * w.numel(), device=dev, dtype=torch.bfloat16)
         K.split3_bf16(K.conv_weight_order_x3p(w, k, k, Cin).contiguous(), w3d)
         if "x3d" in arms_on and Cin % 32 == 0:
-            pd = K.problem(rows, Cout, Kd, x, Cin if dense else 0, w3d, Kd, out, Cout, **kw)
-            fns["x3d"] = lambda: K.gemm_x3d(pd, mode, ws)
+            if k == 1 and st == 1:  # 1x1: dense rows, the prologue per k = channel (round 3)
+                pd = K.problem(rows, Cout, Kd, x, Cin, w3d, Kd, out, Cout, stats=stats,
+                               in_scale=sc if pro else None, in_shift=sh if pro else None)
+                fns["x3d"] = lambda: K.gemm_x3d(pd, 0, ws)
+            else:
+                pd = K.problem(rows, Cout, Kd, x, Cin if dense else 0, w3d, Kd, out, Cout, **kw)
+                fns["x3d"] = lambda: K.gemm_x3d(pd, mode, ws)
         if "x3s" in arms_on and Kd == 64 and k == 1 and st == 1 and Cout in (64, 128, 256):
             ps = K.problem(rows, Cout, Kd, x, Cin if dense else 0, w3s, Kd, out, Cout, **kw)
             fns["x3s"] = lambda: K.gemm_x3s(ps, mode)
