@@ -796,6 +796,7 @@ int gemm_bf16_io(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
   a.p[0] = p;
   a.tiles_m[0] = (int)cdiv(p.M, bm);
   a.tiles_n[0] = (int)cdiv(p.N, bn);
+  a.plain_epi = plain_epilogue(p, bn);  // (bf16 C: the fp32 bound on M * ldc is the stricter one)
   const long long total = (long long)a.tiles_m[0] * a.tiles_n[0];
   a.tiles_begin[1] = (int)total;
   const int cus = cu_count();

@@ -226,6 +226,28 @@ gemm_bf16_kernel(const GemmArgs args) {
     unsigned short* C = reinterpret_cast<unsigned short*>(P.C);
     const long long ldc = P.ldc;
     float csum[TN], csq[TN];
+    if (args.plain_epi == 1 && m0 + BM <= M) {
+      // store-only form for a whole tile (round 3; host: plain_epilogue): one 32-bit lane offset, the row
+      // term of each register as a uniform soffset, no bounds checks or 64-bit addresses
+      const auto rc = rsrc_of(C, (unsigned)((long long)M * ldc * 2));
+      const unsigned lbase = (unsigned)((m0 + wm0 + 4 * lh) * ldc + n0 + wn0 + lr) * 2u;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        csum[j] = 0.f;
+        csq[j] = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const unsigned short h = bf16_bits(acc[i][j][r]);
+            const int rr = 32 * i + (r & 3) + 8 * (r >> 2);
+            __builtin_amdgcn_raw_buffer_store_b16(h, rc, lbase + 64u * j, (int)(rr * ldc * 2), 0);
+            const float v = bf16_val(h);
+            csum[j] += v;
+            csq[j] = fmaf(v, v, csq[j]);
+          }
+      }
+    } else
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       csum[j] = 0.f;
