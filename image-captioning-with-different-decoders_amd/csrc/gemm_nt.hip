@@ -569,6 +569,30 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
     const int relu = P.relu;
     const long long ldc = P.ldc, c_r1 = P.c_r1, c_s2 = P.c_s2;
     float csum[TN], csq[TN];
+    // store-only form (round 3) for a whole tile of C = A.B (k-split slabs included): the decoder's
+    // per-timestep GEMMs and the weight gradients. Uniform test on the problem; one 32-bit lane offset, the
+    // row term of each accumulator register as a uniform soffset, the column block as an immediate
+    const bool plain = alpha == 1.f && (z > 0 || (!bias1 && !bias2)) && beta == 0.f && !relu && c_r1 <= 0 &&
+                       m0 + BM <= M && n0 + BN <= N && (long long)(m0 + BM) * ldc * 4 < (1LL << 31);
+    if (plain) {
+      const auto rc = __builtin_amdgcn_make_buffer_rsrc(Cz, 0, (int)((long long)(m0 + BM) * ldc * 4), 0x00020000);
+      const unsigned lbase = (unsigned)(((m0 + wm0 + 4 * lh) * ldc + n0 + wn0 + lr) * 4);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        csum[j] = 0.f;
+        csq[j] = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float v = acc[i][j][r];  // fmaf(acc, 1, 0) == acc
+            const int rr = 32 * i + (r & 3) + 8 * (r >> 2);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, lbase + 128u * j, (int)(rr * ldc * 4), 0);
+            csum[j] += v;
+            csq[j] = fmaf(v, v, csq[j]);
+          }
+      }
+    } else
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       csum[j] = 0.f;
