@@ -154,6 +154,10 @@ _X3D = os.environ.get("CAPMI_X3D", "1") != "0"
 _BF16_FOLD = int(os.environ.get("CAPMI_BF16_FOLD", "0"))
 # x3 mode: layer1's K = 64 1x1 convs on the short-k streaming kernel (CAPMI_X3S=0: off, A/B)
 _X3S = os.environ.get("CAPMI_X3S", "1") != "0"
+# x3 mode, opt-in (CAPMI_X3P64=1): layer1's 3x3 (N = 64) on x3p's 256 x 64 tiles after the split pass. Faster
+# per conv (127 vs 153 us with its split pass, one box) but not in the pipelined step: 5968-5976 against
+# 5984-5987 img/s with gemm_x3 (two pairs, same box), so gemm_x3 stays
+_X3P64 = os.environ.get("CAPMI_X3P64", "0") == "1"
 # x3 mode, opt-in (CAPMI_X3_TAIL=1): a bottleneck tail relu(bn3(y3) + identity) whose output feeds the next
 # block's conv1 (a plain gemm_x3 1x1) is computed in that GEMM's A staging, which also stores the block
 # output -- bit-identical, but measured slower than the separate capmi_bn_add_relu pass (5959 vs 6138 img/s,
@@ -298,7 +302,8 @@ class EncoderRunner:
             or (kh == 1 and in_ss is None and ci == 2 * co)
             or (rows <= 3136 and not (kh == 1 and in_ss is None))
             or (kh == 1 and in_ss is not None and co == 4 * ci and rows <= 12544)))
-        x3p = (not nchw and not smallk and not x3d and x3 and in_ss is not None and co >= 128
+        x3p = (not nchw and not smallk and not x3d and x3 and in_ss is not None
+               and (co >= 128 or (co == 64 and kh == 3 and _X3P64))
                and ci % 32 == 0 and Kd >= 128 and rows >= 12544 and a_elems * 6 < (1 << 31))
         # x3s (round 3): layer1's K = 64 1x1 convs (layer1.0 conv1 / downsample on the pooled stem, every
         # layer1 conv3 on relu(bn2(y2))) on the short-k streaming kernel (gemm_x3s.hip: weight in VGPRs,

@@ -911,7 +911,8 @@ int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
   a.tiles_begin[1] = (int)total;
   const long long slots2 = 2LL * sk_cus();
   const long long rounds2 = (total + slots2 - 1) / slots2;
-  if (!x3p_force32() && total >= slots2 && (double)total / (double)(rounds2 * slots2) >= 0.7) {
+  // (256 x 64 tiles keep one workgroup per CU: layer1's 3x3 took 255 us at two per CU, 133 us at one)
+  if (!x3p_force32() && bn == 128 && total >= slots2 && (double)total / (double)(rounds2 * slots2) >= 0.7) {
     bk = 16;
     sk = false;
     return 0;

@@ -26,7 +26,7 @@ def routed(tag, rows, Cin, Cout, k, st, pro):
                                            or (rows <= 3136 and not (k == 1 and not in_ss))
                                            or (k == 1 and in_ss and Cout == 4 * Cin and rows <= 12544)):
         return "x3d"
-    if in_ss and Cout >= 128 and Cin % 32 == 0 and kd >= 128 and rows >= 12544:
+    if in_ss and (Cout >= 128 or (Cout == 64 and k == 3)) and Cin % 32 == 0 and kd >= 128 and rows >= 12544:
         return "x3p"
     return "x3"
 
