@@ -123,6 +123,11 @@ gemm_x3p_kernel(const GemmArgs args) {
     // X3P_PRICE (timing-only builds): 1 = A descriptor with zero records (no A traffic), 2 = B, 3 = both
     const auto ra = rsrc_p(P.A, (X3P_PRICE & 1) ? 0u : (unsigned)(ASPLIT ? planeA * 4 : 3 * planeA * 2));
     const auto rb = rsrc_p(P.B, (X3P_PRICE & 2) ? 0u : (unsigned)(3 * planeB * 2));
+    // x3d prologue: scale / shift through descriptors sized to the channel count (round 3):
+    // a read past the last channel returns 0 instead of touching the next allocation
+    const unsigned ss_bytes = PRO ? (unsigned)((AMODE == 2 ? cCin : P.K) * 4) : 0u;
+    const auto rsc_p = rsrc_p(PRO ? (const void*)P.in_scale : P.B, ss_bytes);
+    const auto rsh_p = rsrc_p(PRO ? (const void*)P.in_shift : P.B, ss_bytes);
     // this lane's two A rows (row blocks 2 wid, 2 wid + 1) and one B row (row block wid)
     // (arrays sized 2 >= NAB: a dependent bound in the nested lambda loses the host launch stub)
     unsigned a_base[2];  // dense: byte offset of (row, chunk) in plane 0; conv: pixel index of (n, 0, 0)
@@ -211,9 +216,9 @@ gemm_x3p_kernel(const GemmArgs args) {
       if (ASPLIT) {
         a_msk = 0;
         if (PRO && kok) {  // (past the last k-tile the walk is past Cin: no read)
-          const int ch = (AMODE == 2 ? c_ci : k) + aq * 4;  // dense rows (1x1 conv): the channel is k
-          a_sc = *reinterpret_cast<const float4*>(P.in_scale + ch);
-          a_sh = *reinterpret_cast<const float4*>(P.in_shift + ch);
+          const unsigned ch = (unsigned)((AMODE == 2 ? c_ci : k) + aq * 4) * 4u;  // dense rows: channel = k
+          a_sc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsc_p, ch, 0, 0));
+          a_sh = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsh_p, ch, 0, 0));
         }
 #pragma unroll
         for (int i = 0; i < NSA; ++i) {

@@ -402,3 +402,36 @@ def test_x3d_dense_prologue_equals_conv_form(N, H, Cin, Cout):
     K.sk_check([ws])
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_x3d_prologue_scale_shift_at_allocation_end():
+    """VERDICT r2 weak 12 (the over-read class of the round-2 x3d fault): the BN scale / shift are the LAST
+    Cin floats of their buffers, followed only by NaN sentinels in the same allocation; the x3d prologue reads
+    them through descriptors sized to Cin, so the result equals the one with padded copies bit for bit and no
+    NaN reaches the output (a stride-2 3x3 and a 1x1 conv input, batch 2)."""
+    K = _K()
+    ws = K.gemm_workspace(DEV)
+    for (N, H, Cin, Cout, k, stride) in [(2, 28, 128, 256, 3, 2), (2, 14, 256, 1024, 1, 1)]:
+        pad = k // 2
+        Ho = (H + 2 * pad - k) // stride + 1
+        rows, Kd = N * Ho * Ho, k * k * Cin
+        x = rnd(N * H * H, Cin, seed=61).to(DEV)
+        s, b = (rnd(Cin, seed=62) + 1.0).to(DEV), rnd(Cin, seed=63).to(DEV)
+        tail = torch.full((2, Cin + 64), float("nan"), device=DEV)  # [scale | NaN x 64], [shift | NaN x 64]
+        tail[0, :Cin], tail[1, :Cin] = s, b
+        w3 = split3(K.conv_weight_order_x3p((rnd(Cout, Kd, seed=64) * (2.0 / Kd) ** 0.5).to(DEV), k, k, Cin)
+                    .contiguous())
+        geo = dict(N=N, H=H, W=H, Cin=Cin, KH=k, KW=k, stride=stride, pad=pad, Ho=Ho, Wo=Ho)
+        outs = []
+        for sc, sh in ((s.clone(), b.clone()), (tail[0, :Cin], tail[1, :Cin])):
+            out = torch.empty(rows, Cout, device=DEV)
+            if k == 1 and stride == 1:
+                prob, mode = K.problem(rows, Cout, Kd, x, Cin, w3, Kd, out, Cout, in_scale=sc, in_shift=sh), 0
+            else:
+                prob, mode = K.problem(rows, Cout, Kd, x, 0, w3, Kd, out, Cout, conv=geo, in_scale=sc, in_shift=sh), 2
+            K.gemm_x3d(prob, mode, ws)
+            outs.append(out)
+        torch.cuda.synchronize()
+        K.sk_check([ws])
+        assert bool(torch.isfinite(outs[1]).all())
+        assert torch.equal(outs[0], outs[1])
