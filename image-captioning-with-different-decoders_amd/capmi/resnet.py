@@ -682,6 +682,8 @@ _FT_DGRAD1_KROWS = os.environ.get("CAPMI_FT_DGRAD1_KROWS", "0") != "0"
 # 1x1 dgrads on x3d: neutral in round 2 (1666 both); with the store-only / beta epilogue
 # 1676-1680 -> 1711-1716 img/s (two pairs, one box): on
 _FT_DGRAD1_X3D = os.environ.get("CAPMI_FT_DGRAD1_X3D", "1") != "0"
+# of those, the long-k ones (K >= 4 N: conv3's) on gemm_x3 instead of x3d (CAPMI_FT_DGRAD1_X3=0: all x3d)
+_FT_DGRAD1_X3 = os.environ.get("CAPMI_FT_DGRAD1_X3", "1") != "0"
 
 
 class FineTuneRunner:
@@ -886,11 +888,18 @@ class FineTuneRunner:
                     src = word[:n * kd]
                 K.split3_bf16(src, w3[:3 * n * kd])
             prob.B = w3.data_ptr()
-            launch = lambda: K.gemm_x3d(prob, amode, self.r._ws["sk"])  # noqa: E731
+            if not conv and _FT_DGRAD1_X3 and kd >= 4 * n and prob.c_r1 <= 0:
+                # long-k 1x1 data gradients (conv3's: K = 4 N) on gemm_x3 (the same split planes; 1x1: plain k
+                # order), as the forward's long-k plain c1 convs
+                launch = lambda: K.gemm_x3(prob, amode, self.r._ws["sk"])  # noqa: E731
+                name = K.gemm_x3_kernel_name(prob, amode)
+            else:
+                launch = lambda: K.gemm_x3d(prob, amode, self.r._ws["sk"])  # noqa: E731
+                name = K.gemm_x3d_kernel_name(prob, amode)
             if hook is None:
                 launch()
             else:
-                hook(tag, flops, launch, K.gemm_x3d_kernel_name(prob, amode))
+                hook(tag, flops, launch, name)
 
         K.adaptive_avgpool_bwd_nhwc(dfeat.contiguous(), N, stt["H"], stt["W"], stt["C"], stt["OH"], stt["OW"],
                                     dA[0])
