@@ -858,7 +858,9 @@ int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gemm
   const long long slots = sk_cus();
   const int nkt = p.K / 32;
   const long long rounds = (total + slots - 1) / slots;
-  sk = !sk_off() && total > 0 && nkt >= 8 && (double)total / (double)(rounds * slots) < 0.9;
+  // (round 3) more than two rounds of tiles: data-parallel -- the hardware's dynamic dispatch beat the hybrid
+  // schedule there (layer1 c1: 55 vs 69 us, layer1 3x3: 154 vs 156; CAPMI_SK_OFF A/B on one box)
+  sk = !sk_off() && total > 0 && nkt >= 8 && rounds <= 2 && (double)total / (double)(rounds * slots) < 0.9;
   return 0;
 }
 
