@@ -479,7 +479,8 @@ class EncoderRunner:
             tiles = -(-rows // 128) * -(-co // bn_)
             slots = 2 * torch.cuda.get_device_properties(x.device).multi_processor_count
             rounds = -(-tiles // slots)
-            sk = Kd // 64 >= 4 and tiles / (rounds * slots) < 0.9
+            sk = (os.environ.get("CAPMI_BF16_SK", "0") == "1" and os.environ.get("CAPMI_SK_OFF", "0") != "1"
+                  and Kd // 64 >= 4 and tiles / (rounds * slots) < 0.9)  # (gemm.hip gemm_bf16_io)
             key = (f"gemm_bf16_kernel<128, {bn_}, {mode}, {'true' if sk else 'false'}, "
                    f"{'true' if in_ss is not None else 'false'}>")
             self.conv_hook(tag, 2.0 * rows * co * Kd, launch, key)

@@ -803,7 +803,14 @@ int gemm_bf16_io(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
   const long long slots = (long long)sk_cus() * 2;
   const int nkt = p.K / 64;
   const long long rounds = (total + slots - 1) / slots;
-  const bool sk = !sk_off() && workspace != nullptr && nkt >= 4 && (double)total / (double)(rounds * slots) < 0.9;
+  // (round 3) stream-K for the bf16 convs only on CAPMI_BF16_SK=1: data-parallel grids measured faster in the
+  // pipelined bf16 step (config 5)
+  static const bool bf16_sk = [] {
+    const char* e = getenv("CAPMI_BF16_SK");
+    return e && e[0] == '1';
+  }();
+  const bool sk = bf16_sk && !sk_off() && workspace != nullptr && nkt >= 4 &&
+                  (double)total / (double)(rounds * slots) < 0.9;
   if (!sk) return gemm_bf16_launch(a, amode, bm, bn, (int)total, s);
   CAPMI_REQUIRE(aligned16(workspace), CAPMI_EINVAL);
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
