@@ -828,7 +828,8 @@ namespace {
 // CAPMI_SK_FAMILY_OFF = bit mask of the x3 kernel families launched data-parallel instead of stream-K
 // (1 gemm_x3, 2 x3p, 4 x3d). Default 1 (round 3): in the pipelined step, where the decoder stream holds CUs
 // a stream-K worker may wait on, gemm_x3 measured faster data-parallel (headline 5987-5995 -> 6035-6048,
-// fine-tune 1775 -> 1795 img/s, one box); x3p (-10 %) and x3d (-7 %) keep stream-K
+// fine-tune 1775 -> 1795 img/s, one box; small grids excepted, x3_plan); x3p (-10 %) and x3d (-7 %) keep
+// stream-K
 bool sk_family_off(int bit) {
   static const int mask = [] {
     const char* e = getenv("CAPMI_SK_FAMILY_OFF");
@@ -879,7 +880,9 @@ int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gemm
   const long long rounds = (total + slots - 1) / slots;
   // (round 3) more than two rounds of tiles: data-parallel -- the hardware's dynamic dispatch beat the hybrid
   // schedule there (layer1 c1: 55 vs 69 us, layer1 3x3: 154 vs 156; CAPMI_SK_OFF A/B on one box)
-  sk = !sk_off() && !sk_family_off(1) && total > 0 && nkt >= 8 && rounds <= 2 &&
+  // with the family data-parallel (the default), grids under a quarter of the CUs keep stream-K: a few long-k
+  // tiles would otherwise run on a few CUs and accumulate the whole k serially (conv grids are >= 100 tiles)
+  sk = !sk_off() && (!sk_family_off(1) || total * 4 < slots) && total > 0 && nkt >= 8 && rounds <= 2 &&
        (double)total / (double)(rounds * slots) < 0.9;
   return 0;
 }
