@@ -87,6 +87,11 @@ def test_gemm_sk_plan_on_host():
     rc, (bm, bn, sk, generic, nt) = plan(256, flags=4)
     assert rc == 0 and (bm, bn, generic, nt) == (128, 128, 0, 512)
     assert plan(64, flags=4)[1][1] == 64
+    # gemm_x3 runs data-parallel by default (CAPMI_SK_FAMILY_OFF bit 1): 196 tiles -> no stream-K; a grid
+    # under a quarter of the CUs (three images: 10 tiles of 72 k-steps) keeps it
+    assert sk == 0
+    rc, (bm, bn, sk, generic, nt) = plan(256, flags=4, M=588)
+    assert rc == 0 and sk == 1
     # X3P reports its k-tile depth in `generic`: 32 + stream-K for 98 tiles (< 256 CUs), 16 (two
     # workgroups per CU, data-parallel) for 1568 tiles (0.77 of 4 rounds of 512 slots)
     rc, (bm, bn, sk, generic, nt) = plan(256, flags=8)
