@@ -877,6 +877,19 @@ int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gemm
   a.tiles_begin[1] = (int)total;
   const long long slots = sk_cus();
   const int nkt = p.K / 32;
+  // A/B switch CAPMI_X3_SPLITN=1: a data-parallel grid under one round of 128-wide tiles takes 64-wide ones
+  static const bool splitn = [] {
+    const char* e = getenv("CAPMI_X3_SPLITN");
+    return e && atoi(e) == 1;
+  }();
+  if (splitn && tile == CAPMI_TILE_AUTO && bn == 128 && sk_family_off(1) && total < slots && total * 4 >= slots &&
+      p.N % 64 == 0) {
+    bn = 64;
+    a.tiles_n[0] = (int)cdiv(p.N, bn);
+    a.plain_epi = plain_epilogue(p, bn);
+    total = (long long)a.tiles_m[0] * a.tiles_n[0];
+    a.tiles_begin[1] = (int)total;
+  }
   const long long rounds = (total + slots - 1) / slots;
   // (round 3) more than two rounds of tiles: data-parallel -- the hardware's dynamic dispatch beat the hybrid
   // schedule there (layer1 c1: 55 vs 69 us, layer1 3x3: 154 vs 156; CAPMI_SK_OFF A/B on one box)
