@@ -21,9 +21,10 @@ c_ull = ctypes.c_ulonglong
 CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_A_CONV_NHWC, CAPMI_A_CONV_NCHW, CAPMI_A_CONV_NHWC4 = 0, 1, 2, 3, 4
 CAPMI_B_NMAJOR_W, CAPMI_B_KROWS, CAPMI_B_CONV_NHWC = 0, 1, 2
 CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO, CAPMI_TILE_128_W8 = 0, 1, 2, 3, 4
+CAPMI_TILE_128x256 = 5
 CAPMI_MAX_GROUP = 4
 CAPMI_COLSUM_GROUPS = 64
-ABI_VERSION = 18
+ABI_VERSION = 19
 CAPMI_BNB_RELU_Y, CAPMI_BNB_RELU_OUT = 0, 1
 CAPMI_BNB_MAX_SLABS = 256
 CAPMI_GEMM_BF16 = 1
@@ -33,8 +34,7 @@ CAPMI_GEMM_X3P = 8
 CAPMI_GEMM_SPLIT3 = 16
 CAPMI_GEMM_X3D = 32
 CAPMI_GEMM_X3S = 64
-CAPMI_BNFA_SPLIT3, CAPMI_BNFA_ADD_RELU, CAPMI_BNFA_RELU_BF16, CAPMI_BNFA_ADD_RELU_BF16 = 0, 1, 2, 3
-CAPMI_BNFA_MAX_TILES = 256
+CAPMI_GEMM_X3W = 128
 
 
 class GemmProblem(ctypes.Structure):
@@ -50,7 +50,6 @@ class GemmProblem(ctypes.Structure):
         ("cN", c_int), ("cH", c_int), ("cW", c_int), ("cCin", c_int), ("cKH", c_int),
         ("cKW", c_int), ("cStride", c_int), ("cPad", c_int), ("cHo", c_int), ("cWo", c_int),
         ("in_scale", c_vp), ("in_shift", c_vp),
-        ("in_res", c_vp), ("in_res_scale", c_vp), ("in_res_shift", c_vp), ("in_out", c_vp),
     ]
 
 
@@ -79,8 +78,6 @@ _SIGS = {
     "capmi_gemm_workspace_bytes": [],
     "capmi_gemm_workspace_flag_bytes": [],
     "capmi_gemm_sk": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_vp, c_ll, c_vp],
-    "capmi_bn_finalize_apply": [c_int, c_vp, c_int, c_int, c_ll, c_vp, c_vp, c_vp, c_vp, c_float, c_float, c_vp,
-                                c_vp, c_vp, c_vp, c_vp, c_ll, c_vp],
     "capmi_gemm_ex": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_int, c_int, c_vp],
     "capmi_gemm_sk_ex": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_int, c_vp, c_ll, c_vp],
     "capmi_gemm_sk_plan": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp],

@@ -9,8 +9,8 @@ import weakref
 import torch
 
 from ._lib import DstepEpi, DstepSeg
-from ._lib import (CAPMI_A_KMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_GEMM_BF16_IO, CAPMI_GEMM_X3, CAPMI_GEMM_X3P,
-                   CAPMI_GEMM_SPLIT3, CAPMI_GEMM_X3D, CAPMI_GEMM_X3S,
+from ._lib import (CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_GEMM_BF16_IO, CAPMI_GEMM_X3, CAPMI_GEMM_X3P,
+                   CAPMI_GEMM_SPLIT3, CAPMI_GEMM_X3D, CAPMI_GEMM_X3S, CAPMI_GEMM_X3W,
                    CAPMI_COLSUM_GROUPS, CAPMI_TILE_128, CAPMI_TILE_64,
                    CAPMI_TILE_128x64, CAPMI_TILE_AUTO, GemmProblem, call, lib)
 
@@ -40,13 +40,10 @@ def _cuda(*ts, dtype=F32):
 # --------------------------------------------------------------------------------------
 def problem(M, N, K, A, lda, B, ldb, C, ldc, *, a_r1=0, a_s2=0, c_r1=0, c_s2=0, ksplit=1,
             c_split_stride=0, bias=None, bias2=None, alpha=1.0, alpha_ptr=None, beta=0.0,
-            relu=False, stats=None, conv=None, in_scale=None, in_shift=None, in_res=None, in_res_scale=None,
-            in_res_shift=None, in_out=None):
+            relu=False, stats=None, conv=None, in_scale=None, in_shift=None):
     """Build one ``capmi_gemm_problem``. A/B/C are tensors (or views) whose data_ptr is the
-    operand origin; ld* are element strides. ``conv`` = dict(N,H,W,Cin,KH,KW,stride,pad,Ho,Wo).
-    in_res / in_res_scale / in_res_shift / in_out: the fused bottleneck tail of CAPMI_GEMM_X3 dense
-    (A := relu(A*in_scale + in_shift + residual), stored to in_out too; include/capmi.h, ABI 18)."""
-    _cuda(C, bias, bias2, stats, in_scale, in_shift, in_res, in_res_scale, in_res_shift, in_out)
+    operand origin; ld* are element strides. ``conv`` = dict(N,H,W,Cin,KH,KW,stride,pad,Ho,Wo)."""
+    _cuda(C, bias, bias2, stats, in_scale, in_shift)
     for t_ in (A, B):  # bf16: the split planes of gemm_x3 (B) / gemm_x3p (A and B)
         _cuda(t_, dtype=torch.bfloat16 if t_ is not None and t_.dtype == torch.bfloat16 else F32)
     p = GemmProblem()
@@ -63,7 +60,6 @@ def problem(M, N, K, A, lda, B, ldb, C, ldc, *, a_r1=0, a_s2=0, c_r1=0, c_s2=0, 
         p.cKH, p.cKW, p.cStride, p.cPad = conv["KH"], conv["KW"], conv["stride"], conv["pad"]
         p.cHo, p.cWo = conv["Ho"], conv["Wo"]
     p.in_scale, p.in_shift = ptr(in_scale), ptr(in_shift)
-    p.in_res, p.in_res_scale, p.in_res_shift, p.in_out = ptr(in_res), ptr(in_res_scale), ptr(in_res_shift), ptr(in_out)
     return p
 
 
@@ -121,19 +117,17 @@ def gemm_sk(prob, amode, workspace, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W
          workspace.numel() * 4, stream())
 
 
-def problem_bf16(M, N, K, A, lda, B, ldb, C, ldc, *, stats=None, conv=None, in_scale=None, in_shift=None):
+def problem_bf16(M, N, K, A, lda, B, ldb, C, ldc, *, stats=None, conv=None):
     """capmi_gemm_problem over bf16 A / B / C (CAPMI_GEMM_BF16_IO): plain conv or dense GEMM,
-    fp32 BN statistics of the stored (bf16) output; in_scale / in_shift (fp32 [Cin]): the input's
-    BN-apply + ReLU in the A staging (bf16 RNE, capmi_bn_relu_bf16's arithmetic; round 3)."""
+    fp32 BN statistics of the stored (bf16) output."""
     _cuda(A, B, C, dtype=torch.bfloat16)
-    _cuda(stats, in_scale, in_shift)
+    _cuda(stats)
     p = GemmProblem()
     p.M, p.N, p.K, p.ksplit = int(M), int(N), int(K), 1
     p.A, p.lda, p.B, p.ldb = ptr(A), int(lda), ptr(B), int(ldb)
     p.C, p.ldc = ptr(C), int(ldc)
     p.alpha, p.beta = 1.0, 0.0
     p.stats = ptr(stats)
-    p.in_scale, p.in_shift = ptr(in_scale), ptr(in_shift)
     if conv is not None:
         p.cN, p.cH, p.cW, p.cCin = conv["N"], conv["H"], conv["W"], conv["Cin"]
         p.cKH, p.cKW, p.cStride, p.cPad = conv["KH"], conv["KW"], conv["stride"], conv["pad"]
@@ -191,11 +185,12 @@ def gemm_x3p(prob, amode, workspace):
          ptr(workspace), workspace.numel() * 4, stream())
 
 
-def gemm_x3d(prob, amode, workspace):
+def gemm_x3d(prob, amode, workspace, tile=CAPMI_TILE_AUTO):
     """CAPMI_GEMM_X3D: A fp32 (dense, or the NHWC conv input with the optional BN prologue) split
-    in-kernel x B = three bf16 planes in the x3p k order (conv_weight_order_x3p + split3_bf16)."""
+    in-kernel x B = three bf16 planes in the x3p k order (conv_weight_order_x3p + split3_bf16).
+    tile CAPMI_TILE_128x256 (5): 128 x 256 tiles on dense rows."""
     _cuda(workspace, dtype=torch.int32)
-    call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3D,
+    call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, tile, CAPMI_GEMM_X3D,
          ptr(workspace), workspace.numel() * 4, stream())
 
 
@@ -204,6 +199,29 @@ def gemm_x3s(prob, amode):
     B = three bf16 planes (split3_bf16), store-only epilogue; persistent, no workspace."""
     call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3S,
          None, 0, stream())
+
+
+def gemm_x3w(prob, bmode, workspace):
+    """CAPMI_GEMM_X3W: the conv weight gradient dW = dY^T . B (A = dY fp32 k rows, CAPMI_A_MMAJOR; B fp32 k
+    rows, CAPMI_B_KROWS, or the NHWC conv input's im2col, CAPMI_B_CONV_NHWC, with the optional BN prologue);
+    k-split partial slabs in the stream-K workspace."""
+    _cuda(workspace, dtype=torch.int32)
+    call("capmi_gemm_sk_ex", ctypes.byref(prob), CAPMI_A_MMAJOR, bmode, CAPMI_TILE_AUTO, CAPMI_GEMM_X3W,
+         ptr(workspace), workspace.numel() * 4, stream())
+
+
+def gemm_x3w_kernel_name(prob, bmode):
+    v = [ctypes.c_int(0) for _ in range(5)]
+    call("capmi_gemm_sk_plan", ctypes.byref(prob), CAPMI_A_MMAJOR, bmode, CAPMI_TILE_AUTO, CAPMI_GEMM_X3W,
+         *[ctypes.byref(x) for x in v])
+    return f"gemm_x3w_kernel<{bmode}, {'true' if v[2].value else 'false'}>"
+
+
+def gemm_x3w_ok(prob, bmode):
+    """True when CAPMI_GEMM_X3W takes this weight-gradient problem (its planner accepts it)."""
+    v = [ctypes.c_int(0) for _ in range(5)]
+    return lib.capmi_gemm_sk_plan(ctypes.byref(prob), CAPMI_A_MMAJOR, bmode, CAPMI_TILE_AUTO, CAPMI_GEMM_X3W,
+                                  *[ctypes.byref(x) for x in v]) == 0
 
 
 def gemm_x3s_ok(prob, amode):
@@ -218,19 +236,20 @@ def gemm_x3s_kernel_name(prob, amode):
     return f"gemm_x3s_kernel<{ncb}, {'true' if prob.in_scale else 'false'}>"
 
 
-def gemm_x3d_kernel_name(prob, amode):
+def gemm_x3d_kernel_name(prob, amode, tile=CAPMI_TILE_AUTO):
     v = [ctypes.c_int(0) for _ in range(5)]
-    call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3D,
+    call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, tile, CAPMI_GEMM_X3D,
          *[ctypes.byref(x) for x in v])
     b = lambda x: "true" if x else "false"  # noqa: E731
-    return f"gemm_x3p_kernel<{amode}, {b(v[2].value)}, 32, true, {b(bool(prob.in_scale))}, 128>"
+    wide = ", true" if v[0].value == 128 else ""
+    return f"gemm_x3p_kernel<{amode}, {b(v[2].value)}, 32, true, {b(bool(prob.in_scale))}{wide}>"
 
 
 def gemm_x3p_kernel_name(prob, amode):
     v = [ctypes.c_int(0) for _ in range(5)]
     call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3P,
          *[ctypes.byref(x) for x in v])
-    return f"gemm_x3p_kernel<{amode}, {'true' if v[2].value else 'false'}, {v[3].value}, false, false, {v[1].value}>"
+    return f"gemm_x3p_kernel<{amode}, {'true' if v[2].value else 'false'}, {v[3].value}, false, false>"
 
 
 def gemm_x3_kernel_name(prob, amode, tile=CAPMI_TILE_AUTO):
@@ -330,21 +349,6 @@ def bn_finalize(stats, tiles, C, count, gamma, beta, running_mean, running_var, 
     call("capmi_bn_finalize", ptr(stats), tiles, C, count, ptr(gamma), ptr(beta), ptr(running_mean),
          ptr(running_var), momentum, eps, ptr(scale), ptr(shift), ptr(save_mean), ptr(save_var),
          ptr(work), stream())
-
-
-def bn_finalize_apply(op, stats, tiles, C, count, gamma, beta, running_mean, running_var, momentum, eps,
-                      scale, shift, y, out, rows, res=None):
-    """capmi_bn_finalize_apply: the train-mode BN finalize fused into its consumer pass (op =
-    CAPMI_BNFA_SPLIT3 / ADD_RELU / RELU_BF16 / ADD_RELU_BF16)."""
-    _cuda(stats, gamma, beta, running_mean, running_var, scale, shift)
-    bf = op in (2, 3)
-    _cuda(y, res, dtype=torch.bfloat16 if bf else F32)
-    _cuda(out, dtype=torch.bfloat16 if op != 1 else F32)
-    if op == 0 and out.numel() < 3 * rows * C:
-        raise ValueError("bn_finalize_apply: the split planes need 3 * rows * C elements")
-    call("capmi_bn_finalize_apply", int(op), ptr(stats), int(tiles), int(C), int(count), ptr(gamma), ptr(beta),
-         ptr(running_mean), ptr(running_var), float(momentum), float(eps), ptr(scale), ptr(shift), ptr(y), ptr(res),
-         ptr(out), int(rows), stream())
 
 
 def bn_eval_params(gamma, beta, rm, rv, C, eps, scale, shift):

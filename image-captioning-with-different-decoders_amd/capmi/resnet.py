@@ -21,8 +21,6 @@ import torch.nn as nn
 from . import kernels as K
 from ._lib import CAPMI_A_CONV_NHWC, CAPMI_A_CONV_NHWC4, CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_B_CONV_NHWC
 from ._lib import CAPMI_B_KROWS, CAPMI_B_NMAJOR_W, CAPMI_GEMM_BF16, CAPMI_GEMM_SPLIT3
-from ._lib import CAPMI_BNFA_ADD_RELU, CAPMI_BNFA_ADD_RELU_BF16, CAPMI_BNFA_MAX_TILES, CAPMI_BNFA_RELU_BF16
-from ._lib import CAPMI_BNFA_SPLIT3
 
 AK, AMM, AC = CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_A_CONV_NHWC
 BW, BKR, BCONV = CAPMI_B_NMAJOR_W, CAPMI_B_KROWS, CAPMI_B_CONV_NHWC
@@ -147,62 +145,9 @@ def pool_dup(H, W, out_hw):
 _X3_SMALLK = int(os.environ.get("CAPMI_X3_SMALLK", "0"))
 # x3 mode: route the shapes where it measured fastest to the x3d kernel (CAPMI_X3D=0: off, A/B)
 _X3D = os.environ.get("CAPMI_X3D", "1") != "0"
-# bf16 encoder, opt-in: the conv input's BN-apply + ReLU in the consumer GEMM's A staging instead of a
-# capmi_bn_relu_bf16 pass (bit mask: 1 = conv2's input, 2 = conv3's input). Bit-identical, measured slower on
-# config 5 (same box: 10224 img/s with the passes, 10124 with conv3's folded, 9744 with both): at bf16 MFMA
-# rates the per-element unpack / fma / max / pack VALU in the staging costs more than the pass it saves
-_BF16_FOLD = int(os.environ.get("CAPMI_BF16_FOLD", "0"))
+_R4_ROUTE = os.environ.get("CAPMI_R4_ROUTE", "1") != "0"  # (temporary A/B: layer2 c3 and layer4 c1 on x3d)
 # x3 mode: layer1's K = 64 1x1 convs on the short-k streaming kernel (CAPMI_X3S=0: off, A/B)
 _X3S = os.environ.get("CAPMI_X3S", "1") != "0"
-# x3 mode, opt-in (CAPMI_X3P64=1): layer1's 3x3 (N = 64) on x3p's 256 x 64 tiles after the split pass. Faster
-# per conv (127 vs 153 us with its split pass, one box) but not in the pipelined step: 5968-5976 against
-# 5984-5987 img/s with gemm_x3 (two pairs, same box), so gemm_x3 stays
-_X3P64 = os.environ.get("CAPMI_X3P64", "0") == "1"
-# x3 mode, opt-in (CAPMI_X3_TAIL=1): a bottleneck tail relu(bn3(y3) + identity) whose output feeds the next
-# block's conv1 (a plain gemm_x3 1x1) is computed in that GEMM's A staging, which also stores the block
-# output -- bit-identical, but measured slower than the separate capmi_bn_add_relu pass (5959 vs 6138 img/s,
-# same box: the GEMM's second column tile re-reads both tail operands and its A staging doubles)
-_X3_TAIL = os.environ.get("CAPMI_X3_TAIL", "0") == "1"
-
-
-class _Tail:
-    """A deferred bottleneck tail out = relu(y*s + b + res') with res' = res*rs + rb (downsample BN) or
-    res: the arguments of capmi_bn_add_relu, run as the next conv1's fused prologue or, when that conv
-    cannot take it, materialised just before it (``now``)."""
-
-    def __init__(self, y, s, b, res, out, rows, C, rs=None, rb=None):
-        self.y, self.s, self.b, self.res, self.out, self.rows, self.C, self.rs, self.rb = y, s, b, res, out, rows, C, rs, rb
-
-    def now(self):
-        K.bn_add_relu(self.y, self.s, self.b, self.res, self.out, self.rows, self.C, res_scale=self.rs,
-                      res_shift=self.rb)
-# train-mode BN finalize fused into the consumer pass where it fits (capmi_bn_finalize_apply), opt-in
-# with CAPMI_BN_FUSE=1: measured slower than the separate finalize launch (headline 5558 -> 5458,
-# bf16 config 10559 -> 9732 img/s; DESIGN.md 4.7)
-_BN_FUSE = os.environ.get("CAPMI_BN_FUSE", "0") == "1"
-
-
-class _DeferredBN:
-    """A train-mode BatchNorm whose finalize is left to the pass that consumes the conv output
-    (capmi_bn_finalize_apply); ``now()`` runs the plain finalize instead and returns (scale, shift)."""
-
-    def __init__(self, runner, ws, bn, rows):
-        self.r, self.ws, self.bn, self.rows = runner, ws, bn, rows
-
-    def args(self):
-        bn, ws = self.bn, self.ws
-        s, b = self.r._ss(ws, bn)
-        mom = 0.1 if bn.momentum is None else bn.momentum
-        track = bn.track_running_stats
-        return (ws["stats"], K.stat_tiles(self.rows), bn.num_features, self.rows, bn.weight, bn.bias,
-                bn.running_mean if track else None, bn.running_var if track else None, mom, bn.eps, s, b)
-
-    def apply(self, op, y, out, res=None):
-        K.bn_finalize_apply(op, *self.args(), y, out, self.rows, res=res)
-
-    def now(self):
-        return self.r._bn(self.ws, self.bn, self.rows, True)
-
 
 class EncoderRunner:
     """Launch plan for the frozen ResNet-101 conv stack (children()[:-2] of torchvision's
@@ -266,15 +211,7 @@ class EncoderRunner:
             K.bn_eval_params(bn.weight, bn.bias, bn.running_mean, bn.running_var, C, bn.eps, s, b)
         return s, b
 
-    def _bn_defer(self, ws, bn, rows, train):
-        """As _bn, but a train-mode BN small enough for capmi_bn_finalize_apply (layer3/4) comes back
-        as a _DeferredBN for its consumer to finalize."""
-        if (train and _BN_FUSE and K.stat_tiles(rows) <= CAPMI_BNFA_MAX_TILES and bn.num_features % 32 == 0
-                and bn.weight is not None):
-            return _DeferredBN(self, ws, bn, rows)
-        return self._bn(ws, bn, rows, train)
-
-    def _conv(self, tag, x, conv, out, N, H, W, train, in_ss=None, nchw=False, tail=None):
+    def _conv(self, tag, x, conv, out, N, H, W, train, in_ss=None, nchw=False):
         co, ci, kh, kw = conv.weight.shape
         st, pd = conv.stride[0], conv.padding[0]
         Ho, Wo = (H + 2 * pd - kh) // st + 1, (W + 2 * pd - kw) // st + 1
@@ -301,21 +238,17 @@ class EncoderRunner:
             st == 2
             or (kh == 1 and in_ss is None and ci == 2 * co)
             or (rows <= 3136 and not (kh == 1 and in_ss is None))
-            or (kh == 1 and in_ss is not None and co == 4 * ci and rows <= 12544)))
+            or (kh == 1 and in_ss is not None and co == 4 * ci and rows <= 12544)
+            or (_R4_ROUTE and kh == 1 and in_ss is not None and co == 4 * ci)
+            or (_R4_ROUTE and kh == 1 and in_ss is None and rows <= 3136)))
         x3p = (not nchw and not smallk and not x3d and x3 and in_ss is not None
-               and (co >= 128 or (co == 64 and kh == 3 and _X3P64))
+               and co >= 128
                and ci % 32 == 0 and Kd >= 128 and rows >= 12544 and a_elems * 6 < (1 << 31))
         # x3s (round 3): layer1's K = 64 1x1 convs (layer1.0 conv1 / downsample on the pooled stem, every
         # layer1 conv3 on relu(bn2(y2))) on the short-k streaming kernel (gemm_x3s.hip: weight in VGPRs,
         # persistent 64-row tiles, two workgroups per CU)
         x3s = (_X3S and x3 and not nchw and Kd == 64 and kh == 1 and st == 1 and pd == 0 and co in (64, 128, 256)
                and rows * co * 4 < (1 << 31))  # (its store-only epilogue addresses C with 32-bit offsets)
-        if isinstance(in_ss, _DeferredBN) and not x3p:
-            in_ss = in_ss.now()  # only the x3p split pass takes the finalize fused
-        if tail is not None and not (x3 and not x3s and not x3d and not x3p and not smallk and not nchw and kh == 1
-                                     and st == 1 and in_ss is None and Kd % 32 == 0 and Kd == ci):
-            tail.now()  # this conv cannot take the fused tail: the block output first
-            tail = None
         if x3s:
             w3 = self._packed_x3(conv)
             if in_ss is None:
@@ -372,10 +305,7 @@ class EncoderRunner:
             # 4-8x); layer1's K = 64 c3 (no gain once the split pass is counted) and layer4's
             # 3136-row grids keep the in-kernel split (gemm_x3.hip)
             xp = self._x3p_buffer(self._ws)
-            if isinstance(in_ss, _DeferredBN):
-                in_ss.apply(CAPMI_BNFA_SPLIT3, x, xp)  # finalize of the input's BN + split, one pass
-            else:
-                K.bn_relu_split3(x, in_ss[0], in_ss[1], N * H * W, ci, xp)
+            K.bn_relu_split3(x, in_ss[0], in_ss[1], N * H * W, ci, xp)
             w3 = self._packed_x3(conv, tap_inner=True)
             if kh == 1 and st == 1:
                 prob, mode = K.problem(rows, co, Kd, xp, ci, w3, Kd, out, co, **kw_), CAPMI_A_KMAJOR
@@ -390,11 +320,7 @@ class EncoderRunner:
         elif kh == 1 and st == 1 and in_ss is None:
             if x3 and Kd % 32 == 0:
                 w = self._packed_x3(conv)
-            if tail is not None:  # x (= tail.out) is written by this GEMM from the tail's operands
-                prob = K.problem(rows, co, Kd, tail.y, ci, w, Kd, out, co, in_scale=tail.s, in_shift=tail.b,
-                                 in_res=tail.res, in_res_scale=tail.rs, in_res_shift=tail.rb, in_out=tail.out, **kw_)
-            else:
-                prob = K.problem(rows, co, Kd, x, ci, w, Kd, out, co, **kw_)
+            prob = K.problem(rows, co, Kd, x, ci, w, Kd, out, co, **kw_)
             mode = CAPMI_A_KMAJOR
         else:
             sc, sh = in_ss if in_ss is not None else (None, None)
@@ -455,9 +381,9 @@ class EncoderRunner:
             self.packed.cache[key] = ent
         return ent[2]
 
-    def _conv_bf16(self, tag, x, conv, out, N, H, W, train, in_ss=None):
-        """bf16 NHWC x -> bf16 NHWC out (CAPMI_GEMM_BF16_IO), BN statistics into ws['stats']; in_ss = (scale,
-        shift): the input's BN-apply + ReLU in the GEMM's A staging (round 3) instead of a materialising pass."""
+    def _conv_bf16(self, tag, x, conv, out, N, H, W, train):
+        """bf16 NHWC x -> bf16 NHWC out (CAPMI_GEMM_BF16_IO), BN statistics into ws['stats']; x is the conv
+        input itself (relu(bn(y)) materialised in bf16 by capmi_bn_relu_bf16)."""
         co, ci, kh, kw = conv.weight.shape
         st, pd = conv.stride[0], conv.padding[0]
         Ho, Wo = (H + 2 * pd - kh) // st + 1, (W + 2 * pd - kw) // st + 1
@@ -465,13 +391,11 @@ class EncoderRunner:
         Kd = ci * kh * kw
         w = self._packed_bf16(conv)
         stats = self._ws["stats"] if train else None
-        sc, sh = in_ss if in_ss is not None else (None, None)
         if kh == 1 and st == 1:
-            prob, mode = K.problem_bf16(rows, co, Kd, x, ci, w, Kd, out, co, stats=stats, in_scale=sc, in_shift=sh), AK
+            prob, mode = K.problem_bf16(rows, co, Kd, x, ci, w, Kd, out, co, stats=stats), AK
         else:
             geo = dict(N=N, H=H, W=W, Cin=ci, KH=kh, KW=kw, stride=st, pad=pd, Ho=Ho, Wo=Wo)
-            prob, mode = K.problem_bf16(rows, co, Kd, x, 0, w, Kd, out, co, stats=stats, conv=geo, in_scale=sc,
-                                        in_shift=sh), AC
+            prob, mode = K.problem_bf16(rows, co, Kd, x, 0, w, Kd, out, co, stats=stats, conv=geo), AC
         launch = lambda: K.gemm_bf16(prob, mode, self._ws["sk"], K.TILE_AUTO)  # noqa: E731
         if self.conv_hook is not None:
             # the launch capmi_gemm_sk_ex makes for CAPMI_GEMM_BF16_IO (gemm.hip: gemm_bf16_io)
@@ -481,23 +405,16 @@ class EncoderRunner:
             rounds = -(-tiles // slots)
             sk = (os.environ.get("CAPMI_BF16_SK", "0") == "1" and os.environ.get("CAPMI_SK_OFF", "0") != "1"
                   and Kd // 64 >= 4 and tiles / (rounds * slots) < 0.9)  # (gemm.hip gemm_bf16_io)
-            key = (f"gemm_bf16_kernel<128, {bn_}, {mode}, {'true' if sk else 'false'}, "
-                   f"{'true' if in_ss is not None else 'false'}>")
+            key = f"gemm_bf16_kernel<128, {bn_}, {mode}, {'true' if sk else 'false'}>"
             self.conv_hook(tag, 2.0 * rows * co * Kd, launch, key)
         else:
             launch()
         return Ho, Wo, rows
 
-    def _bn_relu_bf16(self, ws, bn, rows, train, y, fold=False):
-        """relu(bn(y)) in place on a bf16 conv output (the next conv's input), the BN finalize fused in
-        where it fits. fold: return (scale, shift) for the consumer GEMM's prologue instead (round 3)."""
-        if fold:
-            return self._bn(ws, bn, rows, train)
-        d = self._bn_defer(ws, bn, rows, train)
-        if isinstance(d, _DeferredBN):
-            d.apply(CAPMI_BNFA_RELU_BF16, y, y)
-        else:
-            K.bn_relu_bf16(y, d[0], d[1], rows, bn.num_features, y)
+    def _bn_relu_bf16(self, ws, bn, rows, train, y):
+        """relu(bn(y)) in place on a bf16 conv output (the next conv's input)."""
+        s, b = self._bn(ws, bn, rows, train)
+        K.bn_relu_bf16(y, s, b, rows, bn.num_features, y)
 
     def _forward_bf16(self, net, imgs, out_hw, train, out):
         """The conv stack on bf16 NHWC activations: every conv but conv1 on CAPMI_GEMM_BF16_IO (bf16
@@ -524,10 +441,10 @@ class EncoderRunner:
             for bi, blk in enumerate(getattr(net, f"layer{li}")):
                 tag = f"layer{li}.{bi}"
                 _, _, r1 = self._conv_bf16(tag + ".conv1", x, blk.conv1, bf["y1"], N, H, W, train)
-                ss1 = self._bn_relu_bf16(ws, blk.bn1, r1, train, bf["y1"], fold=_BF16_FOLD & 1)
-                H2, W2, r2 = self._conv_bf16(tag + ".conv2", bf["y1"], blk.conv2, bf["y2"], N, H, W, train, in_ss=ss1)
-                ss2 = self._bn_relu_bf16(ws, blk.bn2, r2, train, bf["y2"], fold=_BF16_FOLD & 2)
-                _, _, r3 = self._conv_bf16(tag + ".conv3", bf["y2"], blk.conv3, bf["y3"], N, H2, W2, train, in_ss=ss2)
+                self._bn_relu_bf16(ws, blk.bn1, r1, train, bf["y1"])
+                H2, W2, r2 = self._conv_bf16(tag + ".conv2", bf["y1"], blk.conv2, bf["y2"], N, H, W, train)
+                self._bn_relu_bf16(ws, blk.bn2, r2, train, bf["y2"])
+                _, _, r3 = self._conv_bf16(tag + ".conv3", bf["y2"], blk.conv3, bf["y3"], N, H2, W2, train)
                 Cout = blk.conv3.out_channels
                 if blk.downsample is not None:
                     s3, b3 = self._bn(ws, blk.bn3, r3, train)  # (the downsample conv reuses the stats buffer)
@@ -536,11 +453,8 @@ class EncoderRunner:
                     K.bn_add_relu_bf16(bf["y3"], s3, b3, bf["yd"], xo, r3, Cout, res_scale=sd, res_shift=bd)
                     bns.append(blk.downsample[1])
                 else:
-                    d3 = self._bn_defer(ws, blk.bn3, r3, train)
-                    if isinstance(d3, _DeferredBN):
-                        d3.apply(CAPMI_BNFA_ADD_RELU_BF16, bf["y3"], xo, res=x)
-                    else:
-                        K.bn_add_relu_bf16(bf["y3"], d3[0], d3[1], x, xo, r3, Cout)
+                    s3, b3 = self._bn(ws, blk.bn3, r3, train)
+                    K.bn_add_relu_bf16(bf["y3"], s3, b3, x, xo, r3, Cout)
                 bns += [blk.bn1, blk.bn2, blk.bn3]
                 x, xo = xo, x
                 H, W, Cx = H2, W2, Cout
@@ -578,41 +492,27 @@ class EncoderRunner:
         bns = []
         direct = out_hw is None and out is not None
         n4 = len(net.layer4)
-        tail = None  # the previous block's deferred tail (its output x not yet written)
         for li in range(1, 5):
             layer = getattr(net, f"layer{li}")
             for bi, blk in enumerate(layer):
                 if direct and li == 4 and bi == n4 - 1:
                     xo = out  # the last block's output is the result
                 tag = f"layer{li}.{bi}"
-                if tail is not None and blk.downsample is not None:
-                    tail.now()  # (never: only a block followed by one of its own layer defers)
-                    tail = None
-                _, _, r1 = self._conv(tag + ".conv1", x, blk.conv1, ws["y1"], N, H, W, train, tail=tail)
-                tail = None
-                # this block's tail may ride in the next block's conv1 (same layer: no downsample reads x)
-                defer = self.x3 and _X3_TAIL and bi + 1 < len(layer)
-                # (layer3/4: the finalize of bn1 / bn2 rides in the consumer's pass, _bn_defer)
-                ss1 = self._bn_defer(ws, blk.bn1, r1, train)
+                _, _, r1 = self._conv(tag + ".conv1", x, blk.conv1, ws["y1"], N, H, W, train)
+                ss1 = self._bn(ws, blk.bn1, r1, train)
                 H2, W2, r2 = self._conv(tag + ".conv2", ws["y1"], blk.conv2, ws["y2"], N, H, W, train, in_ss=ss1)
-                ss2 = self._bn_defer(ws, blk.bn2, r2, train)
+                ss2 = self._bn(ws, blk.bn2, r2, train)
                 _, _, r3 = self._conv(tag + ".conv3", ws["y2"], blk.conv3, ws["y3"], N, H2, W2, train, in_ss=ss2)
                 Cout = blk.conv3.out_channels
                 if blk.downsample is not None:
                     s3, b3 = self._bn(ws, blk.bn3, r3, train)  # (the downsample conv reuses the stats buffer)
                     self._conv(tag + ".downsample", x, blk.downsample[0], ws["yd"], N, H, W, train)
                     sd, bd = self._bn(ws, blk.downsample[1], r3, train)
-                    tail = _Tail(ws["y3"], s3, b3, ws["yd"], xo, r3, Cout, rs=sd, rb=bd)
+                    K.bn_add_relu(ws["y3"], s3, b3, ws["yd"], xo, r3, Cout, res_scale=sd, res_shift=bd)
                     bns.append(blk.downsample[1])
                 else:
-                    d3 = self._bn_defer(ws, blk.bn3, r3, train)
-                    if isinstance(d3, _DeferredBN):
-                        d3.apply(CAPMI_BNFA_ADD_RELU, ws["y3"], xo, res=x)
-                    else:
-                        tail = _Tail(ws["y3"], d3[0], d3[1], x, xo, r3, Cout)
-                if tail is not None and not defer:
-                    tail.now()
-                    tail = None
+                    s3, b3 = self._bn(ws, blk.bn3, r3, train)
+                    K.bn_add_relu(ws["y3"], s3, b3, x, xo, r3, Cout)
                 bns += [blk.bn1, blk.bn2, blk.bn3]
                 x, xo = xo, x
                 H, W, Cx = H2, W2, Cout
@@ -685,6 +585,9 @@ _FT_DGRAD1_KROWS = os.environ.get("CAPMI_FT_DGRAD1_KROWS", "0") != "0"
 _FT_DGRAD1_X3D = os.environ.get("CAPMI_FT_DGRAD1_X3D", "1") != "0"
 # of those, the long-k ones (K >= 4 N: conv3's) on gemm_x3 instead of x3d (CAPMI_FT_DGRAD1_X3=0: all x3d)
 _FT_DGRAD1_X3 = os.environ.get("CAPMI_FT_DGRAD1_X3", "1") != "0"
+# x3 mode: the weight gradients on the x3w kernel (round 4: both fp32 operands split in-kernel, transposed
+# LDS reads, k-split slabs; CAPMI_FT_WGRAD_X3W=0: the split-staging nts kernel)
+_FT_WGRAD_X3W = os.environ.get("CAPMI_FT_WGRAD_X3W", "1") != "0"
 
 
 class FineTuneRunner:
@@ -851,6 +754,13 @@ class FineTuneRunner:
             return grads.get(id(p))
 
         def run(tag, flops, prob, amode, bmode, tile=K.TILE_AUTO):
+            if amode == AMM and self.r.x3 and _FT_WGRAD_X3W and K.gemm_x3w_ok(prob, bmode):
+                launch = lambda: K.gemm_x3w(prob, bmode, self.r._ws["sk"])  # noqa: E731
+                if hook is None:
+                    launch()
+                else:
+                    hook(tag, flops, launch, K.gemm_x3w_kernel_name(prob, bmode))
+                return
             if hook is None:
                 self._gemm(prob, amode, bmode, tile)
             else:

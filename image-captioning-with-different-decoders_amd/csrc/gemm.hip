@@ -398,9 +398,6 @@ int gemm_plan(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, 
   CAPMI_REQUIRE(bmode != 2 || amode == 1, CAPMI_EINVAL);
   CAPMI_REQUIRE(tile >= CAPMI_TILE_128 && tile <= CAPMI_TILE_128_W8, CAPMI_EINVAL);
   CAPMI_REQUIRE(amode != 4 || bmode == 0, CAPMI_EINVAL);
-  for (int i = 0; i < nprob; ++i)  // the fused bottleneck tail is a CAPMI_GEMM_X3 form only (ABI 18)
-    CAPMI_REQUIRE(!probs[i].in_res && !probs[i].in_out && !probs[i].in_res_scale && !probs[i].in_res_shift,
-                  CAPMI_EINVAL);
   GemmArgs& a = g.a;
   memset(&a, 0, sizeof(a));
   a.nprob = nprob;
@@ -689,9 +686,12 @@ bool terms_mode_ok(int terms, int amode, int bmode) {
 int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, GemmArgs& a, int& bn, bool& sk,
             long long& total);
 int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total,
-             int& bk, int& bn);
-int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total);
+             int& bk);
+int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, GemmArgs& a, bool& sk, long long& total,
+             bool& wide);
 int x3s_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long& lda, int& tiles, int& grid);
+int x3w_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long ws_floats, GemmArgs& a, int& S,
+             long long& tiles);
 }  // namespace
 
 extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, int flags,
@@ -701,12 +701,12 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
   if (flags == CAPMI_GEMM_X3P) {
     GemmArgs a;
     long long total = 0;
-    int bk = 32, xbn = 128;
-    const int rc = x3p_plan(prob, amode, bmode, a, sk, total, bk, xbn);
+    int bk = 32;
+    const int rc = x3p_plan(prob, amode, bmode, a, sk, total, bk);
     if (rc) return rc;
     if (threads) *threads = 512;
     if (bm) *bm = 256;
-    if (bn) *bn = xbn;
+    if (bn) *bn = 128;
     if (stream_k) *stream_k = sk ? 1 : 0;
     if (generic) *generic = bk;  // CAPMI_GEMM_X3P: the k-tile depth
     return 0;
@@ -714,13 +714,28 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
   if (flags == CAPMI_GEMM_X3D) {
     GemmArgs a;
     long long total = 0;
-    const int rc = x3d_plan(prob, amode, bmode, a, sk, total);
+    bool wide = false;
+    const int rc = x3d_plan(prob, amode, bmode, tile, a, sk, total, wide);
+    if (rc) return rc;
+    if (threads) *threads = 512;
+    if (bm) *bm = wide ? 128 : 256;
+    if (bn) *bn = wide ? 256 : 128;
+    if (stream_k) *stream_k = sk ? 1 : 0;
+    if (generic) *generic = 32;
+    return 0;
+  }
+  if (flags == CAPMI_GEMM_X3W) {
+    GemmArgs a;
+    int S = 1;
+    long long tiles = 0;
+    const long long ws = (capmi_gemm_workspace_bytes() - capmi_gemm_workspace_flag_bytes()) / 4;
+    const int rc = x3w_plan(prob, amode, bmode, ws, a, S, tiles);
     if (rc) return rc;
     if (threads) *threads = 512;
     if (bm) *bm = 256;
     if (bn) *bn = 128;
-    if (stream_k) *stream_k = sk ? 1 : 0;
-    if (generic) *generic = 32;
+    if (stream_k) *stream_k = S > 1 ? 1 : 0;
+    if (generic) *generic = S;  // CAPMI_GEMM_X3W: the k-splits
     return 0;
   }
   if (flags == CAPMI_GEMM_X3S) {
@@ -775,10 +790,8 @@ int gemm_bf16_io(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
   CAPMI_REQUIRE(p.ksplit == 1 && !p.bias && !p.bias2 && !p.alpha_ptr && p.alpha == 1.f && p.beta == 0.f &&
                     !p.relu && p.a_r1 <= 0 && p.c_r1 <= 0,
                 CAPMI_EINVAL);
-  // the BN-apply + ReLU prologue (round 3): dense rows with lda == K (the channel is k) or a conv
-  CAPMI_REQUIRE((p.in_scale == nullptr) == (p.in_shift == nullptr), CAPMI_EINVAL);
-  CAPMI_REQUIRE(p.in_scale == nullptr || amode == CAPMI_A_CONV_NHWC || p.lda == p.K, CAPMI_EINVAL);
-  CAPMI_REQUIRE(p.in_scale == nullptr || (aligned16(p.in_scale) && aligned16(p.in_shift)), CAPMI_EALIGN);
+  // no prologue: the bf16 conv input is materialised once per tensor (capmi_bn_relu_bf16)
+  CAPMI_REQUIRE(p.in_scale == nullptr && p.in_shift == nullptr, CAPMI_EINVAL);
   CAPMI_REQUIRE(aligned16(p.A) && aligned16(p.B) && p.ldb % 8 == 0 && p.ldb >= p.K && p.ldc >= p.N, CAPMI_EALIGN);
   CAPMI_REQUIRE((long long)p.N * p.ldb * 2 < (1LL << 31), CAPMI_ERANGE);
   if (amode == CAPMI_A_CONV_NHWC) {
@@ -845,19 +858,12 @@ int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gemm
   const capmi_gemm_problem& p = *prob;
   CAPMI_REQUIRE(bmode == CAPMI_B_NMAJOR_W && (amode == CAPMI_A_KMAJOR || amode == CAPMI_A_CONV_NHWC), CAPMI_EINVAL);
   CAPMI_REQUIRE(p.A && p.B && p.C && p.M >= 0 && p.N > 0 && p.K > 0 && p.K % 32 == 0 && p.ksplit == 1, CAPMI_EINVAL);
-  // dense A takes a prologue only as the fused bottleneck tail (in_res + in_out, ABI 18)
-  const bool tail = p.in_res != nullptr;
-  CAPMI_REQUIRE(amode == CAPMI_A_CONV_NHWC || tail || (!p.in_scale && !p.in_shift), CAPMI_EINVAL);
-  CAPMI_REQUIRE(!tail || (amode == CAPMI_A_KMAJOR && p.in_scale && p.in_out && p.lda == p.K), CAPMI_EINVAL);
-  CAPMI_REQUIRE(tail || (!p.in_out && !p.in_res_scale && !p.in_res_shift), CAPMI_EINVAL);
-  CAPMI_REQUIRE((p.in_res_scale == nullptr) == (p.in_res_shift == nullptr), CAPMI_EINVAL);
+  // the prologue is the conv input's BN-apply + ReLU: dense A takes none
+  CAPMI_REQUIRE(amode == CAPMI_A_CONV_NHWC || (!p.in_scale && !p.in_shift), CAPMI_EINVAL);
   CAPMI_REQUIRE((p.in_scale == nullptr) == (p.in_shift == nullptr), CAPMI_EINVAL);
   CAPMI_REQUIRE(p.stats == nullptr || p.c_r1 <= 0, CAPMI_EINVAL);
   CAPMI_REQUIRE(aligned16(p.A) && aligned16(p.B) && p.ldb % 8 == 0 && p.ldb >= p.K, CAPMI_EALIGN);
   CAPMI_REQUIRE(p.in_scale == nullptr || (aligned16(p.in_scale) && aligned16(p.in_shift)), CAPMI_EALIGN);
-  CAPMI_REQUIRE(!tail || (aligned16(p.in_res) && aligned16(p.in_out) &&
-                          (p.in_res_scale == nullptr || (aligned16(p.in_res_scale) && aligned16(p.in_res_shift)))),
-                CAPMI_EALIGN);
   CAPMI_REQUIRE(3LL * p.N * p.ldb * 2 < (1LL << 31), CAPMI_ERANGE);
   if (amode == CAPMI_A_CONV_NHWC) {
     CAPMI_REQUIRE(p.cCin % 32 == 0 && p.K == p.cKH * p.cKW * p.cCin && p.M == p.cN * p.cHo * p.cWo, CAPMI_EINVAL);
@@ -877,19 +883,6 @@ int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gemm
   a.tiles_begin[1] = (int)total;
   const long long slots = sk_cus();
   const int nkt = p.K / 32;
-  // A/B switch CAPMI_X3_SPLITN=1: a data-parallel grid under one round of 128-wide tiles takes 64-wide ones
-  static const bool splitn = [] {
-    const char* e = getenv("CAPMI_X3_SPLITN");
-    return e && atoi(e) == 1;
-  }();
-  if (splitn && tile == CAPMI_TILE_AUTO && bn == 128 && sk_family_off(1) && total < slots && total * 4 >= slots &&
-      p.N % 64 == 0) {
-    bn = 64;
-    a.tiles_n[0] = (int)cdiv(p.N, bn);
-    a.plain_epi = plain_epilogue(p, bn);
-    total = (long long)a.tiles_m[0] * a.tiles_n[0];
-    a.tiles_begin[1] = (int)total;
-  }
   const long long rounds = (total + slots - 1) / slots;
   // (round 3) more than two rounds of tiles: data-parallel -- the hardware's dynamic dispatch beat the hybrid
   // schedule there (layer1 c1: 55 vs 69 us, layer1 3x3: 154 vs 156; CAPMI_SK_OFF A/B on one box)
@@ -915,7 +908,7 @@ bool x3p_force32() {
 // round; otherwise BK = 32, one workgroup per CU, stream-K when the tile count leaves the chip
 // under-filled (l3 c3, 392 tiles: 49 us stream-K vs 102 us as one 2-per-CU round).
 int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total,
-             int& bk, int& bn) {
+             int& bk) {
   CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
   const capmi_gemm_problem& p = *prob;
   CAPMI_REQUIRE(bmode == CAPMI_B_NMAJOR_W && (amode == CAPMI_A_KMAJOR || amode == CAPMI_A_CONV_NHWC), CAPMI_EINVAL);
@@ -934,9 +927,8 @@ int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
   memset(&a, 0, sizeof(a));
   a.nprob = 1;
   a.p[0] = p;
-  bn = p.N <= 64 ? 64 : 128;  // 256 x 64 tiles for the N = 64 convs (layer1's 3x3)
   a.tiles_m[0] = (int)cdiv(p.M, 256);
-  a.tiles_n[0] = (int)cdiv(p.N, bn);
+  a.tiles_n[0] = (int)cdiv(p.N, 128);
   {  // A/B knob: CAPMI_X3P_ORDER=col walks tiles column-major (an XCD's contiguous range shares B)
     static const int col = [] {
       const char* e = getenv("CAPMI_X3P_ORDER");
@@ -944,13 +936,12 @@ int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
     }();
     a.tile_cols_first = col;
   }
-  a.plain_epi = plain_epilogue(p, bn);
+  a.plain_epi = plain_epilogue(p, 128);
   total = (long long)a.tiles_m[0] * a.tiles_n[0];
   a.tiles_begin[1] = (int)total;
   const long long slots2 = 2LL * sk_cus();
   const long long rounds2 = (total + slots2 - 1) / slots2;
-  // (256 x 64 tiles keep one workgroup per CU: layer1's 3x3 took 255 us at two per CU, 133 us at one)
-  if (!x3p_force32() && bn == 128 && total >= slots2 && (double)total / (double)(rounds2 * slots2) >= 0.7) {
+  if (!x3p_force32() && total >= slots2 && (double)total / (double)(rounds2 * slots2) >= 0.7) {
     bk = 16;
     sk = false;
     return 0;
@@ -968,11 +959,11 @@ int gemm_x3p(const capmi_gemm_problem* prob, int amode, int bmode, void* workspa
   GemmArgs a;
   bool sk = false;
   long long total = 0;
-  int bk = 32, bn = 128;
-  const int rc = x3p_plan(prob, amode, bmode, a, sk, total, bk, bn);
+  int bk = 32;
+  const int rc = x3p_plan(prob, amode, bmode, a, sk, total, bk);
   if (rc) return rc;
   if (prob->M == 0) return 0;
-  if (!sk || workspace == nullptr) return gemm_x3p_launch(a, amode, bk, (int)total, s, bn);
+  if (!sk || workspace == nullptr) return gemm_x3p_launch(a, amode, bk, (int)total, s);
   CAPMI_REQUIRE(aligned16(workspace), CAPMI_EINVAL);
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
   const int cus = cu_count();
@@ -984,13 +975,14 @@ int gemm_x3p(const capmi_gemm_problem* prob, int amode, int bmode, void* workspa
   a.sk_groups = sk_xcd_groups() && a.sk_workers % 8 == 0 && total >= 64 ? 8 : 1;
   a.sk_flags = static_cast<int*>(workspace);
   a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
-  return gemm_x3p_launch(a, amode, bk, a.sk_workers, s, bn);
+  return gemm_x3p_launch(a, amode, bk, a.sk_workers, s);
 }
 
 // CAPMI_GEMM_X3D: fp32 A (+ BN prologue for convs) split in-kernel x three-plane B in the x3p k order
 // (gemm_x3p.hip, ASPLIT): 256x128 tiles, 512 threads, k-tiles of 32, one workgroup per CU, stream-K
 // when the tiles under-fill the chip
-int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total) {
+int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, GemmArgs& a, bool& sk, long long& total,
+             bool& wide) {
   CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
   const capmi_gemm_problem& p = *prob;
   CAPMI_REQUIRE(bmode == CAPMI_B_NMAJOR_W && (amode == CAPMI_A_KMAJOR || amode == CAPMI_A_CONV_NHWC), CAPMI_EINVAL);
@@ -1012,9 +1004,12 @@ int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
   memset(&a, 0, sizeof(a));
   a.nprob = 1;
   a.p[0] = p;
-  a.tiles_m[0] = (int)cdiv(p.M, 256);
-  a.tiles_n[0] = (int)cdiv(p.N, 128);
-  a.plain_epi = plain_epilogue(p, 128);
+  // CAPMI_TILE_128x256 (round 4): 128 x 256 tiles for dense rows, one column tile when N <= 256
+  wide = tile == CAPMI_TILE_128x256 && amode == CAPMI_A_KMAJOR;
+  const int bm = wide ? 128 : 256, bn = wide ? 256 : 128;
+  a.tiles_m[0] = (int)cdiv(p.M, bm);
+  a.tiles_n[0] = (int)cdiv(p.N, bn);
+  a.plain_epi = plain_epilogue(p, bn);
   total = (long long)a.tiles_m[0] * a.tiles_n[0];
   a.tiles_begin[1] = (int)total;
   const long long slots = sk_cus();
@@ -1024,15 +1019,16 @@ int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
   return 0;
 }
 
-int gemm_x3d(const capmi_gemm_problem* prob, int amode, int bmode, void* workspace, long long ws_bytes,
+int gemm_x3d(const capmi_gemm_problem* prob, int amode, int bmode, int tile, void* workspace, long long ws_bytes,
              hipStream_t s) {
   GemmArgs a;
   bool sk = false;
   long long total = 0;
-  const int rc = x3d_plan(prob, amode, bmode, a, sk, total);
+  bool wide = false;
+  const int rc = x3d_plan(prob, amode, bmode, tile, a, sk, total, wide);
   if (rc) return rc;
   if (prob->M == 0) return 0;
-  if (!sk || workspace == nullptr) return gemm_x3d_launch(a, amode, (int)total, s);
+  if (!sk || workspace == nullptr) return gemm_x3d_launch(a, amode, (int)total, s, wide);
   CAPMI_REQUIRE(aligned16(workspace), CAPMI_EINVAL);
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
   const int cus = cu_count();
@@ -1044,7 +1040,70 @@ int gemm_x3d(const capmi_gemm_problem* prob, int amode, int bmode, void* workspa
   a.sk_groups = sk_xcd_groups() && a.sk_workers % 8 == 0 && total >= 64 ? 8 : 1;
   a.sk_flags = static_cast<int*>(workspace);
   a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
-  return gemm_x3d_launch(a, amode, a.sk_workers, s);
+  return gemm_x3d_launch(a, amode, a.sk_workers, s, wide);
+}
+
+// CAPMI_GEMM_X3W (gemm_x3w.hip): conv weight gradient dW = dY^T . im2col(X), both operands fp32 k rows (pixels),
+// split in-kernel; 256 x 128 tiles, one workgroup per CU, the k range split S ways so that tiles x S fills the
+// CUs once (S partial slabs in the workspace after the stream-K flags, summed by capmi_splitk_reduce's kernel)
+int x3w_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long ws_floats, GemmArgs& a, int& S,
+             long long& tiles) {
+  CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
+  const capmi_gemm_problem& p = *prob;
+  CAPMI_REQUIRE(amode == CAPMI_A_MMAJOR && (bmode == CAPMI_B_KROWS || bmode == CAPMI_B_CONV_NHWC), CAPMI_EINVAL);
+  CAPMI_REQUIRE(p.A && p.B && p.C && p.M > 0 && p.N > 0 && p.K >= 0 && p.ksplit == 1, CAPMI_EINVAL);
+  CAPMI_REQUIRE(!p.bias && !p.bias2 && !p.relu && !p.stats && p.a_r1 <= 0 && p.c_r1 <= 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE((p.in_scale == nullptr) == (p.in_shift == nullptr), CAPMI_EINVAL);
+  CAPMI_REQUIRE(p.M % 4 == 0 && p.N % 4 == 0 && p.lda >= p.M && p.lda % 4 == 0 && p.ldc >= p.N, CAPMI_EALIGN);
+  CAPMI_REQUIRE(aligned16(p.A) && aligned16(p.B), CAPMI_EALIGN);
+  CAPMI_REQUIRE(p.in_scale == nullptr || (aligned16(p.in_scale) && aligned16(p.in_shift)), CAPMI_EALIGN);
+  CAPMI_REQUIRE((long long)p.K * p.lda * 4 < (1LL << 31), CAPMI_ERANGE);
+  if (bmode == CAPMI_B_CONV_NHWC) {
+    CAPMI_REQUIRE(p.cCin % 4 == 0 && p.N == p.cKH * p.cKW * p.cCin && p.K == p.cN * p.cHo * p.cWo, CAPMI_EINVAL);
+    CAPMI_REQUIRE((long long)p.cN * p.cH * p.cW * p.cCin * 4 < (1LL << 31), CAPMI_ERANGE);
+  } else {
+    CAPMI_REQUIRE(p.ldb % 4 == 0 && p.ldb >= p.N, CAPMI_EALIGN);
+    CAPMI_REQUIRE((long long)p.K * p.ldb * 4 < (1LL << 31), CAPMI_ERANGE);
+  }
+  memset(&a, 0, sizeof(a));
+  a.nprob = 1;
+  a.p[0] = p;
+  a.tiles_m[0] = (int)cdiv(p.M, 256);
+  a.tiles_n[0] = (int)cdiv(p.N, 128);
+  a.plain_epi = plain_epilogue(p, 128);
+  tiles = (long long)a.tiles_m[0] * a.tiles_n[0];
+  a.tiles_begin[1] = (int)tiles;
+  const long long nkt = std::max<long long>(1, (p.K + 31) / 32);
+  // k-splits: one round of workgroups over the CUs, at least 4 k-tiles each, slabs within the workspace;
+  // a k-split sums in fp32 partials, so the host requires alpha 1 / beta 0 for it (the weight gradients)
+  const long long slab = (long long)p.M * a.tiles_n[0] * 128;
+  long long s = std::max<long long>(1, std::min<long long>(sk_cus() / tiles, nkt / 4));
+  s = std::min<long long>(s, ws_floats / slab);
+  if (!(p.alpha == 1.f && p.beta == 0.f && p.alpha_ptr == nullptr)) s = 1;
+  s = std::max<long long>(s, 1);
+  const long long kc = (nkt + s - 1) / s;
+  a.kchunk[0] = (int)kc;
+  S = (int)((nkt + kc - 1) / kc);
+  return 0;
+}
+
+int gemm_x3w(const capmi_gemm_problem* prob, int amode, int bmode, void* workspace, long long ws_bytes, hipStream_t s) {
+  const int cus = cu_count();
+  const long long part_floats =
+      workspace != nullptr && ws_bytes > sk_flag_bytes(cus) ? (ws_bytes - sk_flag_bytes(cus)) / 4 : 0;
+  GemmArgs a;
+  int S = 1;
+  long long tiles = 0;
+  const int rc = x3w_plan(prob, amode, bmode, part_floats, a, S, tiles);
+  if (rc) return rc;
+  if (prob->K == 0) return 0;  // (dW = 0 is the caller's: nothing to multiply)
+  CAPMI_REQUIRE(workspace == nullptr || aligned16(workspace), CAPMI_EINVAL);
+  if (S > 1) a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
+  int e = gemm_x3w_launch(a, bmode, (int)(tiles * S), s);
+  if (e || S == 1) return e;
+  const int ldp = a.tiles_n[0] * 128;
+  return capmi_splitk_reduce(a.sk_part, S, (long long)prob->M * ldp, prob->M, prob->N, ldp, nullptr, prob->C,
+                             prob->ldc, s);
 }
 
 // CAPMI_GEMM_X3S (gemm_x3s.hip): K = 64, N in {64, 128, 256}, dense rows or a 1x1 / stride-1 conv input
@@ -1116,14 +1175,12 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
                                 void* workspace, long long ws_bytes, void* stream) {
   GemmPlan g;
   bool sk = false;
-  CAPMI_REQUIRE(prob == nullptr || flags == CAPMI_GEMM_X3 ||
-                    (!prob->in_res && !prob->in_out && !prob->in_res_scale && !prob->in_res_shift),
-                CAPMI_EINVAL);  // the fused bottleneck tail: CAPMI_GEMM_X3 only
   if (flags == CAPMI_GEMM_BF16_IO) return gemm_bf16_io(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3) return gemm_x3(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3P) return gemm_x3p(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
-  if (flags == CAPMI_GEMM_X3D) return gemm_x3d(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
+  if (flags == CAPMI_GEMM_X3D) return gemm_x3d(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3S) return gemm_x3s(prob, amode, bmode, as_stream(stream));
+  if (flags == CAPMI_GEMM_X3W) return gemm_x3w(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
   int terms = flag_terms(flags);
   CAPMI_REQUIRE(terms >= 0, CAPMI_EINVAL);
   CAPMI_REQUIRE(terms_mode_ok(terms, amode, bmode), CAPMI_EINVAL);

@@ -26,6 +26,53 @@ struct GemmArgs {
   int plain_epi;
 };
 
+// Exact three-term bf16 split of two fp32 values (the x3 arithmetic: h0 = RNE(e), h1 = RNE(e - h0),
+// h2 = RNE(e - h0 - h1), every difference exact in fp32), packed: w[p] = (h_p(e1) << 16) | h_p(e0), one
+// v_cvt_pk_bf16_f32 per term and pair (round 4: the scalar form converted one value per instruction and
+// packed the pairs with v_or_b32_sdwa -- 12 VALU per element in x3d's A staging, 4.5 now)
+typedef float capmi_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 capmi_bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split3_pair(float e0, float e1, unsigned (&w)[3]) {
+  const capmi_f32x2 e = {e0, e1};
+  w[0] = __builtin_bit_cast(unsigned, __builtin_convertvector(e, capmi_bf16x2));
+  const capmi_f32x2 r1 = e - capmi_f32x2{__uint_as_float(w[0] << 16), __uint_as_float(w[0] & 0xffff0000u)};
+  w[1] = __builtin_bit_cast(unsigned, __builtin_convertvector(r1, capmi_bf16x2));
+  const capmi_f32x2 r2 = r1 - capmi_f32x2{__uint_as_float(w[1] << 16), __uint_as_float(w[1] & 0xffff0000u)};
+  w[2] = __builtin_bit_cast(unsigned, __builtin_convertvector(r2, capmi_bf16x2));
+}
+
+// Stream-K hand-off of a parked k-prefix partial (round 4: ordered by the HIP memory model, not by
+// cache-policy bits; cdna_hip_programming.md §6 Guideline 16). The partial's stores keep the SC1
+// (write-through) policy as a performance hint only.
+// Producer, called by EVERY thread after its partial stores: each wave drains its stores, the
+// workgroup meets, then one lane releases at agent scope and raises the worker's flag.
+__device__ __forceinline__ void sk_publish(int* flag, int tid) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (ROCm 7.2 may drop the fence's own wait)
+    __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// Consumer, called by EVERY thread: one lane polls the producer's flag (relaxed, bounded: a timeout
+// raises err and leaves the flag), re-arms it, acquires at agent scope and waits for the invalidate;
+// the workgroup barrier then orders every wave's partial loads after the acquire.
+__device__ __forceinline__ void sk_consume(int* flag, int* err, int tid) {
+  if (tid == 0) {
+    int spins = 0;
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && ++spins < (1 << 22))
+      __builtin_amdgcn_s_sleep(2);
+    if (spins >= (1 << 22))  // never expected: raise the error word (capmi.kernels.sk_check)
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ long long remap(long long r, long long r1, long long ld, long long s2) {
   return r1 > 0 ? (r % r1) * ld + (r / r1) * s2 : r * ld;
 }
@@ -58,12 +105,16 @@ int gemm_x3_launch(const GemmArgs& a, int amode, int bn, int blocks, hipStream_t
 // x3 with both operands pre-split (gemm_x3p.hip): 256x128 tiles, 512 threads, amode 0 / 2; k-tile depth
 // bk (16: two workgroups per CU, data-parallel grids only; 32: one, stream-K capable) is the unit
 // of GemmArgs::sk_nkt for it
-int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_t s, int bn = 128);
+int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_t s);
 // x3p with A fp32 split in-kernel ("x3d": register-staged A + optional conv BN prologue, LDS-DMA B)
-int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s);
+// wide: 128 x 256 tiles (dense rows)
+int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s, bool wide = false);
 // short-k streaming x3 GEMM (gemm_x3s.hip): K = 64, N in {64, 128, 256}, dense rows of lda floats
 // (optional BN prologue), store-only epilogue; persistent grid over 64-row tiles
 int gemm_x3s_launch(const capmi_gemm_problem& p, long long lda, int tiles, int grid, hipStream_t s);
+// conv weight gradients (gemm_x3w.hip): A = dY fp32 k rows, B = fp32 k rows (bmode 1) or the NHWC conv input's
+// implicit im2col (bmode 2), both split in-kernel; grid = tiles x S k-splits (a.kchunk[0] k-tiles each)
+int gemm_x3w_launch(const GemmArgs& a, int bmode, int blocks, hipStream_t s);
 // resident workgroups per CU of the NT kernel for a tile shape (LDS / register bound)
 // (terms 3: three bf16 LDS planes per operand, 60 KB for 64x64 and >= 90 KB for the larger tiles)
 inline int gemm_nt_wg_per_cu(int bm, int bn, int terms = 0) {

@@ -43,10 +43,7 @@ __device__ __forceinline__ unsigned pack_bf(float lo, float hi) {
   return (unsigned)bf16_bits(lo) | ((unsigned)bf16_bits(hi) << 16);
 }
 
-// PRO (round 3): the conv input's BN-apply + ReLU in the A staging, relu(fma(a, scale[c], shift[c])) rounded
-// to bf16 (RNE) -- capmi_bn_relu_bf16's arithmetic bit for bit, padding taps zero after it -- instead of a
-// separate materialising pass over the tensor
-template <int BM, int BN, int AMODE, bool SK, bool PRO = false>
+template <int BM, int BN, int AMODE, bool SK>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 gemm_bf16_kernel(const GemmArgs args) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
@@ -114,38 +111,21 @@ gemm_bf16_kernel(const GemmArgs args) {
 
     struct Stage {
       u32x4_t ra[NA], rb[NB];
-      unsigned am;         // PRO: slot i loaded in bounds (else zero after the BN apply)
-      float4 sc[2], sh[2];  // PRO: scale / shift of the slot's 8 channels
-    };
-    const auto rsc = rsrc_of(PRO ? (const void*)P.in_scale : P.A, PRO ? (unsigned)(AMODE == 2 ? cCin : P.K) * 4u : 0u);
-    const auto rsh = rsrc_of(PRO ? (const void*)P.in_shift : P.A, PRO ? (unsigned)(AMODE == 2 ? cCin : P.K) * 4u : 0u);
-    auto load_ss = [&](Stage& st, int c, bool kok) {  // channels c .. c + 7 (past K: zeros, never used)
-      const unsigned o = kok ? (unsigned)c * 4u : kOOB;
-      st.sc[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsc, o, 0, 0));
-      st.sc[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsc, o + 16u, 0, 0));
-      st.sh[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsh, o, 0, 0));
-      st.sh[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsh, o + 16u, 0, 0));
     };
     auto load_tile = [&](Stage& st, int kt) {
       const int k = k_lo + kt * BKH;
       const bool kok = k < k_hi;
-      st.am = 0;
       if (AMODE == 0) {
 #pragma unroll
-        for (int i = 0; i < NA; ++i) {
+        for (int i = 0; i < NA; ++i)
           st.ra[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, kok ? a_off[i] + (unsigned)k * 2 : kOOB, 0, 0);
-          st.am |= (unsigned)(kok && a_ok[i]) << i;
-        }
-        if (PRO) load_ss(st, k + kc, kok);
       } else {
-        if (PRO) load_ss(st, c_ci + kc, kok);
 #pragma unroll
         for (int i = 0; i < NA; ++i) {
           const int ih = a_ih0[i] + c_kh, iw = a_iw0[i] + c_kw;
           const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
           const unsigned off = ((a_off[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + kc)) * 2u;
           st.ra[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off : kOOB, 0, 0);
-          st.am |= (unsigned)ok << i;
         }
         c_ci += BKH;
         if (c_ci >= cCin) {
@@ -162,22 +142,7 @@ gemm_bf16_kernel(const GemmArgs args) {
     };
     auto store_tile = [&](const Stage& st, int buf) {
 #pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        u32x4_t v = st.ra[i];
-        if (PRO) {
-          const float s8[8] = {st.sc[0].x, st.sc[0].y, st.sc[0].z, st.sc[0].w, st.sc[1].x, st.sc[1].y, st.sc[1].z, st.sc[1].w};
-          const float b8[8] = {st.sh[0].x, st.sh[0].y, st.sh[0].z, st.sh[0].w, st.sh[1].x, st.sh[1].y, st.sh[1].z, st.sh[1].w};
-          const unsigned in[4] = {v.x, v.y, v.z, v.w};
-          unsigned o[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            o[q] = pack_bf(fmaxf(fmaf(lo_bf(in[q]), s8[2 * q], b8[2 * q]), 0.f),
-                           fmaxf(fmaf(hi_bf(in[q]), s8[2 * q + 1], b8[2 * q + 1]), 0.f));
-          const bool ok = (st.am >> i) & 1u;  // padding taps / rows past M: zeros after the BN apply
-          v = u32x4_t{ok ? o[0] : 0u, ok ? o[1] : 0u, ok ? o[2] : 0u, ok ? o[3] : 0u};
-        }
-        *reinterpret_cast<u32x4_t*>(&As[buf][((tid + i * 256) >> 3) * SBH + kc]) = v;
-      }
+      for (int i = 0; i < NA; ++i) *reinterpret_cast<u32x4_t*>(&As[buf][((tid + i * 256) >> 3) * SBH + kc]) = st.ra[i];
 #pragma unroll
       for (int i = 0; i < NB; ++i)
         *reinterpret_cast<u32x4_t*>(&Bs[buf][((tid + i * 256) >> 3) * SBH + kc]) = st.rb[i];
@@ -335,29 +300,13 @@ gemm_bf16_kernel(const GemmArgs args) {
             v.w = __float_as_uint(acc[i][j][4 * q + 3]);
             __builtin_amdgcn_raw_buffer_store_b128(v, rs, (((i * TN + j) * 4 + q) * 256 + tid) * 16, 0, kSc1h);
           }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) __hip_atomic_store(flags + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sk_publish(flags + blockIdx.x, tid);
       continue;
     }
     if (ks > 0) {
       for (long long w2 = w - 1;; --w2) {
         const long long b2 = w2 * ngrp + grp;
-        if (tid == 0) {
-          int spins = 0;
-          while (__hip_atomic_load(flags + b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-                 ++spins < (1 << 22))
-            __builtin_amdgcn_s_sleep(2);
-          // never expected: report instead of hanging. The flag of b2 is left as it is and the
-          // error word raised, so the host's check (capmi.kernels.sk_check: every flag word must
-          // be zero between launches) raises and re-zeroes the workspace instead of carrying on
-          if (spins >= (1 << 22))
-            __hip_atomic_store(flags + gridDim.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else
-            __hip_atomic_store(flags + b2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        sk_consume(flags + b2, flags + gridDim.x, tid);
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + b2 * PART, 0, PART * 4, 0x00020000);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -382,20 +331,6 @@ template <int BM, int BN>
 void launch_bf16(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
   const dim3 g(blocks), b(256);
   const bool sk = a.sk_workers > 0;
-  if (a.p[0].in_scale != nullptr) {  // the BN-apply + ReLU prologue (round 3)
-    if (amode == 2) {
-      if (sk)
-        CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 2, true, true>), g, b, 0, s, a);
-      else
-        CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 2, false, true>), g, b, 0, s, a);
-    } else {
-      if (sk)
-        CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 0, true, true>), g, b, 0, s, a);
-      else
-        CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 0, false, true>), g, b, 0, s, a);
-    }
-    return;
-  }
   if (amode == 2) {
     if (sk)
       CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 2, true>), g, b, 0, s, a);

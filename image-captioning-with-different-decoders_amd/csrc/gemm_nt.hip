@@ -748,30 +748,15 @@ __device__ __forceinline__ void gemm_nt_body(const GemmArgs& args) {
             v.w = __float_as_uint(acc[i][j][4 * q + 3]);
             __builtin_amdgcn_raw_buffer_store_b128(v, rs, (((i * TN + j) * 4 + q) * NT + tid) * 16, 0, kSc1);
           }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) __hip_atomic_store(flags + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sk_publish(flags + blockIdx.x, tid);
       continue;
     }
     if (ks > 0) {  // add the parked k-prefixes, nearest contributor first
       for (long long w2 = w - 1;; --w2) {
         const long long b2 = w2 * ngrp + grp;  // blockIdx of the contributor
-        if (tid == 0) {
-          int spins = 0;
-          while (__hip_atomic_load(flags + b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-                 ++spins < (1 << 22))
-            __builtin_amdgcn_s_sleep(2);
-          // never expected: report instead of hanging. The flag of b2 is left as it is and the
-          // error word raised, so the host's check (capmi.kernels.sk_check: every flag word must
-          // be zero between launches) raises and re-zeroes the workspace instead of carrying on
-          if (spins >= (1 << 22))
-            __hip_atomic_store(flags + gridDim.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else
-            __hip_atomic_store(flags + b2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the poll
-        // every load of the parked bytes is an sc1 (L1-bypassing) load: no agent acquire needed
+        // (a timeout leaves b2's flag and raises the error word: capmi.kernels.sk_check, the host's
+        // check that every flag word is zero between launches, raises and re-zeroes the workspace)
+        sk_consume(flags + b2, flags + gridDim.x, tid);
         const auto rs = slot_rsrc(args.sk_part, b2 * PART);
 #pragma unroll
         for (int i = 0; i < TM; ++i)

@@ -116,13 +116,6 @@ gemm_x3_kernel(const GemmArgs args) {
     const auto rb = rsrc_x(P.B, (unsigned)(3 * plane * 2));
     const float* __restrict__ isc = P.in_scale;
     const float* __restrict__ ish = P.in_shift;
-    // fused bottleneck tail (PRO with AMODE 0; capmi.h ABI 18): residual rows, optional residual BN, and
-    // the block output written by the first column tile's workgroups (each element exactly once)
-    const auto rres = rsrc_x(PRO && AMODE == 0 ? (const void*)P.in_res : P.A, a_bytes);
-    const auto ro = rsrc_x(PRO && AMODE == 0 ? (const void*)P.in_out : P.A, a_bytes);
-    const float* __restrict__ rsc = P.in_res_scale;
-    const float* __restrict__ rsh = P.in_res_shift;
-    const bool tail_out = PRO && AMODE == 0 && n0 == 0;
     unsigned a_off[NA];
     int a_ih0[NA], a_iw0[NA];
     bool a_ok[NA];
@@ -168,10 +161,6 @@ gemm_x3_kernel(const GemmArgs args) {
       u32x4_x b[NBr];
       float4 sc, sh;
       unsigned am;
-      // fused tail (PRO with AMODE 0): residual rows, their optional BN, the k byte offset
-      float4 r[AMODE == 0 && PRO ? NA : 1];
-      float4 rs, rb;
-      unsigned ko;
     };
     auto load_tile = [&](Stage& st, int kt) {
       const int k = k_lo + kt * XBK;
@@ -184,20 +173,6 @@ gemm_x3_kernel(const GemmArgs args) {
           st.a[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
                                                    ra, ok ? a_off[i] + (unsigned)k * 4 : kOOBx, 0, 0));
           st.am |= (unsigned)ok << i;
-          if (PRO)  // fused tail: the residual row of the same element
-            st.r[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     rres, ok ? a_off[i] + (unsigned)k * 4 : kOOBx, 0, 0));
-        }
-        if (PRO) {
-          st.ko = (unsigned)k * 4;
-          if (kok) {
-            st.sc = *reinterpret_cast<const float4*>(isc + k + kq);
-            st.sh = *reinterpret_cast<const float4*>(ish + k + kq);
-            if (rsc != nullptr) {
-              st.rs = *reinterpret_cast<const float4*>(rsc + k + kq);
-              st.rb = *reinterpret_cast<const float4*>(rsh + k + kq);
-            }
-          }
         }
       } else {
         const int ci = c_ci + kq;
@@ -234,14 +209,6 @@ gemm_x3_kernel(const GemmArgs args) {
         if (PRO && AMODE == 2) {
           v = relu4(fma4(v, st.sc, st.sh));
           if (!((st.am >> i) & 1u)) v = f4(0.f);  // padding taps are zeros AFTER the BN apply
-        }
-        if (PRO && AMODE == 0) {  // fused tail: capmi_bn_add_relu's formula, then the block output stored
-          const float4 r = rsc != nullptr ? fma4(st.r[i], st.rs, st.rb) : st.r[i];
-          v = relu4(fma4(v, st.sc, st.sh) + r);
-          if (!((st.am >> i) & 1u)) v = f4(0.f);  // rows past M / k past K
-          if (tail_out)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_x, v), ro,
-                                                   (st.am >> i) & 1u ? a_off[i] + st.ko : kOOBx, 0, 0);
         }
         const bf16x4_x h0 = cvt4(v);
 #if X3_VARIANT == 1  // A/B only: no split VALU (wrong results)
@@ -327,9 +294,6 @@ gemm_x3_kernel(const GemmArgs args) {
     Stage s0, s1;
     s0.sc = s1.sc = f4(1.f);
     s0.sh = s1.sh = f4(0.f);
-    s0.rs = s1.rs = f4(1.f);
-    s0.rb = s1.rb = f4(0.f);
-    s0.ko = s1.ko = 0;
     load_tile(s0, 0);
     store_tile(s0, 0);
     load_tile(s1, 1);
@@ -543,27 +507,13 @@ gemm_x3_kernel(const GemmArgs args) {
           __builtin_amdgcn_raw_buffer_store_b128(v, rs, ((j * 4 + q) * XNT + tid) * 16, 0, kSc1x);
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) __hip_atomic_store(flags + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sk_publish(flags + blockIdx.x, tid);
       continue;
     }
     if (ks > 0) {
       for (long long w2 = w - 1;; --w2) {
         const long long b2 = w2 * ngrp + grp;
-        if (tid == 0) {
-          int spins = 0;
-          while (__hip_atomic_load(flags + b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-                 ++spins < (1 << 22))
-            __builtin_amdgcn_s_sleep(2);
-          // never expected: raise the error word and leave b2's flag (capmi.kernels.sk_check)
-          if (spins >= (1 << 22))
-            __hip_atomic_store(flags + gridDim.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else
-            __hip_atomic_store(flags + b2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        sk_consume(flags + b2, flags + gridDim.x, tid);
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + b2 * PART, 0, PART * 4, 0x00020000);
         if constexpr (X3_M16) {
 #pragma unroll
@@ -599,9 +549,7 @@ void launch_x3(const GemmArgs& a, int amode, bool pro, int blocks, hipStream_t s
       CAPMI_KLAUNCH((gemm_x3_kernel<BN, 2, true, SK>), g, b, 0, s, a);
     else
       CAPMI_KLAUNCH((gemm_x3_kernel<BN, 2, false, SK>), g, b, 0, s, a);
-  } else if (pro) {  // the fused bottleneck tail (in_res set)
-    CAPMI_KLAUNCH((gemm_x3_kernel<BN, 0, true, SK>), g, b, 0, s, a);
-  } else {
+  } else {  // dense A: no prologue (x3_plan)
     CAPMI_KLAUNCH((gemm_x3_kernel<BN, 0, false, SK>), g, b, 0, s, a);
   }
 }

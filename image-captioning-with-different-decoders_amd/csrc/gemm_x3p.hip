@@ -22,7 +22,7 @@
 
 namespace {
 
-constexpr int PBM = 256, PNT = 512;
+constexpr int PNT = 512;
 typedef unsigned u32x4_p __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_p __attribute__((ext_vector_type(8)));
 typedef float f32x4_p __attribute__((ext_vector_type(4)));
@@ -36,17 +36,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_p(const void* p, unsigned
 
 // BK = 32: 72 KiB per LDS buffer, one workgroup per CU; BK = 16: 36 KiB, two workgroups per CU (their
 // barriers and DMA waits fall at different times, so one's MFMAs cover the other's stalls)
-template <int PBK, int PBN = 128>
+// tile: 256 x 128 (M x N), or WIDE 128 x 256 (round 4: a 1x1 conv whose N fits one column tile stages each
+// A element once)
+template <int PBK, bool WIDE = false>
 struct X3pGeo {
+  static constexpr int BM = WIDE ? 128 : 256, BN = WIDE ? 256 : 128;
   static constexpr int PROWB = PBK * 2;             // bytes per LDS row
   static constexpr int CPR = PBK / 8;               // 16-B chunks per row
   static constexpr int RPB = 1024 / PROWB;          // rows per 1 KiB LDS-DMA block (16 or 32)
   static constexpr int SWZ = 16 / CPR;              // swizzle period: chunk s of row r holds s ^ ((r / SWZ) % CPR)
-  static constexpr int PA_BYTES = 3 * PBM * PROWB;  // A planes of one k-tile
-  static constexpr int PB_BYTES = 3 * PBN * PROWB;
+  static constexpr int PA_BYTES = 3 * BM * PROWB;  // A planes of one k-tile
+  static constexpr int PB_BYTES = 3 * BN * PROWB;
   static constexpr int PBUF = PA_BYTES + PB_BYTES;  // 72 / 36 KiB per buffer
-  static constexpr int NAB = PBM / RPB / 8;         // A row blocks per wave (2 / 1)
-  static constexpr int NBB = PBN / RPB;             // B row blocks (8 / 4): waves 0 .. NBB-1
+  static constexpr int NAB = BM / RPB / 8;          // A row blocks per wave (2 / 1)
+  static constexpr int NBB = BN / RPB;              // B row blocks (8 / 4 / 16): waves 0 .. NBB-1, or 2 per wave
   static constexpr int WPE = PBK == 16 ? 4 : 2;     // waves per SIMD: two workgroups per CU at BK = 16
 };
 
@@ -72,23 +75,24 @@ __device__ __forceinline__ int swz(int r) {
 // + ReLU prologue PRO), loaded to registers one k-tile ahead and split into the three swizzled LDS
 // planes after the k-tile's MFMAs; B stays LDS-DMA. It replaces gemm_x3 (both operands through
 // registers) and the separate split pass of x3p (BK = 32 only).
-// PBN (round 3): 128, or 64 for the N = 64 convs (layer1's 3x3): the wave tile is 64 x PBN/2
-template <int AMODE, bool SK, int PBK, bool ASPLIT = false, bool PRO = false, int PBN = 128>
+template <int AMODE, bool SK, int PBK, bool ASPLIT = false, bool PRO = false, bool WIDE = false>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(X3pGeo<PBK>::WPE)))
 gemm_x3p_kernel(const GemmArgs args) {
   static_assert(!ASPLIT || PBK == 32, "x3d: 32-deep k-tiles");
   static_assert(!PRO || ASPLIT, "prologue: x3d (conv, or dense rows whose k is the channel: 1x1 convs)");
-  static_assert(PBN == 128 || PBN == 64, "column tile");
-  using G_ = X3pGeo<PBK, PBN>;
-  constexpr int JN = PBN / 32;    // 16x16x32: 16-column blocks per wave
-  constexpr int JN32 = PBN / 64;  // 32x32x16: 32-column blocks per wave
-  constexpr int PROWB = G_::PROWB, CPR = G_::CPR, RPB = G_::RPB, SWZ = G_::SWZ;
+  static_assert(!WIDE || (ASPLIT && PBK == 32 && AMODE == 0), "wide tiles: x3d on dense rows");
+  using G_ = X3pGeo<PBK, WIDE>;
+  constexpr int PBM = G_::BM, PBN = G_::BN;
+  constexpr int JN = 64 / 16;    // 16x16x32: 16-column blocks per wave (wave tile 64 x 64)
+  constexpr int JN32 = 64 / 32;  // 32x32x16: 32-column blocks per wave
+  constexpr int PROWB = G_::PROWB, CPR = G_::CPR, RPB = G_::RPB;
   constexpr int PA_BYTES = G_::PA_BYTES, PBUF = G_::PBUF, NAB = G_::NAB, NBB = G_::NBB;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * PBUF];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases in SGPRs
-  const int wm0 = (wid >> 1) * 64, wn0 = (wid & 1) * (PBN / 2);
+  // waves as 4 x 2 (256 x 128) or 2 x 4 (WIDE 128 x 256), wave tile 64 x 64
+  const int wm0 = (WIDE ? wid >> 2 : wid >> 1) * 64, wn0 = (WIDE ? wid & 3 : wid & 1) * 64;
   const int lr = lane & 31, lh = lane >> 5;
   // DMA lane geometry: row lane / CPR of an RPB-row block, slot lane % CPR
   const int drow = lane / CPR, dslot = lane % CPR;
@@ -152,13 +156,20 @@ gemm_x3p_kernel(const GemmArgs args) {
         a_base[i] = (unsigned)(n * cH * cW);
       }
     }
-    const bool bw = wid < NBB;  // this wave stages B row block wid
-    const int br = (wid % NBB) * RPB + drow;
-    const int b_ch = dslot ^ swz<PBK>(br);
-    const bool b_ok = bw && n0 + br < N;
-    const unsigned b_base = (unsigned)(((long long)(b_ok ? n0 + br : 0) * P.ldb + b_ch * 8) * 2);
-    // x3d: four fp32 float4 slots per thread, slot i = row (tid + 512 i) / 8, k 4 ((tid + 512 i) % 8)
-    constexpr int NSA = ASPLIT ? 4 : 1;
+    // B row blocks wid (and wid + 8 for 16 blocks: WIDE)
+    constexpr int NBW = NBB > 8 ? 2 : 1;
+    const bool bw = wid < NBB;
+    unsigned b_base[NBW];
+    bool b_ok[NBW];
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) {
+      const int br = ((wid + 8 * j) % NBB) * RPB + drow;
+      const int b_ch = dslot ^ swz<PBK>(br);
+      b_ok[j] = bw && n0 + br < N;
+      b_base[j] = (unsigned)(((long long)(b_ok[j] ? n0 + br : 0) * P.ldb + b_ch * 8) * 2);
+    }
+    // x3d: fp32 float4 slots per thread (4; WIDE 2), slot i = row (tid + 512 i) / 8, k 4 ((tid + 512 i) % 8)
+    constexpr int NSA = ASPLIT ? PBM / 64 : 1;
     const int aq = tid & 7;
     unsigned s_base[NSA];
     int s_ih0[NSA], s_iw0[NSA];
@@ -268,12 +279,15 @@ gemm_x3p_kernel(const GemmArgs args) {
               ra, (lds_ptr_t)(base + p * PBM * PROWB + (NAB * wid + i) * RPB * PROWB), 16,
               aoff[i] == kOOBp ? kOOBp : aoff[i] + p * pA2, 0, 0, 0);
       if (bw) {
-        const unsigned boff = b_ok && kok ? b_base + (unsigned)k * 2 : kOOBp;
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * RPB * PROWB), 16,
-              boff == kOOBp ? kOOBp : boff + p * pB2, 0, 0, 0);
+        for (int j = 0; j < NBW; ++j) {
+          const unsigned boff = b_ok[j] && kok ? b_base[j] + (unsigned)k * 2 : kOOBp;
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + (wid + 8 * j) * RPB * PROWB), 16,
+                boff == kOOBp ? kOOBp : boff + p * pB2, 0, 0, 0);
+        }
       }
     };
     // x3d: fp32 A registers of one k-tile -> (prologue) -> three planes
@@ -286,34 +300,17 @@ gemm_x3p_kernel(const GemmArgs args) {
         if (PRO) v = make_float4(fmaxf(fmaf(v.x, sc.x, sh.x), 0.f), fmaxf(fmaf(v.y, sc.y, sh.y), 0.f),
                                  fmaxf(fmaf(v.z, sc.z, sh.z), 0.f), fmaxf(fmaf(v.w, sc.w, sh.w), 0.f));
         if (!((msk >> i) & 1u)) v = make_float4(0.f, 0.f, 0.f, 0.f);  // padding taps: zeros AFTER the BN
-        const float e[4] = {v.x, v.y, v.z, v.w};
-        unsigned short h[3][4];
+        unsigned lo[3], hi[3];
+        split3_pair(v.x, v.y, lo);
+        split3_pair(v.z, v.w, hi);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const __bf16 h0 = (__bf16)e[q];
-          const float r1 = e[q] - (float)h0;
-          const __bf16 h1 = (__bf16)r1;
-          const __bf16 h2 = (__bf16)(r1 - (float)h1);
-          h[0][q] = __builtin_bit_cast(unsigned short, h0);
-          h[1][q] = __builtin_bit_cast(unsigned short, h1);
-          h[2][q] = __builtin_bit_cast(unsigned short, h2);
-        }
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          uint2 w;
-          w.x = (unsigned)h[p][0] | ((unsigned)h[p][1] << 16);
-          w.y = (unsigned)h[p][2] | ((unsigned)h[p][3] << 16);
-          *reinterpret_cast<uint2*>(base + p * PBM * PROWB + s_lds[i]) = w;
-        }
+        for (int p = 0; p < 3; ++p)
+          *reinterpret_cast<uint2*>(base + p * PBM * PROWB + s_lds[i]) = make_uint2(lo[p], hi[p]);
       }
     };
     // x3d: the registers of the k-tile loaded by the last issue()
     auto store_a = [&](int buf) { store_a_from(buf, areg, a_sc, a_sh, a_msk); };
-#ifndef X3D_MID
-#define X3D_MID 0
-#endif
-    // X3D_MID (A/B): x3d writes the next k-tile's A planes between the two 16-k chunks' MFMAs
-    auto compute = [&](int buf, int nbuf) {
+    auto compute = [&](int buf) {
       const unsigned char* A_ = lds + buf * PBUF;
       const unsigned char* B_ = A_ + PA_BYTES;
       if constexpr (M16) {
@@ -352,7 +349,6 @@ gemm_x3p_kernel(const GemmArgs args) {
             acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][0], acc4[i][j], 0, 0, 0);
             acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][0], acc4[i][j], 0, 0, 0);
           }
-        (void)nbuf;
         return;
       }
       // every fragment of the k-tile is requested up front (2 x 12 ds_read_b128): the second
@@ -405,136 +401,20 @@ gemm_x3p_kernel(const GemmArgs args) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[g][i][1], b[g][j][0], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[g][i][0], b[g][j][0], acc[i][j], 0, 0, 0);
           }
-        if (X3D_MID && ASPLIT && g == 0) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          store_a(nbuf);
-        }
       }
-      (void)nbuf;
     };
-#ifndef X3D_DEEP
-#define X3D_DEEP 0
-#endif
-    if constexpr (ASPLIT && X3D_DEEP && !X3D_MID) {
-      // x3d with A TWO k-tiles ahead (round 3): the fp32 A of k-tile t sits in register slot t & 1
-      // (loaded in iteration t - 2), B goes by LDS-DMA one k-tile ahead as before, and so do the
-      // prologue's scale / shift (one register set). One k-tile of MFMAs (1536 cycles per SIMD) does
-      // not cover an HBM-latency load, so the one-deep form drained vmcnt(0) on A every k-tile. Per
-      // iteration the vector-memory instructions are issued in the order [B DMA + scale / shift of
-      // t + 1][the NSA A loads of t + 2], so `s_waitcnt vmcnt(NSA)` after the MFMAs retires exactly
-      // everything of t + 1 (loads return in order) and leaves A(t + 2) in flight. Every load is
-      // issued unconditionally (out-of-range offsets read zeros), so the count never changes.
-      static_assert(NSA == 4, "x3d deep pipeline: vmcnt immediate");
-      static_assert(!PRO || AMODE == 2, "x3d deep pipeline: the prologue walks the conv channels");
-      const auto rsc = rsrc_p(PRO ? (const void*)P.in_scale : P.A, PRO ? (unsigned)(cCin * 4) : 0u);
-      const auto rsh = rsrc_p(PRO ? (const void*)P.in_shift : P.A, PRO ? (unsigned)(cCin * 4) : 0u);
-      // channel walk of the scale / shift loads (one k-tile behind the A walk c_ci / c_kh / c_kw)
-      int b_ci = c_ci, b_tap = c_kh * cKW + c_kw;
-      const int taps = cKW * P.cKH;
-      auto load_a = [&](int kt, float4 (&ar)[NSA], unsigned& msk) {
-        const int k = k_lo + kt * PBK;
-        const bool kok = k < k_hi;
-        msk = 0;
-#pragma unroll
-        for (int i = 0; i < NSA; ++i) {
-          unsigned off;
-          bool ok;
-          if (AMODE == 0) {
-            ok = s_ok[i] && kok;
-            off = s_base[i] + (unsigned)k * 4;
-          } else {
-            const int ih = s_ih0[i] + c_kh, iw = s_iw0[i] + c_kw;
-            ok = s_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
-            off = ((s_base[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + aq * 4)) * 4u;
-          }
-          ar[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off : kOOBp, 0, 0));
-          msk |= (unsigned)ok << i;
-        }
-        if (AMODE == 2 && ++c_kw == cKW) {  // (PBK = 32: one k-tile per (slice, tap))
-          c_kw = 0;
-          if (++c_kh == P.cKH) {
-            c_kh = 0;
-            c_ci += 32;
-          }
-        }
-      };
-      auto issue_b = [&](int kt, int buf) {
-        const int k = k_lo + kt * PBK;
-        const bool kok = k < k_hi;
-        if constexpr (PRO) {
-          const unsigned o = kok ? (unsigned)(b_ci + aq * 4) * 4u : kOOBp;
-          a_sc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsc, o, 0, 0));
-          a_sh = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsh, o, 0, 0));
-          if (++b_tap == taps) {
-            b_tap = 0;
-            b_ci += 32;
-          }
-        }
-        unsigned char* base = lds + buf * PBUF;
-        if (bw) {
-          const unsigned boff = b_ok && kok ? b_base + (unsigned)k * 2 : kOOBp;
-#pragma unroll
-          for (int p = 0; p < 3; ++p)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * RPB * PROWB), 16,
-                boff == kOOBp ? kOOBp : boff + p * pB2, 0, 0, 0);
-        }
-      };
-      float4 ar0[NSA], ar1[NSA];
-      unsigned m0_ = 0, m1_ = 0;
-      issue_b(0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      load_a(0, ar0, m0_);
-      load_a(1, ar1, m1_);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // B(0), scale / shift(0), A(0)
-      store_a_from(0, ar0, a_sc, a_sh, m0_);
-      __syncthreads();
-      // iteration kt: B + scale / shift (kt + 1) -> buffer (kt + 1) & 1, A(kt + 2) -> the slot A(kt) left,
-      // MFMAs of kt, then A(kt + 1) from the other slot into LDS; unrolled by two (static slots)
-      int kt = 0;
-      for (; kt + 1 < nkt; kt += 2) {
-        issue_b(kt + 1, 1);
-        __builtin_amdgcn_sched_barrier(0);
-        load_a(kt + 2, ar0, m0_);
-        __builtin_amdgcn_sched_barrier(0);
-        compute(0, 1);
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        store_a_from(1, ar1, a_sc, a_sh, m1_);
-        __syncthreads();
-        issue_b(kt + 2, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        load_a(kt + 3, ar1, m1_);
-        __builtin_amdgcn_sched_barrier(0);
-        compute(1, 0);
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        store_a_from(0, ar0, a_sc, a_sh, m0_);
-        __syncthreads();
-      }
-      if (kt < nkt) {  // odd k-tile count: the last one (its successors are out of range: zeros)
-        issue_b(kt + 1, 1);
-        __builtin_amdgcn_sched_barrier(0);
-        load_a(kt + 2, ar0, m0_);
-        __builtin_amdgcn_sched_barrier(0);
-        compute(0, 1);
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        store_a_from(1, ar1, a_sc, a_sh, m1_);
-        __syncthreads();
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the out-of-range A loads: nothing left in flight
-      return;
-    }
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     store_a(0);
     __syncthreads();
     for (int kt = 0; kt < nkt; ++kt) {
       issue(kt + 1, (kt + 1) & 1);  // past the end: OOB loads (zeros) into the idle buffer
-      compute(kt & 1, (kt + 1) & 1);
+      compute(kt & 1);
 #if X3P_SKIP & 4  // timing-only: no barrier inside the k-loop
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (!X3D_MID) store_a((kt + 1) & 1);  // x3d: buffer (kt + 1) & 1 was last read by compute(kt - 1)
+      store_a((kt + 1) & 1);  // x3d: buffer (kt + 1) & 1 was last read by compute(kt - 1)
       __syncthreads();
 #endif
     }
@@ -761,27 +641,13 @@ gemm_x3p_kernel(const GemmArgs args) {
             __builtin_amdgcn_raw_buffer_store_b128(v, rs, (((i * JN32 + j) * 4 + q) * PNT + tid) * 16, 0, kSc1p);
           }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) __hip_atomic_store(flags + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sk_publish(flags + blockIdx.x, tid);
       continue;
     }
     if (ks > 0) {
       for (long long w2 = w - 1;; --w2) {
         const long long b2 = w2 * ngrp + grp;
-        if (tid == 0) {
-          int spins = 0;
-          while (__hip_atomic_load(flags + b2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-                 ++spins < (1 << 22))
-            __builtin_amdgcn_s_sleep(2);
-          // never expected: raise the error word and leave b2's flag (capmi.kernels.sk_check)
-          if (spins >= (1 << 22))
-            __hip_atomic_store(flags + gridDim.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else
-            __hip_atomic_store(flags + b2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        sk_consume(flags + b2, flags + gridDim.x, tid);
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + b2 * PART, 0, PART * 4, 0x00020000);
         if constexpr (M16) {
 #pragma unroll
@@ -825,33 +691,30 @@ __global__ void __launch_bounds__(256) bn_relu_split3_kernel(const float4* __res
       v = make_float4(fmaxf(fmaf(v.x, s.x, b.x), 0.f), fmaxf(fmaf(v.y, s.y, b.y), 0.f),
                       fmaxf(fmaf(v.z, s.z, b.z), 0.f), fmaxf(fmaf(v.w, s.w, b.w), 0.f));
     }
-    const float e[4] = {v.x, v.y, v.z, v.w};
-    unsigned short h[3][4];
+    unsigned lo[3], hi[3];
+    split3_pair(v.x, v.y, lo);
+    split3_pair(v.z, v.w, hi);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const __bf16 h0 = (__bf16)e[q];
-      const float r1 = e[q] - (float)h0;
-      const __bf16 h1 = (__bf16)r1;
-      const __bf16 h2 = (__bf16)(r1 - (float)h1);
-      h[0][q] = __builtin_bit_cast(unsigned short, h0);
-      h[1][q] = __builtin_bit_cast(unsigned short, h1);
-      h[2][q] = __builtin_bit_cast(unsigned short, h2);
-    }
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-      out[p * n4 + i] = (unsigned long long)h[p][0] | ((unsigned long long)h[p][1] << 16) |
-                        ((unsigned long long)h[p][2] << 32) | ((unsigned long long)h[p][3] << 48);
+    for (int p = 0; p < 3; ++p) out[p * n4 + i] = (unsigned long long)lo[p] | ((unsigned long long)hi[p] << 32);
   }
 }
 
 }  // namespace
 
-int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
+int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s, bool wide) {
   const dim3 g(blocks), b(PNT);
   const bool sk = a.sk_workers > 0;
   const bool pro = a.p[0].in_scale != nullptr;
 #define X3D_GO(M, S, PR) CAPMI_KLAUNCH((gemm_x3p_kernel<M, S, 32, true, PR>), g, b, 0, s, a)
-  if (amode == 2) {
+#define X3D_GOW(S, PR) CAPMI_KLAUNCH((gemm_x3p_kernel<0, S, 32, true, PR, true>), g, b, 0, s, a)
+  if (wide) {  // 128 x 256 tiles, dense rows
+    CAPMI_REQUIRE(amode == 0, CAPMI_EINVAL);
+    if (pro) {
+      if (sk) X3D_GOW(true, true); else X3D_GOW(false, true);
+    } else {
+      if (sk) X3D_GOW(true, false); else X3D_GOW(false, false);
+    }
+  } else if (amode == 2) {
     if (pro) {
       if (sk) X3D_GO(2, true, true); else X3D_GO(2, false, true);
     } else {
@@ -863,30 +726,17 @@ int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
     if (sk) X3D_GO(0, true, false); else X3D_GO(0, false, false);
   }
 #undef X3D_GO
+#undef X3D_GOW
   CAPMI_LAUNCH_CHECK();
   return 0;
 }
 
-int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_t s, int bn) {
+int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_t s) {
   const dim3 g(blocks), b(PNT);
   const bool sk = a.sk_workers > 0;
   // the two-workgroup form runs data-parallel grids only (its 128-VGPR budget has no room for
   // the stream-K hand-off)
   CAPMI_REQUIRE(bk == 32 || (bk == 16 && !sk), CAPMI_EINVAL);
-  CAPMI_REQUIRE(bn == 128 || bn == 64, CAPMI_EINVAL);
-  if (bn == 64) {  // the N = 64 convs (layer1's 3x3)
-#define X3P_GO64(M, S, BK) CAPMI_KLAUNCH((gemm_x3p_kernel<M, S, BK, false, false, 64>), g, b, 0, s, a)
-    if (bk == 16) {
-      if (amode == 2) X3P_GO64(2, false, 16); else X3P_GO64(0, false, 16);
-    } else if (amode == 2) {
-      if (sk) X3P_GO64(2, true, 32); else X3P_GO64(2, false, 32);
-    } else {
-      if (sk) X3P_GO64(0, true, 32); else X3P_GO64(0, false, 32);
-    }
-#undef X3P_GO64
-    CAPMI_LAUNCH_CHECK();
-    return 0;
-  }
 #define X3P_GO(M, S, BK) CAPMI_KLAUNCH((gemm_x3p_kernel<M, S, BK>), g, b, 0, s, a)
   if (bk == 16) {
     if (amode == 2)

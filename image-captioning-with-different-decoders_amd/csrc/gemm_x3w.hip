@@ -1,0 +1,325 @@
+// fp32-accurate conv WEIGHT gradient on the bf16 matrix cores ("x3w", round 4): C[m][n] = sum_k A[k][m] B[k][n],
+// k = output pixel, A = dY (the conv output's gradient, fp32 [pixel][Cout]) and B = the conv input relu(bn(y))
+// as fp32 k rows ([pixel][Cin]: a 1x1 conv) or the implicit im2col of the NHWC input (n = (kh, kw, ci), the
+// packed weight order; stride / padding taps read zeros), the BN-apply + ReLU applied to B in the kernel
+// (in_scale / in_shift). Replaces the weight-gradient half of nn.Conv2d's backward for the trainable layer2-4
+// convs of EncoderAttention.fine_tune (models/encoder.py:112-121, driven by models/attention.py:417-430).
+//
+// Both operands are K-OUTER in memory (a k-tile is 32 pixel rows of channels): the transpose of what the MFMA
+// takes (each lane 8 consecutive k of one m / n). Each thread loads its fp32 float4s of the next k-tile while
+// the current one is multiplied, then splits them exactly into the three bf16 terms of gemm_x3 (split3_pair)
+// and stores them row-major into a swizzled LDS image; the MFMA operands are read back with
+// ds_read_b64_tr_b16, which hands each 16-lane group a 4 k-row x 16-column block column-major, so two reads
+// give a lane its 8 consecutive k. x3 arithmetic (six cross products above 2^-23 |a||b|, fp32 accumulation,
+// smallest terms first); tile 256 x 128 (M x N), 512 threads as 4 x 2 waves of 64 x 64 (16 blocks of
+// v_mfma_f32_16x16x32_bf16 x 6 products per 32-deep k-tile), LDS double buffer of 2 x 72 KiB, one barrier
+// per k-tile. A weight gradient has few output tiles (layer3's 3x3: 18) and a long k (12544 pixels at
+// batch 64): the k range is split S ways so the grid fills the CUs, and the S partial slabs are summed in a
+// fixed order afterwards (deterministic). It replaces the split-staging nts kernel's weight gradients (round-3
+// VERDICT: 0.26 of the x3 bound, 244 MB per launch against 28 MB).
+#include "gemm_args.h"
+
+namespace {
+
+constexpr int WBM = 256, WBN = 128, WBK = 32, WNT = 512;
+constexpr int WA_ROWB = WBM * 2;            // bytes per A k-row per plane (256 bf16)
+constexpr int WB_ROWB = WBN * 2;            // bytes per B k-row per plane (128 bf16)
+constexpr int WA_PLANE = WBK * WA_ROWB;     // 16 KiB
+constexpr int WB_PLANE = WBK * WB_ROWB;     // 8 KiB
+constexpr int WA_BYTES = 3 * WA_PLANE;      // 48 KiB
+constexpr int WBUF = WA_BYTES + 3 * WB_PLANE;  // 72 KiB per buffer
+constexpr unsigned kOOBw = 0x80000000u;
+typedef float f32x4_w __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_w __attribute__((ext_vector_type(8)));
+typedef short s16x4_w __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_w* lds_s16x4_w;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_w(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+// 16-B chunk c of k-row r is stored in slot c ^ wsw(r). A transposed read's 32-lane half takes k-rows
+// {8h .. 8h+3, 8h+8 .. 8h+11} (or those + 4) x the same 32 bytes of columns; rows 256 / 512 B apart share
+// their banks, so the XOR by 2 x (the row's index in that set of 8) puts the 16 chunks on 16 distinct slots
+// of the 64-bank window (conflict-free)
+__device__ __forceinline__ int wsw(int r) { return ((r & 3) | (((r >> 3) & 1) << 2)) << 1; }
+
+// one ds_read_b64_tr_b16: the 4 k-rows r0 + (lane & 15) / 4 ... of this lane's group, columns c0 + 4 (lane & 3)
+__device__ __forceinline__ s16x4_w tr_read(const unsigned char* plane, int rowb, int r, int col) {
+  const int off = r * rowb + ((((col >> 3) ^ wsw(r))) << 4) + ((col & 4) << 1);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_w)(plane + off));
+}
+
+// BMODE: CAPMI_B_KROWS (1, B dense k rows) or CAPMI_B_CONV_NHWC (2, implicit im2col of the conv input);
+// SK: k-split into partial slabs (the grid's S > 1)
+template <int BMODE, bool SK>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+gemm_x3w_kernel(const GemmArgs args) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * WBUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm0 = (wid >> 1) * 64, wn0 = (wid & 1) * 64;
+  f32x4_w acc4[4][4];
+
+  auto mainloop = [&](const capmi_gemm_problem& P, int m0, int n0, int k_lo, int k_hi) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc4[i][j] = f32x4_w{0.f, 0.f, 0.f, 0.f};
+    const int nkt = (k_hi - k_lo + WBK - 1) / WBK;
+    if (nkt <= 0) return;
+    const int M = P.M, N = P.N;
+    const long long planeB = BMODE == 2 ? (long long)P.cN * P.cH * P.cW * P.cCin : (long long)P.K * P.ldb;
+    const auto ra = rsrc_w(P.A, (unsigned)((long long)P.K * P.lda * 4));
+    const auto rb = rsrc_w(P.B, (unsigned)(planeB * 4));
+    // prologue scale / shift through descriptors sized to the channel count (a read past it returns 0)
+    const unsigned ss_bytes = P.in_scale ? (unsigned)((BMODE == 2 ? P.cCin : N) * 4) : 0u;
+    const auto rsc = rsrc_w(P.in_scale ? (const void*)P.in_scale : P.A, ss_bytes);
+    const auto rsh = rsrc_w(P.in_shift ? (const void*)P.in_shift : P.A, ss_bytes);
+    // A = dY fp32 [k][lda]: a k-tile is 32 rows x 256 columns = 2048 float4, 4 per thread: float4 f =
+    // tid + 512 i is row tid / 64 + 8 i, columns m0 + 4 (tid % 64) (one wave writes one whole LDS row)
+    const int a_c4 = tid & 63, a_r0 = tid >> 6;
+    const bool a_mok = m0 + 4 * a_c4 < M;
+    // B fp32 [k][ldb] or the conv input: 32 rows x 128 columns = 1024 float4, 2 per thread: row tid / 32 + 16 i,
+    // columns n0 + 4 (tid % 32); a thread keeps its n (and so its tap and channels) for the whole k-loop
+    const int b_c4 = tid & 31, b_r0 = tid >> 5;
+    const int b_n = n0 + 4 * b_c4;
+    const bool b_nok = b_n < N;
+    int b_ci = b_n, b_kh = 0, b_kw = 0;
+    if (BMODE == 2) {
+      const int tap = b_n / P.cCin;
+      b_ci = b_n - tap * P.cCin;
+      b_kh = tap / P.cKW;
+      b_kw = tap - b_kh * P.cKW;
+    }
+    float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), sh = make_float4(0.f, 0.f, 0.f, 0.f);
+    const bool pro = P.in_scale != nullptr;
+    if (pro && b_nok) {
+      sc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsc, (unsigned)b_ci * 4u, 0, 0));
+      sh = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsh, (unsigned)b_ci * 4u, 0, 0));
+    }
+    const int hw = P.cHo * P.cWo;
+    float4 ar[4], br[2];
+    unsigned bmask = 0;
+    auto load = [&](int kt) {
+      const int k = k_lo + kt * WBK;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = k + a_r0 + 8 * i;
+        const bool ok = a_mok && row < k_hi;
+        ar[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               ra, ok ? (unsigned)(((long long)row * P.lda + m0 + 4 * a_c4) * 4) : kOOBw, 0, 0));
+      }
+      bmask = 0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int pix = k + b_r0 + 16 * i;
+        unsigned off = kOOBw;
+        if (b_nok && pix < k_hi) {
+          if (BMODE == 2) {
+            const int n_img = pix / hw, rem = pix - n_img * hw;
+            const int oh = rem / P.cWo, ow = rem - oh * P.cWo;
+            const int ih = oh * P.cStride - P.cPad + b_kh, iw = ow * P.cStride - P.cPad + b_kw;
+            if ((unsigned)ih < (unsigned)P.cH && (unsigned)iw < (unsigned)P.cW)
+              off = (unsigned)(((long long)(n_img * P.cH + ih) * P.cW + iw) * P.cCin + b_ci) * 4u;
+          } else {
+            off = (unsigned)(((long long)pix * P.ldb + b_n) * 4);
+          }
+        }
+        br[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, 0));
+        bmask |= (unsigned)(off != kOOBw) << i;
+      }
+    };
+    // registers -> (B: BN-apply + ReLU, padding taps zero AFTER it) -> three swizzled bf16 planes
+    auto store = [&](int buf) {
+      unsigned char* base = lds + buf * WBUF;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = a_r0 + 8 * i;
+        const int o = r * WA_ROWB + (((a_c4 >> 1) ^ wsw(r)) << 4) + (a_c4 & 1) * 8;
+        unsigned lo[3], hi[3];
+        split3_pair(ar[i].x, ar[i].y, lo);
+        split3_pair(ar[i].z, ar[i].w, hi);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(base + p * WA_PLANE + o) = make_uint2(lo[p], hi[p]);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = b_r0 + 16 * i;
+        const int o = r * WB_ROWB + (((b_c4 >> 1) ^ wsw(r)) << 4) + (b_c4 & 1) * 8;
+        float4 v = br[i];
+        if (pro) v = make_float4(fmaxf(fmaf(v.x, sc.x, sh.x), 0.f), fmaxf(fmaf(v.y, sc.y, sh.y), 0.f),
+                                 fmaxf(fmaf(v.z, sc.z, sh.z), 0.f), fmaxf(fmaf(v.w, sc.w, sh.w), 0.f));
+        if (!((bmask >> i) & 1u)) v = make_float4(0.f, 0.f, 0.f, 0.f);
+        unsigned lo[3], hi[3];
+        split3_pair(v.x, v.y, lo);
+        split3_pair(v.z, v.w, hi);
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          *reinterpret_cast<uint2*>(base + WA_BYTES + p * WB_PLANE + o) = make_uint2(lo[p], hi[p]);
+      }
+    };
+    // transposed fragment reads: lane l of group g = l / 16 takes k-rows 8g + (l & 15) / 4 (+ 4), columns
+    // base + 4 (l & 3); it receives column l & 15 of those 4 rows, k = 8g .. 8g + 3 (+ 4 .. 7)
+    const int g8 = (lane >> 4) * 8, q = (lane & 15) >> 2, c4 = (lane & 3) * 4;
+    auto compute = [&](int buf) {
+      const unsigned char* A_ = lds + buf * WBUF;
+      const unsigned char* B_ = A_ + WA_BYTES;
+      bf16x8_w a[4][3], b[4][3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const s16x4_w lo = tr_read(A_ + p * WA_PLANE, WA_ROWB, g8 + q, wm0 + 16 * i + c4);
+          const s16x4_w hi = tr_read(A_ + p * WA_PLANE, WA_ROWB, g8 + 4 + q, wm0 + 16 * i + c4);
+          a[i][p] = __builtin_bit_cast(bf16x8_w, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const s16x4_w lo = tr_read(B_ + p * WB_PLANE, WB_ROWB, g8 + q, wn0 + 16 * j + c4);
+          const s16x4_w hi = tr_read(B_ + p * WB_PLANE, WB_ROWB, g8 + 4 + q, wn0 + 16 * j + c4);
+          b[j][p] = __builtin_bit_cast(bf16x8_w, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+      // smallest terms first into each fp32 accumulator (gemm_x3p.hip's order)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][1], acc4[i][j], 0, 0, 0);
+          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][2], acc4[i][j], 0, 0, 0);
+          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[j][0], acc4[i][j], 0, 0, 0);
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][1], acc4[i][j], 0, 0, 0);
+          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][0], acc4[i][j], 0, 0, 0);
+          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][0], acc4[i][j], 0, 0, 0);
+        }
+    };
+    load(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store(0);
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+      load(kt + 1);  // past the end: OOB loads (zeros), stored into the idle buffer
+      compute(kt & 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      store((kt + 1) & 1);  // buffer (kt + 1) & 1 was last read by compute(kt - 1)
+      __syncthreads();
+    }
+  };
+
+  // epilogue: C (fp32, ldc) = alpha A.B (+ beta C); 16x16 blocks: lane l holds rows 4 (l / 16) .. + 3 of
+  // column l % 16 of each block
+  auto epilogue = [&](const capmi_gemm_problem& P, int tm, int tn) {
+    const int M = P.M, N = P.N;
+    const int m0 = tm * WBM, n0 = tn * WBN;
+    const float alpha = P.alpha * (P.alpha_ptr ? *P.alpha_ptr : 1.f);
+    const float beta = P.beta;
+    float* C = P.C;
+    const long long ldc = P.ldc;
+    const int cl = lane & 15, rq = lane >> 4;
+    if (args.plain_epi) {  // store-only form (host: plain_epilogue): 16 row offsets per lane once
+      const auto rc = rsrc_w(C, (unsigned)((long long)M * ldc * 4));
+      unsigned roff[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm0 + 16 * i + 4 * rq + r;
+          roff[i][r] = row < M ? (unsigned)row * (unsigned)ldc * 4u : kOOBw;
+        }
+      const unsigned cb = (unsigned)(n0 + wn0 + cl) * 4u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc4[i][j][r];
+            if (args.plain_epi == 2)
+              v = fmaf(beta, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rc, roff[i][r] + cb + 64u * j, 0, 0)), v);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, roff[i][r] + cb + 64u * j, 0, 0);
+          }
+      return;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wn0 + 16 * j + cl;
+      if (col >= N) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm0 + 16 * i + 4 * rq + r;
+          if (row < M) {
+            float* cp = C + (long long)row * ldc + col;
+            float v = acc4[i][j][r] * alpha;
+            if (beta != 0.f) v = fmaf(beta, *cp, v);
+            *cp = v;
+          }
+        }
+    }
+  };
+
+  // grid = tiles x S k-splits (S = args.kchunk[0] k-tiles each; the host reduces the S partial slabs with
+  // capmi_splitk_reduce, a fixed order: deterministic). XCD-aware order: blocks of one XCD (blockIdx % 8)
+  // are contiguous in bid, and bid = z * tiles + t, so an XCD runs the tiles of one k-chunk z: the chunk's
+  // dY rows are read into that XCD's L2 once for all its tiles
+  const capmi_gemm_problem& P = args.p[0];
+  const int tiles_n = args.tiles_n[0], tiles = args.tiles_m[0] * tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+  }
+  const int z = bid / tiles, t = bid - z * tiles;
+  const int tm = t / tiles_n, tn = t - tm * tiles_n;
+  const int kc = args.kchunk[0] * WBK;
+  const int k_lo = z * kc, k_hi = min(P.K, k_lo + kc);
+  mainloop(P, tm * WBM, tn * WBN, k_lo, k_hi);
+  if (!SK) {
+    epilogue(P, tm, tn);
+    return;
+  }
+  // k-split: the raw partial into slab z of the workspace ([S][M][ldp], ldp = tiles_n * WBN)
+  const int ldp = tiles_n * WBN;
+  const auto rc = rsrc_w(args.sk_part + (long long)z * P.M * ldp, (unsigned)((long long)P.M * ldp * 4));
+  const int cl = lane & 15, rq = lane >> 4;
+  const int m0 = tm * WBM, n0 = tn * WBN;
+  const unsigned cb = (unsigned)(n0 + wn0 + cl) * 4u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + wm0 + 16 * i + 4 * rq + r;
+      const unsigned ro = row < P.M ? (unsigned)row * (unsigned)ldp * 4u : kOOBw;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc4[i][j][r]), rc, ro + cb + 64u * j, 0, 0);
+    }
+}
+
+}  // namespace
+
+int gemm_x3w_launch(const GemmArgs& a, int bmode, int blocks, hipStream_t s) {
+  const dim3 g(blocks), b(WNT);
+  const bool sk = a.kchunk[0] * WBK < a.p[0].K;  // k split over several workgroups: partial slabs
+  if (bmode == 2) {
+    if (sk)
+      CAPMI_KLAUNCH((gemm_x3w_kernel<2, true>), g, b, 0, s, a);
+    else
+      CAPMI_KLAUNCH((gemm_x3w_kernel<2, false>), g, b, 0, s, a);
+  } else {
+    if (sk)
+      CAPMI_KLAUNCH((gemm_x3w_kernel<1, true>), g, b, 0, s, a);
+    else
+      CAPMI_KLAUNCH((gemm_x3w_kernel<1, false>), g, b, 0, s, a);
+  }
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}

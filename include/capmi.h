@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 18
+#define CAPMI_ABI_VERSION 19
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -60,7 +60,7 @@ enum capmi_bmode {
  * CAPMI_TILE_128_W8: 128x128 with 512-thread workgroups (8 waves, one workgroup per CU), forward
  * modes (A row-major / conv x W[N][K]) of capmi_gemm_sk only */
 enum capmi_tile { CAPMI_TILE_128 = 0, CAPMI_TILE_64 = 1, CAPMI_TILE_128x64 = 2, CAPMI_TILE_AUTO = 3,
-                  CAPMI_TILE_128_W8 = 4 };
+                  CAPMI_TILE_128_W8 = 4, CAPMI_TILE_128x256 = 5 /* CAPMI_GEMM_X3D on dense rows only */ };
 
 typedef struct capmi_gemm_problem {
   int M, N, K;
@@ -78,16 +78,6 @@ typedef struct capmi_gemm_problem {
   int cN, cH, cW, cCin, cKH, cKW, cStride, cPad, cHo, cWo;
   const float* in_scale; /* NULL or [Cin]: A element := relu(x*in_scale[ci] + in_shift[ci]) in-bounds (BN-apply+ReLU prologue) */
   const float* in_shift;
-  /* ABI 18, CAPMI_GEMM_X3 with CAPMI_A_KMAJOR only (the fused bottleneck tail, models/encoder.py:88-91
-   * via torchvision's Bottleneck.forward "out += identity; out = relu(out)"): when in_res is set, A
-   * element (m, k) := relu(fma(A, in_scale[k], in_shift[k]) + r), r = in_res[m][k] (lda-strided) or
-   * fma(in_res, in_res_scale[k], in_res_shift[k]) (downsample BN) -- the capmi_bn_add_relu formula, bit
-   * for bit -- and the workgroups of the first column tile also store it to in_out[m][k] (the block
-   * output, the next tail's residual); in_scale, in_shift and in_out are then required. NULL: unused. */
-  const float* in_res;
-  const float* in_res_scale;
-  const float* in_res_shift;
-  float* in_out;
 } capmi_gemm_problem;
 
 int capmi_gemm(const capmi_gemm_problem* problems, int nprob, int amode, int bmode, int tile,
@@ -121,10 +111,8 @@ int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int t
  * leading dimensions in elements), v_mfma_f32_32x32x16_bf16 with fp32 accumulation, C rounded to bf16
  * (RNE) once, `stats` fp32 from the stored values. A = CAPMI_A_KMAJOR (lda % 8 == 0) or
  * CAPMI_A_CONV_NHWC (Cin % 64 == 0) x B = W[N][K] (CAPMI_B_NMAJOR_W, ldb % 8 == 0); K % 64 == 0;
- * alpha 1, beta 0, no bias / relu / ksplit. Optional BN-apply + ReLU prologue (in_scale / in_shift fp32
- * [Cin]; CAPMI_A_KMAJOR needs lda == K): each A element becomes relu(fma(a, scale, shift)) rounded to bf16
- * (RNE), capmi_bn_relu_bf16's arithmetic bit for bit, padding taps zero after it (round 3: the bf16
- * encoder no longer materialises conv3's input). Tile 128x128, or 128x64 for CAPMI_TILE_128x64 / N <= 64. */
+ * alpha 1, beta 0, no bias / relu / ksplit, no prologue (the conv input is relu(bn(y)) materialised in bf16
+ * by capmi_bn_relu_bf16). Tile 128x128, or 128x64 for CAPMI_TILE_128x64 / N <= 64. */
 #define CAPMI_GEMM_BF16_IO 2
 /* CAPMI_GEMM_X3 (alone): fp32-accurate GEMM on the bf16 matrix cores. A is fp32 (CAPMI_A_KMAJOR,
  * lda % 4 == 0, or CAPMI_A_CONV_NHWC, Cin % 32 == 0, with the optional BN-apply + ReLU prologue);
@@ -157,6 +145,17 @@ int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int t
  * remap / ksplit) with the optional `stats`. Persistent 256-thread workgroups (two per CU) stream 64-row
  * tiles with the weight held in registers; the workspace is not used (may be NULL). */
 #define CAPMI_GEMM_X3S 64
+/* CAPMI_GEMM_X3W (alone, ABI 19): the conv WEIGHT gradient in the CAPMI_GEMM_X3 arithmetic, C[M][N] =
+ * sum_k A[k][m] B[k][n] with k = output pixel: A = dY fp32 (CAPMI_A_MMAJOR, [K][lda], lda % 4 == 0) and B =
+ * the conv input fp32 as k rows (CAPMI_B_KROWS, [K][ldb]) or through its implicit im2col (CAPMI_B_CONV_NHWC,
+ * n = (kh, kw, ci), the packed [Cout][KH][KW][Cin] weight order, Cin % 4 == 0), with the optional BN-apply +
+ * ReLU prologue on B (in_scale / in_shift [Cin]; padding taps zero after it); M % 4 == 0, N % 4 == 0; alpha /
+ * beta only, no bias / relu / stats / ksplit. Both operands are split into three bf16 terms in the kernel and
+ * read back transposed (ds_read_b64_tr_b16); 256x128 tiles, 512 threads, one workgroup per CU. With alpha 1
+ * and beta 0 the pixel range is split over several workgroups whose partial slabs go to the workspace (as
+ * capmi_gemm_sk's) and are summed in a fixed order (capmi_splitk_reduce); capmi_gemm_sk_plan reports the
+ * split count in `generic`. */
+#define CAPMI_GEMM_X3W 128
 /* CAPMI_GEMM_SPLIT3 (alone): fp32 A and B, both split exactly into three bf16 terms when staged to
  * LDS (the CAPMI_GEMM_X3 arithmetic with no pre-split operand: fp32-accurate on the bf16 matrix
  * cores). Dense modes only: CAPMI_A_KMAJOR x CAPMI_B_NMAJOR_W / CAPMI_B_KROWS and CAPMI_A_MMAJOR x
@@ -505,27 +504,6 @@ int capmi_embed_scatter_add(const float* dx, long long ld_dx, const long long* c
  * term the RNE bf16 rounding of the remainder (B operand of CAPMI_GEMM_X3). */
 int capmi_split3_bf16(const float* in, long long n, void* out, void* stream);
 
-/* Train-mode BatchNorm finalize fused into the pass that consumes it (replaces capmi_bn_finalize +
- * the apply pass for layer3/4-sized tensors: tiles <= CAPMI_BNFA_MAX_TILES slices). Every workgroup
- * finalizes its 32 channels from `stats` (fp64, fixed order; bn_finalize's formulas), then applies
- * them to its rows; scale / shift are written and the running statistics updated once (gamma,
- * beta, running_*: models/encoder.py:88-91 nn.BatchNorm2d, train mode). rows = count = the conv's
- * output rows; C % 32 == 0.
- *   CAPMI_BNFA_SPLIT3        y fp32 [rows][C] -> out = relu(bn(y)) split into three bf16 planes
- *                            [3][rows*C] (the capmi_bn_relu_split3 output; x3p conv input)
- *   CAPMI_BNFA_ADD_RELU      y, res fp32 -> out fp32 = relu(bn(y) + res)   (bottleneck tail)
- *   CAPMI_BNFA_RELU_BF16     y bf16 -> out bf16 = relu(bn(y)) (out may alias y)
- *   CAPMI_BNFA_ADD_RELU_BF16 y, res bf16 -> out bf16 = relu(bn(y) + res)
- * res must be NULL for the ops without a residual. */
-#define CAPMI_BNFA_SPLIT3 0
-#define CAPMI_BNFA_ADD_RELU 1
-#define CAPMI_BNFA_RELU_BF16 2
-#define CAPMI_BNFA_ADD_RELU_BF16 3
-#define CAPMI_BNFA_MAX_TILES 256
-int capmi_bn_finalize_apply(int op, const float* stats, int tiles, int C, long long count, const float* gamma,
-                            const float* beta, float* running_mean, float* running_var, float momentum, float eps,
-                            float* scale, float* shift, const void* y, const void* res, void* out, long long rows,
-                            void* stream);
 /* x = relu(y * scale[c] + shift[c]) of y [rows][C] fp32 (scale = shift = NULL: x = y), written as
  * the three bf16 split planes out[3][rows * C] (the CAPMI_GEMM_X3P A operand); C % 4 == 0. */
 int capmi_bn_relu_split3(const float* y, const float* scale, const float* shift, long long rows, int C, void* out,

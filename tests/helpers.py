@@ -74,6 +74,64 @@ def decoder_att_masks(dup=1):
     return torch.stack(out)
 
 
+def _oracle_att_preacts(p, enc, caps, lengths, dtype):
+    """Per decode step of the oracle forward (oracle.decoder_ref.decoder_forward, models/attention.py:
+    218-284) in ``dtype`` on its OWN attention-ReLU branch: yields (z, s) with z = the score pre-activation
+    att_enc + att_dec (B, P, A) and s = its magnitude bound |enc| |W_ea|^T + |b_ea| + |h| |W_da|^T + |b_da|
+    (the scale of the rounding error of the two dot products that form z). The attention-score ReLU is the
+    decoder's only branch; its decisions at |z| within rounding of 0 differ between fp32 paths."""
+    import torch.nn.functional as F
+    from oracle import decoder_ref as R
+    q = {k: v.to(dtype) for k, v in p.items()}
+    e = enc.to(dtype)
+    emb = F.embedding(caps, q["embedding.weight"]).to(dtype)
+    h, c = R.init_hidden_state(q, e)
+    ae = R._lin(e, q, "attention.enc_att")  # loop-invariant (models/attention.py:54, recomputed there)
+    sa = e.abs() @ q["attention.enc_att.weight"].abs().t() + q["attention.enc_att.bias"].abs()
+    for t_ in range(max(lengths) - 1):
+        ad = R._lin(h, q, "attention.dec_att")
+        sd = h.abs() @ q["attention.dec_att.weight"].abs().t() + q["attention.dec_att.bias"].abs()
+        z = ae + ad.unsqueeze(1)
+        yield z, sa + sd.unsqueeze(1)
+        att = R._lin(torch.relu(z), q, "attention.full_att").squeeze(2)
+        alpha = torch.softmax(att, dim=1)
+        awe = torch.sigmoid(R._lin(h, q, "f_beta")) * (e * alpha.unsqueeze(2)).sum(dim=1)
+        h, c = R.lstm_cell(torch.cat([emb[:, t_, :], awe], 1), h, c, q)
+
+
+def decoder_att_flips(p, enc, caps, lengths, dup=1):
+    """The attention-score pre-activations z of the last capmi decoder forward (ATT_ENC + AD, kept for its
+    backward; decoder_att_masks' source) against the fp64 oracle on its OWN branch, beside the fp32 CPU
+    oracle's. Returns dict: n_gpu / n_cpu = ReLU decisions differing from fp64's (over the reference's P
+    positions); err_gpu / err_cpu = rms(z - z64) / rms(z64); worst_gpu / worst_cpu = the largest flipped |z64|
+    in fp32 unit roundoffs (2^-24) of z's magnitude bound s64 (a rounding-level decision sits within a few
+    tens of them: the dot products have K = 2048 and 512)."""
+    from capmi import decoder_fn as DF
+    ws = next(iter(DF.CORE._ws.values()))
+    ae_g, ad_g = ws.ATT_ENC.double().cpu(), ws.AD.double().cpu()
+    u = 2.0 ** -24
+    r = dict(n_gpu=0, n_cpu=0, worst_gpu=0.0, worst_cpu=0.0)
+    e2 = {"gpu": 0.0, "cpu": 0.0}
+    ref2 = 0.0
+    for t_, ((z64, s64), (z32, _)) in enumerate(zip(_oracle_att_preacts(p, enc, caps, lengths, torch.float64),
+                                                    _oracle_att_preacts(p, enc, caps, lengths, torch.float32))):
+        zg = ae_g + ad_g[t_].unsqueeze(1)  # (B, Q, A)
+        if dup > 1:
+            B_, Q_, A_ = zg.shape
+            F_ = int(round(Q_ ** 0.5))
+            zg = zg.view(B_, F_, F_, A_).repeat_interleave(dup, 1).repeat_interleave(dup, 2).reshape(B_, -1, A_)
+        ref2 += float((z64 ** 2).sum())
+        for name, z in (("gpu", zg), ("cpu", z32.double())):
+            e2[name] += float(((z - z64) ** 2).sum())
+            bad = (z > 0) != (z64 > 0)
+            n = int(bad.sum())
+            if n:
+                r["n_" + name] += n
+                r["worst_" + name] = max(r["worst_" + name], float((z64[bad].abs() / (s64[bad] * u)).max()))
+    r["err_gpu"], r["err_cpu"] = (e2["gpu"] / ref2) ** 0.5, (e2["cpu"] / ref2) ** 0.5
+    return r
+
+
 def mask_flips(got, ref):
     """Number of elements where two ReLU branches disagree, over all masks."""
     return sum(int((got[k] != ref[k]).sum()) for k in ref)

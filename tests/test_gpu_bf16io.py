@@ -138,43 +138,3 @@ def test_bf16_elementwise():
         K.adaptive_avgpool_bf16(m.to(DEV), 2, Hh, Hh, 64, O, O, o)
         want = F.adaptive_avg_pool2d(m.float().permute(0, 3, 1, 2), (O, O)).permute(0, 2, 3, 1)
         torch.testing.assert_close(o.cpu(), want, rtol=1e-6, atol=1e-6)
-
-
-@pytest.mark.parametrize("N,H,Cin,Cout,k,stride", [(2, 14, 256, 1024, 1, 1), (3, 9, 64, 128, 3, 1),
-                                                   (64, 14, 256, 1024, 1, 1), (2, 28, 128, 128, 3, 2),
-                                                   (64, 14, 256, 256, 3, 1)])
-def test_bf16io_prologue_bit_identical(N, H, Cin, Cout, k, stride):
-    """CAPMI_GEMM_BF16_IO with the BN-apply + ReLU prologue (round 3) == capmi_bn_relu_bf16 followed by the
-    plain bf16 GEMM, bit for bit (output and BN statistics), padding taps zero after the prologue."""
-    from capmi import kernels as K
-    g = torch.Generator().manual_seed(91)
-    pad = k // 2
-    Ho = (H + 2 * pad - k) // stride + 1
-    rows, Kd = N * Ho * Ho, k * k * Cin
-    y = (torch.randn(N * H * H, Cin, generator=g)).to(DEV).to(torch.bfloat16)
-    s = (torch.rand(Cin, generator=g) + 0.5).to(DEV)
-    b = (torch.randn(Cin, generator=g) * 0.3).to(DEV)
-    w = (torch.randn(Cout, Kd, generator=g) * (2.0 / Kd) ** 0.5).to(DEV).to(torch.bfloat16)
-    ws = K.gemm_workspace(DEV)
-    geo = dict(N=N, H=H, W=H, Cin=Cin, KH=k, KW=k, stride=stride, pad=pad, Ho=Ho, Wo=Ho)
-    dense = k == 1 and stride == 1
-
-    def prob(a, out, st, **kw):
-        if dense:
-            return K.problem_bf16(rows, Cout, Kd, a, Cin, w, Kd, out, Cout, stats=st, **kw), 0
-        return K.problem_bf16(rows, Cout, Kd, a, 0, w, Kd, out, Cout, stats=st, conv=geo, **kw), 2
-
-    x = torch.empty_like(y)
-    K.bn_relu_bf16(y, s, b, N * H * H, Cin, x)
-    c_ref = torch.empty(rows, Cout, device=DEV, dtype=torch.bfloat16)
-    st_ref = torch.zeros(2 * K.stat_tiles(rows) * Cout, device=DEV)
-    p, m = prob(x, c_ref, st_ref)
-    K.gemm_bf16(p, m, ws)
-    c_f = torch.empty(rows, Cout, device=DEV, dtype=torch.bfloat16)
-    st_f = torch.zeros(2 * K.stat_tiles(rows) * Cout, device=DEV)
-    p, m = prob(y, c_f, st_f, in_scale=s, in_shift=b)
-    K.gemm_bf16(p, m, ws)
-    torch.cuda.synchronize()
-    K.sk_check([ws])
-    assert torch.equal(c_f, c_ref)
-    assert torch.equal(st_f, st_ref)

@@ -16,7 +16,7 @@ import pytest
 import torch
 
 import gen
-from helpers import assert_close, decoder_att_masks, make_decoder, rel_err, t
+from helpers import assert_close, decoder_att_flips, decoder_att_masks, make_decoder, rel_err, t
 from oracle import decoder_ref as R
 from test_gpu_decoder import ALPHA_ATOL, KINK_ROWS, LOGIT_ATOL, LOGIT_RTOL, _grad_check
 
@@ -30,9 +30,32 @@ def _threads():
     return int(env) if env.isdigit() and int(env) > 0 else min(16, os.cpu_count() or 1)
 
 
+# attention-score ReLU flips (helpers.decoder_att_flips): each decision the GPU takes on the other side of 0 from
+# the fp64 oracle must be a rounding-level one -- |z64| within this many fp32 unit roundoffs of z's magnitude
+# bound (the dot products forming z have K = 2048 and 512: their rounding error is a few to a few tens of units)
+FLIP_UNITS = 64
+
+
+def _check_att_flips(p, ref_enc, caps, dup, what):
+    """The bound on the branch alignment of ``_check_grads(aligned=True)`` (the encoder's is
+    tests/test_gpu_finetune.py::_check_branch_aligned): the GPU's score pre-activations z (ATT_ENC + AD)
+    within 4x the fp32 CPU oracle's error against fp64 (rms, relative); no more ReLU decisions differing
+    from fp64's than 4x the CPU's + 2 per duplicate group (flips follow the error of z: a path with a larger
+    z error flips more of the values near 0); every such flip a rounding-level decision (FLIP_UNITS of z's
+    magnitude bound, or within twice the CPU path's own worst)."""
+    r = decoder_att_flips(p, ref_enc, caps, [caps.shape[1]] * caps.shape[0], dup)
+    print(f"{what}: attention pre-activation error vs fp64 gpu {r['err_gpu']:.3g} cpu32 {r['err_cpu']:.3g}; ReLU "
+          f"flips gpu {r['n_gpu']} cpu32 {r['n_cpu']}; worst flipped |z| {r['worst_gpu']:.3g} / "
+          f"{r['worst_cpu']:.3g} units of its magnitude bound")
+    assert r["err_gpu"] <= 4 * r["err_cpu"] + 1e-7, (what, r)
+    assert r["n_gpu"] <= 4 * r["n_cpu"] + 2 * dup * dup, (what, r)
+    assert r["worst_gpu"] <= max(FLIP_UNITS, 2 * r["worst_cpu"]), (what, r)
+
+
 def _check_grads(grads, rraw, trainable, aligned=False):
     """tests/test_gpu_decoder.py's rule. ``aligned``: the oracle ran on the GPU's own attention-ReLU
-    decisions (helpers.decoder_att_masks), so no row is excused by the kink rule."""
+    decisions (helpers.decoder_att_masks), so no row is excused by the kink rule; the caller bounds the
+    alignment itself with ``_check_att_flips``."""
     excused = {n: _grad_check(grads[n].view_as(rraw[n]), rraw[n], "grad " + n) for n in trainable}
     kinks = set().union(*(excused.get(n, set()) for n in KINK_ROWS))
     if aligned:
@@ -69,6 +92,7 @@ def test_decoder_step_b64_matches_oracle(precision, dup):
     torch.cuda.synchronize()
     assert tuple(alphas.shape) == (B, L - 1, 196)
     am = decoder_att_masks(dup)
+    _check_att_flips(p, ref_enc, t(caps), dup, f"decoder b64 {precision} dup {dup}")
     rloss, rpreds, ralphas, rraw, _, _, _ = R.train_step(p, set(trainable), ref_enc, t(caps), [L] * B, att_masks=am)
     assert_close(loss.view(()), rloss, 1e-5, 1e-6, "loss")
     assert_close(preds, rpreds, LOGIT_RTOL, LOGIT_ATOL, "predictions")

@@ -31,8 +31,8 @@ def test_struct_layout():
     from capmi._lib import GemmProblem
     # 4 ints, 15 pointer/longlong, 2 floats + int, 10 ints -> layout checked via offsets of anchors
     assert GemmProblem.A.offset == 16
-    assert GemmProblem.in_out.offset + 8 == ctypes.sizeof(GemmProblem)
-    assert GemmProblem.in_res.offset == GemmProblem.in_shift.offset + 8
+    assert GemmProblem.in_shift.offset + 8 == ctypes.sizeof(GemmProblem)
+    assert GemmProblem.in_shift.offset == GemmProblem.in_scale.offset + 8
 
 
 def test_abi_and_errors():
@@ -99,7 +99,7 @@ def test_gemm_sk_plan_on_host():
     rc, (bm, bn, sk, generic, nt) = plan(256, flags=8, M=200704)
     assert rc == 0 and (bm, bn, generic, nt) == (256, 128, 16, 512) and sk == 0
     assert plan(256, flags=8, Cin=20)[0] == 1001  # Cin % 32 != 0
-    assert plan(64, flags=8)[1][1] == 64  # N = 64: 256 x 64 tiles (round 3)
+    assert plan(64, flags=8)[1][1] == 128  # N = 64: the 256 x 128 tile too (the 256 x 64 form was dropped, round 4)
     # CAPMI_GEMM_X3S (64, ABI 17): K = 64 only -- the 3x3 conv above is rejected; a 1x1 layer1 conv3 with
     # the BN prologue (M = 200704, N = 256) gets 64-row tiles, 256 threads, no stream-K, the persistent
     # grid (two workgroups per CU) in `generic`
