@@ -24,7 +24,7 @@ CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO, CAPMI_TILE_12
 CAPMI_TILE_128x256 = 5
 CAPMI_MAX_GROUP = 4
 CAPMI_COLSUM_GROUPS = 64
-ABI_VERSION = 19
+ABI_VERSION = 20
 CAPMI_BNB_RELU_Y, CAPMI_BNB_RELU_OUT = 0, 1
 CAPMI_BNB_MAX_SLABS = 256
 CAPMI_GEMM_BF16 = 1
@@ -50,6 +50,7 @@ class GemmProblem(ctypes.Structure):
         ("cN", c_int), ("cH", c_int), ("cW", c_int), ("cCin", c_int), ("cKH", c_int),
         ("cKW", c_int), ("cStride", c_int), ("cPad", c_int), ("cHo", c_int), ("cWo", c_int),
         ("in_scale", c_vp), ("in_shift", c_vp),
+        ("in_res", c_vp), ("in_res_scale", c_vp), ("in_res_shift", c_vp), ("in_out", c_vp),  # ABI 20
     ]
 
 

@@ -398,6 +398,7 @@ int gemm_plan(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, 
   CAPMI_REQUIRE(bmode != 2 || amode == 1, CAPMI_EINVAL);
   CAPMI_REQUIRE(tile >= CAPMI_TILE_128 && tile <= CAPMI_TILE_128_W8, CAPMI_EINVAL);
   CAPMI_REQUIRE(amode != 4 || bmode == 0, CAPMI_EINVAL);
+  for (int i = 0; i < nprob; ++i) CAPMI_REQUIRE(!has_tail(probs[i]), CAPMI_EINVAL);  // CAPMI_GEMM_X3D only
   GemmArgs& a = g.a;
   memset(&a, 0, sizeof(a));
   a.nprob = nprob;
@@ -990,6 +991,14 @@ int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gem
   // dense rows take the prologue when k is the channel (a 1x1 conv's input: lda == K)
   CAPMI_REQUIRE(amode == CAPMI_A_CONV_NHWC || (!p.in_scale && !p.in_shift) || p.lda == p.K, CAPMI_EINVAL);
   CAPMI_REQUIRE((p.in_scale == nullptr) == (p.in_shift == nullptr), CAPMI_EINVAL);
+  // fused bottleneck tail (ABI 20): dense rows with the prologue, an output, the residual BN both or neither
+  const bool tail = p.in_res != nullptr;
+  CAPMI_REQUIRE(!tail || (amode == CAPMI_A_KMAJOR && p.in_scale && p.in_out), CAPMI_EINVAL);
+  CAPMI_REQUIRE(tail || (!p.in_out && !p.in_res_scale && !p.in_res_shift), CAPMI_EINVAL);
+  CAPMI_REQUIRE((p.in_res_scale == nullptr) == (p.in_res_shift == nullptr), CAPMI_EINVAL);
+  CAPMI_REQUIRE(!tail || (aligned16(p.in_res) && aligned16(p.in_out) &&
+                          (!p.in_res_scale || (aligned16(p.in_res_scale) && aligned16(p.in_res_shift)))),
+                CAPMI_EALIGN);
   CAPMI_REQUIRE(p.a_r1 <= 0 && (p.stats == nullptr || p.c_r1 <= 0), CAPMI_EINVAL);
   CAPMI_REQUIRE(aligned16(p.A) && aligned16(p.B) && p.ldb % 8 == 0 && p.ldb >= p.K, CAPMI_EALIGN);
   CAPMI_REQUIRE(p.in_scale == nullptr || (aligned16(p.in_scale) && aligned16(p.in_shift)), CAPMI_EALIGN);
@@ -1175,6 +1184,8 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
                                 void* workspace, long long ws_bytes, void* stream) {
   GemmPlan g;
   bool sk = false;
+  // the fused bottleneck tail (ABI 20) is a CAPMI_GEMM_X3D form only
+  CAPMI_REQUIRE(prob == nullptr || flags == CAPMI_GEMM_X3D || !has_tail(*prob), CAPMI_EINVAL);
   if (flags == CAPMI_GEMM_BF16_IO) return gemm_bf16_io(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3) return gemm_x3(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3P) return gemm_x3p(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));

@@ -93,6 +93,11 @@ inline int plain_epilogue(const capmi_gemm_problem& p, int bn) {
   return ok ? (p.beta == 0.f ? 1 : 2) : 0;
 }
 
+// Host: does problem p carry any field of the fused bottleneck tail (ABI 20, CAPMI_GEMM_X3D only)?
+inline bool has_tail(const capmi_gemm_problem& p) {
+  return p.in_res || p.in_res_scale || p.in_res_shift || p.in_out;
+}
+
 // v2 kernel: A K-major dense / NHWC conv / NHWC4 conv1 / M-major (k rows), B = W[N][K] or k rows;
 // BM x BN in {128x128, 128x64, 64x64}
 int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int blocks, hipStream_t s,

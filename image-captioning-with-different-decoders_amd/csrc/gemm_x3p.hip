@@ -75,12 +75,17 @@ __device__ __forceinline__ int swz(int r) {
 // + ReLU prologue PRO), loaded to registers one k-tile ahead and split into the three swizzled LDS
 // planes after the k-tile's MFMAs; B stays LDS-DMA. It replaces gemm_x3 (both operands through
 // registers) and the separate split pass of x3p (BK = 32 only).
-template <int AMODE, bool SK, int PBK, bool ASPLIT = false, bool PRO = false, bool WIDE = false>
+// TAIL (round 4, dense rows): A is the previous bottleneck block's conv3 output y and the A element the
+// block output relu(fma(y, s, b) + r'), r' = res (TAIL 1) or fma(res, rs, rb) (TAIL 2, downsample BN) --
+// capmi_bn_add_relu's arithmetic -- which the first column tile's workgroups also store to in_out (each
+// (row, k) is staged by exactly one of them, whatever the stream-K split of the k range)
+template <int AMODE, bool SK, int PBK, bool ASPLIT = false, bool PRO = false, bool WIDE = false, int TAIL = 0>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(X3pGeo<PBK>::WPE)))
 gemm_x3p_kernel(const GemmArgs args) {
   static_assert(!ASPLIT || PBK == 32, "x3d: 32-deep k-tiles");
   static_assert(!PRO || ASPLIT, "prologue: x3d (conv, or dense rows whose k is the channel: 1x1 convs)");
   static_assert(!WIDE || (ASPLIT && PBK == 32 && AMODE == 0), "wide tiles: x3d on dense rows");
+  static_assert(!TAIL || (PRO && AMODE == 0), "fused bottleneck tail: x3d prologue on dense rows");
   using G_ = X3pGeo<PBK, WIDE>;
   constexpr int PBM = G_::BM, PBN = G_::BN;
   constexpr int JN = 64 / 16;    // 16x16x32: 16-column blocks per wave (wave tile 64 x 64)
@@ -132,6 +137,12 @@ gemm_x3p_kernel(const GemmArgs args) {
     const unsigned ss_bytes = PRO ? (unsigned)((AMODE == 2 ? cCin : P.K) * 4) : 0u;
     const auto rsc_p = rsrc_p(PRO ? (const void*)P.in_scale : P.B, ss_bytes);
     const auto rsh_p = rsrc_p(PRO ? (const void*)P.in_shift : P.B, ss_bytes);
+    // TAIL: the residual (A's layout), its BN (TAIL 2) and the block output; the output descriptor has no
+    // records outside the first column tile (its stores are dropped there)
+    const auto rr_p = rsrc_p(TAIL ? (const void*)P.in_res : P.B, TAIL ? (unsigned)(planeA * 4) : 0u);
+    const auto rrs_p = rsrc_p(TAIL == 2 ? (const void*)P.in_res_scale : P.B, TAIL == 2 ? ss_bytes : 0u);
+    const auto rrb_p = rsrc_p(TAIL == 2 ? (const void*)P.in_res_shift : P.B, TAIL == 2 ? ss_bytes : 0u);
+    const auto ro_p = rsrc_p(TAIL ? (const void*)P.in_out : P.B, TAIL && n0 == 0 ? (unsigned)(planeA * 4) : 0u);
     // this lane's two A rows (row blocks 2 wid, 2 wid + 1) and one B row (row block wid)
     // (arrays sized 2 >= NAB: a dependent bound in the nested lambda loses the host launch stub)
     unsigned a_base[2];  // dense: byte offset of (row, chunk) in plane 0; conv: pixel index of (n, 0, 0)
@@ -199,6 +210,9 @@ gemm_x3p_kernel(const GemmArgs args) {
     float4 areg[NSA];
     float4 a_sc = make_float4(1.f, 1.f, 1.f, 1.f), a_sh = make_float4(0.f, 0.f, 0.f, 0.f);
     unsigned a_msk = 0;
+    float4 rreg[TAIL ? NSA : 1];  // TAIL: residual slots, their BN, the slots' offsets (kOOBp: none)
+    float4 r_sc = make_float4(1.f, 1.f, 1.f, 1.f), r_sh = make_float4(0.f, 0.f, 0.f, 0.f);
+    unsigned o_off[TAIL ? NSA : 1];
     // conv k order (ci / 32, kh, kw, ci % 32): the taps of one 32-channel slice are consecutive
     // k-tiles, so the input rows a tile re-reads for its KH*KW taps are re-read within KH*KW k-tiles
     // (L2-resident) instead of once per full sweep over Cin; the weights are packed to match
@@ -230,6 +244,10 @@ gemm_x3p_kernel(const GemmArgs args) {
           const unsigned ch = (unsigned)((AMODE == 2 ? c_ci : k) + aq * 4) * 4u;  // dense rows: channel = k
           a_sc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsc_p, ch, 0, 0));
           a_sh = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsh_p, ch, 0, 0));
+          if (TAIL == 2) {
+            r_sc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rrs_p, ch, 0, 0));
+            r_sh = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rrb_p, ch, 0, 0));
+          }
         }
 #pragma unroll
         for (int i = 0; i < NSA; ++i) {
@@ -245,6 +263,10 @@ gemm_x3p_kernel(const GemmArgs args) {
           }
           areg[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off : kOOBp, 0, 0));
           a_msk |= (unsigned)ok << i;
+          if constexpr (TAIL != 0) {
+            rreg[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rr_p, ok ? off : kOOBp, 0, 0));
+            o_off[i] = ok ? off : kOOBp;
+          }
         }
       }
       unsigned aoff[2];
@@ -297,8 +319,14 @@ gemm_x3p_kernel(const GemmArgs args) {
 #pragma unroll
       for (int i = 0; i < NSA; ++i) {
         float4 v = ar[i];
-        if (PRO) v = make_float4(fmaxf(fmaf(v.x, sc.x, sh.x), 0.f), fmaxf(fmaf(v.y, sc.y, sh.y), 0.f),
-                                 fmaxf(fmaf(v.z, sc.z, sh.z), 0.f), fmaxf(fmaf(v.w, sc.w, sh.w), 0.f));
+        if constexpr (TAIL != 0) {  // the block output, bit for bit capmi_bn_add_relu's
+          const float4 r = TAIL == 2 ? fma4(rreg[i], r_sc, r_sh) : rreg[i];
+          v = relu4(fma4(v, sc, sh) + r);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_p, v), ro_p, o_off[i], 0, 0);
+        } else if (PRO) {
+          v = make_float4(fmaxf(fmaf(v.x, sc.x, sh.x), 0.f), fmaxf(fmaf(v.y, sc.y, sh.y), 0.f),
+                          fmaxf(fmaf(v.z, sc.z, sh.z), 0.f), fmaxf(fmaf(v.w, sc.w, sh.w), 0.f));
+        }
         if (!((msk >> i) & 1u)) v = make_float4(0.f, 0.f, 0.f, 0.f);  // padding taps: zeros AFTER the BN
         unsigned lo[3], hi[3];
         split3_pair(v.x, v.y, lo);
@@ -705,9 +733,26 @@ int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s, boo
   const dim3 g(blocks), b(PNT);
   const bool sk = a.sk_workers > 0;
   const bool pro = a.p[0].in_scale != nullptr;
+  const int tail = a.p[0].in_res == nullptr ? 0 : a.p[0].in_res_scale ? 2 : 1;
 #define X3D_GO(M, S, PR) CAPMI_KLAUNCH((gemm_x3p_kernel<M, S, 32, true, PR>), g, b, 0, s, a)
 #define X3D_GOW(S, PR) CAPMI_KLAUNCH((gemm_x3p_kernel<0, S, 32, true, PR, true>), g, b, 0, s, a)
-  if (wide) {  // 128 x 256 tiles, dense rows
+#define X3D_GOT(S, W, T) CAPMI_KLAUNCH((gemm_x3p_kernel<0, S, 32, true, true, W, T>), g, b, 0, s, a)
+  if (tail) {  // the fused bottleneck tail (dense rows, the prologue set: x3d_plan checks)
+    CAPMI_REQUIRE(amode == 0 && pro, CAPMI_EINVAL);
+    if (wide) {
+      if (tail == 2) {
+        if (sk) X3D_GOT(true, true, 2); else X3D_GOT(false, true, 2);
+      } else {
+        if (sk) X3D_GOT(true, true, 1); else X3D_GOT(false, true, 1);
+      }
+    } else {
+      if (tail == 2) {
+        if (sk) X3D_GOT(true, false, 2); else X3D_GOT(false, false, 2);
+      } else {
+        if (sk) X3D_GOT(true, false, 1); else X3D_GOT(false, false, 1);
+      }
+    }
+  } else if (wide) {  // 128 x 256 tiles, dense rows
     CAPMI_REQUIRE(amode == 0, CAPMI_EINVAL);
     if (pro) {
       if (sk) X3D_GOW(true, true); else X3D_GOW(false, true);
@@ -727,6 +772,7 @@ int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s, boo
   }
 #undef X3D_GO
 #undef X3D_GOW
+#undef X3D_GOT
   CAPMI_LAUNCH_CHECK();
   return 0;
 }
