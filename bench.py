@@ -502,12 +502,17 @@ def main():
                                 "frac": round(fam_flops / (fam_ms * 1e-3) / 1e12 / peak, 4),
                                 "conv_ms_per_step": round(fam_ms / args.steps, 3),
                                 "conv_gflop_per_image": round(per_img / 1e9, 3)},
-                "timing": timing}
+                "timing": timing,
+                # which pass gives achieved / frac: the serialized one (encoder and decoder on one
+                # stream, as the rocprofv3 kernel trace runs the bench) unless the steps themselves were eager;
+                # in_pipeline below is the same kernel with the decoder stream beside it
+                "frac_pass": "timed eager steps" if args.eager else "serialized timing pass (after the timed region)"}
         if timer_pipe is not None:
             pp = timer_pipe.result().get(key)
             if pp:
                 # the same kernel's launches inside the pipelined step (decoder kernels sharing the CUs)
-                roof["in_pipeline"] = {"avg_launch_us": round(pp[2] * 1e3 / pp[0], 2),
+                roof["in_pipeline"] = {"pass": "pipelined timing pass (two streams, as the timed step)",
+                                       "avg_launch_us": round(pp[2] * 1e3 / pp[0], 2),
                                        "achieved": round(pp[1] / (pp[2] * 1e-3) / 1e12, 3),
                                        "frac": round(pp[1] / (pp[2] * 1e-3) / 1e12 / peak, 4)}
     cpu = None

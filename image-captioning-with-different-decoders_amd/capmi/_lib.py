@@ -21,10 +21,9 @@ c_ull = ctypes.c_ulonglong
 CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_A_CONV_NHWC, CAPMI_A_CONV_NCHW, CAPMI_A_CONV_NHWC4 = 0, 1, 2, 3, 4
 CAPMI_B_NMAJOR_W, CAPMI_B_KROWS, CAPMI_B_CONV_NHWC = 0, 1, 2
 CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO, CAPMI_TILE_128_W8 = 0, 1, 2, 3, 4
-CAPMI_TILE_128x256 = 5
 CAPMI_MAX_GROUP = 4
 CAPMI_COLSUM_GROUPS = 64
-ABI_VERSION = 20
+ABI_VERSION = 22
 CAPMI_BNB_RELU_Y, CAPMI_BNB_RELU_OUT = 0, 1
 CAPMI_BNB_MAX_SLABS = 256
 CAPMI_GEMM_BF16 = 1
@@ -50,7 +49,6 @@ class GemmProblem(ctypes.Structure):
         ("cN", c_int), ("cH", c_int), ("cW", c_int), ("cCin", c_int), ("cKH", c_int),
         ("cKW", c_int), ("cStride", c_int), ("cPad", c_int), ("cHo", c_int), ("cWo", c_int),
         ("in_scale", c_vp), ("in_shift", c_vp),
-        ("in_res", c_vp), ("in_res_scale", c_vp), ("in_res_shift", c_vp), ("in_out", c_vp),  # ABI 20
     ]
 
 

@@ -40,14 +40,11 @@ def _cuda(*ts, dtype=F32):
 # --------------------------------------------------------------------------------------
 def problem(M, N, K, A, lda, B, ldb, C, ldc, *, a_r1=0, a_s2=0, c_r1=0, c_s2=0, ksplit=1,
             c_split_stride=0, bias=None, bias2=None, alpha=1.0, alpha_ptr=None, beta=0.0,
-            relu=False, stats=None, conv=None, in_scale=None, in_shift=None, in_res=None, in_res_scale=None,
-            in_res_shift=None, in_out=None):
+            relu=False, stats=None, conv=None, in_scale=None, in_shift=None):
     """Build one ``capmi_gemm_problem``. A/B/C are tensors (or views) whose data_ptr is the
     operand origin; ld* are element strides. ``conv`` = dict(N,H,W,Cin,KH,KW,stride,pad,Ho,Wo).
-    ``in_res`` / ``in_res_scale`` / ``in_res_shift`` / ``in_out``: the fused bottleneck tail of gemm_x3d on
-    dense rows (ABI 20; the block output relu(A*in_scale + in_shift + res') is the A element and is stored
-    to in_out). The problem keeps raw pointers only: the caller holds every tensor until the launch."""
-    _cuda(C, bias, bias2, stats, in_scale, in_shift, in_res, in_res_scale, in_res_shift, in_out)
+    The problem keeps raw pointers only: the caller holds every tensor until the launch."""
+    _cuda(C, bias, bias2, stats, in_scale, in_shift)
     for t_ in (A, B):  # bf16: the split planes of gemm_x3 (B) / gemm_x3p (A and B)
         _cuda(t_, dtype=torch.bfloat16 if t_ is not None and t_.dtype == torch.bfloat16 else F32)
     p = GemmProblem()
@@ -64,7 +61,6 @@ def problem(M, N, K, A, lda, B, ldb, C, ldc, *, a_r1=0, a_s2=0, c_r1=0, c_s2=0, 
         p.cKH, p.cKW, p.cStride, p.cPad = conv["KH"], conv["KW"], conv["stride"], conv["pad"]
         p.cHo, p.cWo = conv["Ho"], conv["Wo"]
     p.in_scale, p.in_shift = ptr(in_scale), ptr(in_shift)
-    p.in_res, p.in_res_scale, p.in_res_shift, p.in_out = ptr(in_res), ptr(in_res_scale), ptr(in_res_shift), ptr(in_out)
     return p
 
 
@@ -190,12 +186,11 @@ def gemm_x3p(prob, amode, workspace):
          ptr(workspace), workspace.numel() * 4, stream())
 
 
-def gemm_x3d(prob, amode, workspace, tile=CAPMI_TILE_AUTO):
+def gemm_x3d(prob, amode, workspace):
     """CAPMI_GEMM_X3D: A fp32 (dense, or the NHWC conv input with the optional BN prologue) split
-    in-kernel x B = three bf16 planes in the x3p k order (conv_weight_order_x3p + split3_bf16).
-    tile CAPMI_TILE_128x256 (5): 128 x 256 tiles on dense rows."""
+    in-kernel x B = three bf16 planes in the x3p k order (conv_weight_order_x3p + split3_bf16)."""
     _cuda(workspace, dtype=torch.int32)
-    call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, tile, CAPMI_GEMM_X3D,
+    call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3D,
          ptr(workspace), workspace.numel() * 4, stream())
 
 
@@ -241,16 +236,12 @@ def gemm_x3s_kernel_name(prob, amode):
     return f"gemm_x3s_kernel<{ncb}, {'true' if prob.in_scale else 'false'}>"
 
 
-def gemm_x3d_kernel_name(prob, amode, tile=CAPMI_TILE_AUTO):
+def gemm_x3d_kernel_name(prob, amode):
     v = [ctypes.c_int(0) for _ in range(5)]
-    call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, tile, CAPMI_GEMM_X3D,
+    call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3D,
          *[ctypes.byref(x) for x in v])
     b = lambda x: "true" if x else "false"  # noqa: E731
-    wide = v[0].value == 128
-    tail = 0 if not prob.in_res else 2 if prob.in_res_scale else 1
-    if tail:
-        return f"gemm_x3p_kernel<{amode}, {b(v[2].value)}, 32, true, true, {b(wide)}, {tail}>"
-    return f"gemm_x3p_kernel<{amode}, {b(v[2].value)}, 32, true, {b(bool(prob.in_scale))}{', true' if wide else ''}>"
+    return f"gemm_x3p_kernel<{amode}, {b(v[2].value)}, 32, true, {b(bool(prob.in_scale))}>"
 
 
 def gemm_x3p_kernel_name(prob, amode):

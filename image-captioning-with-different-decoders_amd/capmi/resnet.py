@@ -20,7 +20,7 @@ import torch.nn as nn
 
 from . import kernels as K
 from ._lib import CAPMI_A_CONV_NHWC, CAPMI_A_CONV_NHWC4, CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_B_CONV_NHWC
-from ._lib import CAPMI_B_KROWS, CAPMI_B_NMAJOR_W, CAPMI_GEMM_BF16, CAPMI_GEMM_SPLIT3, CAPMI_TILE_128x256
+from ._lib import CAPMI_B_KROWS, CAPMI_B_NMAJOR_W, CAPMI_GEMM_BF16, CAPMI_GEMM_SPLIT3
 
 AK, AMM, AC = CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_A_CONV_NHWC
 BW, BKR, BCONV = CAPMI_B_NMAJOR_W, CAPMI_B_KROWS, CAPMI_B_CONV_NHWC
@@ -147,19 +147,6 @@ _X3_SMALLK = int(os.environ.get("CAPMI_X3_SMALLK", "0"))
 _X3D = os.environ.get("CAPMI_X3D", "1") != "0"
 # x3 mode: layer1's K = 64 1x1 convs on the short-k streaming kernel (CAPMI_X3S=0: off, A/B)
 _X3S = os.environ.get("CAPMI_X3S", "1") != "0"
-# x3 mode (round 4): a bottleneck tail relu(bn3(y3) + res') followed by a block of the same stage whose conv1
-# has 128 or 256 outputs (layer2 / layer3) is computed in that conv1's A staging -- x3d with one column tile
-# (256 x 128, or 128 x 256 for N = 256), which also stores the block output -- instead of the separate
-# capmi_bn_add_relu pass (CAPMI_X3_TAIL=0: off, A/B)
-_X3_TAIL = os.environ.get("CAPMI_X3_TAIL", "1") != "0"
-
-
-class _Tail:
-    """A bottleneck tail out = relu(y*s + b + res') with res' = res*rs + rb (downsample BN) or res, deferred
-    to the next block's conv1 (EncoderRunner._conv1_tail)."""
-
-    def __init__(self, y, s, b, res, out, rs=None, rb=None):
-        self.y, self.s, self.b, self.res, self.out, self.rs, self.rb = y, s, b, res, out, rs, rb
 
 class EncoderRunner:
     """Launch plan for the frozen ResNet-101 conv stack (children()[:-2] of torchvision's
@@ -358,32 +345,6 @@ class EncoderRunner:
         del stats
         return Ho, Wo, rows
 
-    def _tail_ok(self, conv, rows):
-        """Can ``conv`` (a block's conv1, 1x1 / stride 1 on the block input) take the previous block's tail
-        in its A staging (x3d TAIL form, one column tile)?"""
-        co, ci, kh, _ = conv.weight.shape
-        return (self.x3 and _X3_TAIL and _X3D and kh == 1 and conv.stride[0] == 1 and co in (128, 256)
-                and ci % 32 == 0 and rows * ci * 4 < (1 << 31))
-
-    def _conv1_tail(self, tag, conv, out, N, H, W, train, t):
-        """conv1 (1x1) of a block whose input is the previous block's deferred tail ``t``: the gemm_x3d TAIL
-        form computes the input relu(y3*s3 + b3 + res') in its A staging and stores it to ``t.out`` (the block
-        output: this block's residual) -- bit-identical to capmi_bn_add_relu + the plain x3d conv
-        (tests/test_gpu_x3.py::test_x3d_fused_tail_bit_identical)."""
-        co, ci = conv.weight.shape[:2]
-        rows = N * H * W
-        w3 = self._packed_x3(conv, tap_inner=True)
-        prob = K.problem(rows, co, ci, t.y, ci, w3, ci, out, co, stats=self._ws["stats"] if train else None,
-                         in_scale=t.s, in_shift=t.b, in_res=t.res, in_res_scale=t.rs, in_res_shift=t.rb,
-                         in_out=t.out)
-        tile = CAPMI_TILE_128x256 if co > 128 else K.TILE_AUTO
-        launch = lambda: K.gemm_x3d(prob, AK, self._ws["sk"], tile=tile)  # noqa: E731
-        if self.conv_hook is not None:
-            self.conv_hook(tag, 2.0 * rows * co * ci, launch, K.gemm_x3d_kernel_name(prob, AK, tile))
-        else:
-            launch()
-        return H, W, rows
-
     def _packed_x3(self, conv, tap_inner=False):
         """[3][Cout][K] bf16 split of the packed fp32 weight (B operand of gemm_x3; with ``tap_inner``
         in gemm_x3p's conv k order), refreshed when the weight tensor changes (FineTuneRunner drops
@@ -529,40 +490,27 @@ class EncoderRunner:
         bns = []
         direct = out_hw is None and out is not None
         n4 = len(net.layer4)
-        tail = None  # the previous block's deferred tail (its output x not yet written)
         for li in range(1, 5):
             layer = getattr(net, f"layer{li}")
             for bi, blk in enumerate(layer):
                 if direct and li == 4 and bi == n4 - 1:
                     xo = out  # the last block's output is the result
                 tag = f"layer{li}.{bi}"
-                if tail is not None:  # (only a block followed by one of its own stage defers: no downsample)
-                    _, _, r1 = self._conv1_tail(tag + ".conv1", blk.conv1, ws["y1"], N, H, W, train, tail)
-                    tail = None
-                else:
-                    _, _, r1 = self._conv(tag + ".conv1", x, blk.conv1, ws["y1"], N, H, W, train)
+                _, _, r1 = self._conv(tag + ".conv1", x, blk.conv1, ws["y1"], N, H, W, train)
                 ss1 = self._bn(ws, blk.bn1, r1, train)
                 H2, W2, r2 = self._conv(tag + ".conv2", ws["y1"], blk.conv2, ws["y2"], N, H, W, train, in_ss=ss1)
                 ss2 = self._bn(ws, blk.bn2, r2, train)
                 _, _, r3 = self._conv(tag + ".conv3", ws["y2"], blk.conv3, ws["y3"], N, H2, W2, train, in_ss=ss2)
                 Cout = blk.conv3.out_channels
-                # this block's tail rides in the next block's conv1 when that conv can take it
-                defer = bi + 1 < len(layer) and self._tail_ok(layer[bi + 1].conv1, r3)
                 if blk.downsample is not None:
                     s3, b3 = self._bn(ws, blk.bn3, r3, train)  # (the downsample conv reuses the stats buffer)
                     self._conv(tag + ".downsample", x, blk.downsample[0], ws["yd"], N, H, W, train)
                     sd, bd = self._bn(ws, blk.downsample[1], r3, train)
-                    if defer:
-                        tail = _Tail(ws["y3"], s3, b3, ws["yd"], xo, rs=sd, rb=bd)
-                    else:
-                        K.bn_add_relu(ws["y3"], s3, b3, ws["yd"], xo, r3, Cout, res_scale=sd, res_shift=bd)
+                    K.bn_add_relu(ws["y3"], s3, b3, ws["yd"], xo, r3, Cout, res_scale=sd, res_shift=bd)
                     bns.append(blk.downsample[1])
                 else:
                     s3, b3 = self._bn(ws, blk.bn3, r3, train)
-                    if defer:
-                        tail = _Tail(ws["y3"], s3, b3, x, xo)
-                    else:
-                        K.bn_add_relu(ws["y3"], s3, b3, x, xo, r3, Cout)
+                    K.bn_add_relu(ws["y3"], s3, b3, x, xo, r3, Cout)
                 bns += [blk.bn1, blk.bn2, blk.bn3]
                 x, xo = xo, x
                 H, W, Cx = H2, W2, Cout

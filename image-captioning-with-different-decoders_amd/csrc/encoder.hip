@@ -8,6 +8,7 @@
 // models/attention.py:374 (encoder.train()).
 #include <cstdlib>
 
+#include "bn_final.h"
 #include "common.h"
 
 __global__ void conv_weight_pack_kernel(const float* __restrict__ w, int Cout, int Cin, int KH,
@@ -70,144 +71,21 @@ extern "C" int capmi_image_nhwc4(const float* in, int N, int C, int H, int W, fl
 }
 
 // ---------------------------------------------------------------------------------
-// BN finalize: G slice-groups x 64 channels reduce the GEMM's per-slice (Σ, Σx²) in fp64,
-// the last group of each channel block turns them into scale/shift and running stats.
+// BN finalize (stand-alone launch): one 512-thread workgroup per 8 channels, the canonical fp64 order of
+// bn_final.h -- the same sums, bit for bit, as the finalize fused into the x3 conv GEMMs (round 4; it
+// replaced the slice-count-dependent direct / two-level kernels of rounds 1-3)
 // ---------------------------------------------------------------------------------
-constexpr int BNF_MAXG = 32;
-
-// One launch: block (cb, g) reduces slice group g of channels [64cb, 64cb+64) to fp64 (Σ, Σx²),
-// publishes it with write-through (sc1) 8-B stores and bumps the channel block's arrival
-// counter; the block whose add returns G-1 is the last one and finalizes those 64 channels,
-// summing the G partials in group order (deterministic) behind one agent-scope acquire, then
-// re-arms the counter to 0. The counters live in the caller's work buffer, zeroed once.
-__global__ void __launch_bounds__(1024)
-bn_finalize_kernel(const float* __restrict__ stats, int tiles, int C, int per_g,
-                   unsigned long long* part, int* counters, long long count,
-                   const float* __restrict__ gamma, const float* __restrict__ beta,
-                   float* running_mean, float* running_var, float momentum, float eps,
-                   float* __restrict__ scale, float* __restrict__ shift, float* save_mean,
-                   float* save_var) {
-  // 1024 threads = 16 slice rows x 64 channels: 8 loads in flight per lane, so a group's slices
-  // take one or two memory round trips
-  __shared__ double rs[16][64], rq[16][64];
-  __shared__ int last;
-  const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  const int G = gridDim.y;
-  const int t0 = blockIdx.y * per_g, t1 = min(tiles, t0 + per_g);
-  double s = 0.0, q = 0.0;
-  if (c < C) {
-    for (int t = t0 + tl; t < t1; t += 128) {
-      float2 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int tt = t + 16 * u;
-        v[u] = tt < t1 ? *reinterpret_cast<const float2*>(stats + ((long long)tt * C + c) * 2)
-                       : make_float2(0.f, 0.f);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        s += v[u].x;
-        q += v[u].y;
-      }
-    }
-  }
-  rs[tl][cl] = s;
-  rq[tl][cl] = q;
-  __syncthreads();
-  if (tl == 0) {  // wave 0 publishes the group's partial and takes the arrival ticket
-    if (c < C) {
-      s = 0.0;
-      q = 0.0;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        s += rs[r][cl];
-        q += rq[r][cl];
-      }
-      unsigned long long* p = part + ((long long)blockIdx.y * C + c) * 2;
-      __hip_atomic_store(p, (unsigned long long)__double_as_longlong(s), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p + 1, (unsigned long long)__double_as_longlong(q), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int prev = 0;
-    if (cl == 0) prev = __hip_atomic_fetch_add(counters + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    prev = __shfl(prev, 0, 64);
-    if (cl == 0) last = prev == G - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  // the last group: one agent-scope acquire per wave, then every wave sums its share of the G
-  // partials (fixed order: group g = tl + 16i, then wave order)
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  s = 0.0;
-  q = 0.0;
-  if (c < C) {
-    const double2* pd = reinterpret_cast<const double2*>(part);
-    for (int g = tl; g < G; g += 16) {
-      const double2 v = pd[(long long)g * C + c];
-      s += v.x;
-      q += v.y;
-    }
-  }
-  __syncthreads();  // rs / rq reused
-  rs[tl][cl] = s;
-  rq[tl][cl] = q;
-  __syncthreads();
-  if (tl != 0) return;
-  if (c < C) {
-    s = 0.0;
-    q = 0.0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s += rs[r][cl];
-      q += rq[r][cl];
-    }
-    const double n = (double)count;
-    const double mean = s / n;
-    double var = q / n - mean * mean;
-    if (var < 0) var = 0;
-    const double inv = 1.0 / sqrt(var + (double)eps);
-    const float sc = (float)((double)gamma[c] * inv);
-    scale[c] = sc;
-    shift[c] = (float)((double)beta[c] - mean * (double)sc);
-    if (save_mean) save_mean[c] = (float)mean;
-    if (save_var) save_var[c] = (float)var;
-    if (running_mean) {
-      const double unb = count > 1 ? var * n / (n - 1.0) : var;
-      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-      running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
-    }
-  }
-  if (cl == 0) __hip_atomic_store(counters + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__global__ void __launch_bounds__(512) bn_finalize_kernel(const float* __restrict__ stats, int tiles, int C,
+                                                          BnFinArgs f) {
+  __shared__ double2 scratch[64 * BNF_CG];
+  bnf_group<512>(f, stats, tiles, C, blockIdx.x, scratch);
 }
 
-// Direct finalize: each 1024-thread block reads every slice of its channels itself and finalizes --
-// no partials, no arrival counter, one launch latency. Block width by slice count (batch 64):
-// <= 64 slices (layer4) 64 channels x 8 loads in flight; 65-256 (layer3) 16 channels x 4 loads;
-// more (layer1/2: 784 / 3136 slices) 4 channels x 16 loads, one round of loads up to 4096 slices
-// (it replaced the two-level group kernel below: 7-8 -> 4.4-5.3 us per call, tools/bnf_ab.sh).
-constexpr int BNF_DIRECT = 256;
-// CAPMI_BNF_NARROW=0: always the 64-channel form (A/B measurement)
-bool bnf_narrow() {
-  static const bool on = [] {
-    const char* e = getenv("CAPMI_BNF_NARROW");
-    return !(e && e[0] == '0' && e[1] == 0);
-  }();
-  return on;
-}
-
-// CW channels per workgroup: a wave reads 64 / CW slice rows of CW channels per load. CW = 16
-// spreads a layer3-sized reduction (196 slices) over 4x more CUs in one round of loads; CW = 64
-// (fewer, wider workgroups) is the faster form for layer4's 49 slices.
+// (temporary A/B, round 4) the round-3 direct finalize: each 1024-thread block reads every slice of its CW
+// channels (CW = 64 / 16 / 4 by slice count) -- CAPMI_BNF_OLD=1
 template <int CW, int U>
 __global__ void __launch_bounds__(1024)
-bn_finalize_direct_kernel(const float* __restrict__ stats, int tiles, int C, long long count,
-                          const float* __restrict__ gamma, const float* __restrict__ beta, float* running_mean,
-                          float* running_var, float momentum, float eps, float* __restrict__ scale,
-                          float* __restrict__ shift, float* save_mean, float* save_var) {
+bn_finalize_direct_kernel(const float* __restrict__ stats, int tiles, int C, BnFinArgs f) {
   constexpr int TS = 64 / CW, ROWS = 16 * TS;
   __shared__ double rs[16][CW], rq[16][CW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -231,7 +109,7 @@ bn_finalize_direct_kernel(const float* __restrict__ stats, int tiles, int C, lon
     }
   }
 #pragma unroll
-  for (int o = CW; o < 64; o <<= 1) {  // the TS slice lanes of a channel, fixed order
+  for (int o = CW; o < 64; o <<= 1) {
     s += __shfl_xor(s, o);
     q += __shfl_xor(q, o);
   }
@@ -248,21 +126,15 @@ bn_finalize_direct_kernel(const float* __restrict__ stats, int tiles, int C, lon
     s += rs[r][cl];
     q += rq[r][cl];
   }
-  const double n = (double)count;
-  const double mean = s / n;
-  double var = q / n - mean * mean;
-  if (var < 0) var = 0;
-  const double inv = 1.0 / sqrt(var + (double)eps);
-  const float sc = (float)((double)gamma[c] * inv);
-  scale[c] = sc;
-  shift[c] = (float)((double)beta[c] - mean * (double)sc);
-  if (save_mean) save_mean[c] = (float)mean;
-  if (save_var) save_var[c] = (float)var;
-  if (running_mean) {
-    const double unb = count > 1 ? var * n / (n - 1.0) : var;
-    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
-  }
+  bnf_apply(f, c, s, q);
+}
+
+bool bnf_old() {
+  static const bool on = [] {
+    const char* e = getenv("CAPMI_BNF_OLD");
+    return e && e[0] == '1';
+  }();
+  return on;
 }
 
 extern "C" int capmi_bn_finalize(const float* stats, int tiles, int C, long long count,
@@ -275,35 +147,21 @@ extern "C" int capmi_bn_finalize(const float* stats, int tiles, int C, long long
   CAPMI_REQUIRE((running_mean == nullptr) == (running_var == nullptr), CAPMI_EINVAL);
   CAPMI_REQUIRE(((uintptr_t)stats & 7) == 0 && ((uintptr_t)work & 15) == 0, CAPMI_EALIGN);
   CAPMI_REQUIRE(C <= 8192, CAPMI_ERANGE);
-  hipStream_t st = as_stream(stream);
-#define CAPMI_BNF_DIRECT(CW, U)                                                                            \
-  hipLaunchKernelGGL((bn_finalize_direct_kernel<CW, U>), dim3(cdiv(C, CW)), dim3(1024), 0, st, stats, tiles, C, \
-                     count, gamma, beta, running_mean, running_var, momentum, eps, scale, shift, save_mean,      \
-                     save_var)
-  if (tiles <= 64 || !bnf_narrow()) {
-    if (tiles <= BNF_DIRECT) {
-      CAPMI_BNF_DIRECT(64, 8);
-      CAPMI_LAUNCH_CHECK();
-      return 0;
-    }
-  } else {
-    if (tiles <= BNF_DIRECT)
-      CAPMI_BNF_DIRECT(16, 4);
+  const BnFinArgs f{gamma, beta, running_mean, running_var, scale, shift, save_mean, save_var, momentum, eps, count};
+  if (bnf_old()) {
+    if (tiles <= 64)
+      hipLaunchKernelGGL((bn_finalize_direct_kernel<64, 8>), dim3(cdiv(C, 64)), dim3(1024), 0, as_stream(stream), stats,
+                         tiles, C, f);
+    else if (tiles <= 256)
+      hipLaunchKernelGGL((bn_finalize_direct_kernel<16, 4>), dim3(cdiv(C, 16)), dim3(1024), 0, as_stream(stream), stats,
+                         tiles, C, f);
     else
-      CAPMI_BNF_DIRECT(4, 16);  // one round of loads up to 4096 slices, no partials or counters
+      hipLaunchKernelGGL((bn_finalize_direct_kernel<4, 16>), dim3(cdiv(C, 4)), dim3(1024), 0, as_stream(stream), stats,
+                         tiles, C, f);
     CAPMI_LAUNCH_CHECK();
     return 0;
   }
-#undef CAPMI_BNF_DIRECT
-  const int G = std::min(BNF_MAXG, std::max(1, (tiles + 127) / 128));
-  const int per_g = (tiles + G - 1) / G;
-  // [0, 64 doubles): the arrival counters (one int per 64-channel block, fixed place whatever
-  // C is, so BN layers of different widths can share one zeroed work buffer); then partials
-  int* counters = static_cast<int*>(work);
-  unsigned long long* part = static_cast<unsigned long long*>(work) + 64;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64), G), dim3(1024), 0, as_stream(stream), stats,
-                     tiles, C, per_g, part, counters, count, gamma, beta, running_mean, running_var,
-                     momentum, eps, scale, shift, save_mean, save_var);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, BNF_CG)), dim3(512), 0, as_stream(stream), stats, tiles, C, f);
   CAPMI_LAUNCH_CHECK();
   return 0;
 }

@@ -398,7 +398,6 @@ int gemm_plan(const capmi_gemm_problem* probs, int nprob, int amode, int bmode, 
   CAPMI_REQUIRE(bmode != 2 || amode == 1, CAPMI_EINVAL);
   CAPMI_REQUIRE(tile >= CAPMI_TILE_128 && tile <= CAPMI_TILE_128_W8, CAPMI_EINVAL);
   CAPMI_REQUIRE(amode != 4 || bmode == 0, CAPMI_EINVAL);
-  for (int i = 0; i < nprob; ++i) CAPMI_REQUIRE(!has_tail(probs[i]), CAPMI_EINVAL);  // CAPMI_GEMM_X3D only
   GemmArgs& a = g.a;
   memset(&a, 0, sizeof(a));
   a.nprob = nprob;
@@ -688,8 +687,7 @@ int x3_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gemm
             long long& total);
 int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total,
              int& bk);
-int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, GemmArgs& a, bool& sk, long long& total,
-             bool& wide);
+int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total);
 int x3s_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long& lda, int& tiles, int& grid);
 int x3w_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long ws_floats, GemmArgs& a, int& S,
              long long& tiles);
@@ -715,12 +713,11 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
   if (flags == CAPMI_GEMM_X3D) {
     GemmArgs a;
     long long total = 0;
-    bool wide = false;
-    const int rc = x3d_plan(prob, amode, bmode, tile, a, sk, total, wide);
+    const int rc = x3d_plan(prob, amode, bmode, a, sk, total);
     if (rc) return rc;
     if (threads) *threads = 512;
-    if (bm) *bm = wide ? 128 : 256;
-    if (bn) *bn = wide ? 256 : 128;
+    if (bm) *bm = 256;
+    if (bn) *bn = 128;
     if (stream_k) *stream_k = sk ? 1 : 0;
     if (generic) *generic = 32;
     return 0;
@@ -982,8 +979,7 @@ int gemm_x3p(const capmi_gemm_problem* prob, int amode, int bmode, void* workspa
 // CAPMI_GEMM_X3D: fp32 A (+ BN prologue for convs) split in-kernel x three-plane B in the x3p k order
 // (gemm_x3p.hip, ASPLIT): 256x128 tiles, 512 threads, k-tiles of 32, one workgroup per CU, stream-K
 // when the tiles under-fill the chip
-int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, GemmArgs& a, bool& sk, long long& total,
-             bool& wide) {
+int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total) {
   CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
   const capmi_gemm_problem& p = *prob;
   CAPMI_REQUIRE(bmode == CAPMI_B_NMAJOR_W && (amode == CAPMI_A_KMAJOR || amode == CAPMI_A_CONV_NHWC), CAPMI_EINVAL);
@@ -991,14 +987,6 @@ int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gem
   // dense rows take the prologue when k is the channel (a 1x1 conv's input: lda == K)
   CAPMI_REQUIRE(amode == CAPMI_A_CONV_NHWC || (!p.in_scale && !p.in_shift) || p.lda == p.K, CAPMI_EINVAL);
   CAPMI_REQUIRE((p.in_scale == nullptr) == (p.in_shift == nullptr), CAPMI_EINVAL);
-  // fused bottleneck tail (ABI 20): dense rows with the prologue, an output, the residual BN both or neither
-  const bool tail = p.in_res != nullptr;
-  CAPMI_REQUIRE(!tail || (amode == CAPMI_A_KMAJOR && p.in_scale && p.in_out), CAPMI_EINVAL);
-  CAPMI_REQUIRE(tail || (!p.in_out && !p.in_res_scale && !p.in_res_shift), CAPMI_EINVAL);
-  CAPMI_REQUIRE((p.in_res_scale == nullptr) == (p.in_res_shift == nullptr), CAPMI_EINVAL);
-  CAPMI_REQUIRE(!tail || (aligned16(p.in_res) && aligned16(p.in_out) &&
-                          (!p.in_res_scale || (aligned16(p.in_res_scale) && aligned16(p.in_res_shift)))),
-                CAPMI_EALIGN);
   CAPMI_REQUIRE(p.a_r1 <= 0 && (p.stats == nullptr || p.c_r1 <= 0), CAPMI_EINVAL);
   CAPMI_REQUIRE(aligned16(p.A) && aligned16(p.B) && p.ldb % 8 == 0 && p.ldb >= p.K, CAPMI_EALIGN);
   CAPMI_REQUIRE(p.in_scale == nullptr || (aligned16(p.in_scale) && aligned16(p.in_shift)), CAPMI_EALIGN);
@@ -1013,12 +1001,9 @@ int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gem
   memset(&a, 0, sizeof(a));
   a.nprob = 1;
   a.p[0] = p;
-  // CAPMI_TILE_128x256 (round 4): 128 x 256 tiles for dense rows, one column tile when N <= 256
-  wide = tile == CAPMI_TILE_128x256 && amode == CAPMI_A_KMAJOR;
-  const int bm = wide ? 128 : 256, bn = wide ? 256 : 128;
-  a.tiles_m[0] = (int)cdiv(p.M, bm);
-  a.tiles_n[0] = (int)cdiv(p.N, bn);
-  a.plain_epi = plain_epilogue(p, bn);
+  a.tiles_m[0] = (int)cdiv(p.M, 256);
+  a.tiles_n[0] = (int)cdiv(p.N, 128);
+  a.plain_epi = plain_epilogue(p, 128);
   total = (long long)a.tiles_m[0] * a.tiles_n[0];
   a.tiles_begin[1] = (int)total;
   const long long slots = sk_cus();
@@ -1028,16 +1013,15 @@ int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, Gem
   return 0;
 }
 
-int gemm_x3d(const capmi_gemm_problem* prob, int amode, int bmode, int tile, void* workspace, long long ws_bytes,
+int gemm_x3d(const capmi_gemm_problem* prob, int amode, int bmode, void* workspace, long long ws_bytes,
              hipStream_t s) {
   GemmArgs a;
   bool sk = false;
   long long total = 0;
-  bool wide = false;
-  const int rc = x3d_plan(prob, amode, bmode, tile, a, sk, total, wide);
+  const int rc = x3d_plan(prob, amode, bmode, a, sk, total);
   if (rc) return rc;
   if (prob->M == 0) return 0;
-  if (!sk || workspace == nullptr) return gemm_x3d_launch(a, amode, (int)total, s, wide);
+  if (!sk || workspace == nullptr) return gemm_x3d_launch(a, amode, (int)total, s);
   CAPMI_REQUIRE(aligned16(workspace), CAPMI_EINVAL);
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
   const int cus = cu_count();
@@ -1049,7 +1033,7 @@ int gemm_x3d(const capmi_gemm_problem* prob, int amode, int bmode, int tile, voi
   a.sk_groups = sk_xcd_groups() && a.sk_workers % 8 == 0 && total >= 64 ? 8 : 1;
   a.sk_flags = static_cast<int*>(workspace);
   a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
-  return gemm_x3d_launch(a, amode, a.sk_workers, s, wide);
+  return gemm_x3d_launch(a, amode, a.sk_workers, s);
 }
 
 // CAPMI_GEMM_X3W (gemm_x3w.hip): conv weight gradient dW = dY^T . im2col(X), both operands fp32 k rows (pixels),
@@ -1070,6 +1054,8 @@ int x3w_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long ws_
   if (bmode == CAPMI_B_CONV_NHWC) {
     CAPMI_REQUIRE(p.cCin % 4 == 0 && p.N == p.cKH * p.cKW * p.cCin && p.K == p.cN * p.cHo * p.cWo, CAPMI_EINVAL);
     CAPMI_REQUIRE((long long)p.cN * p.cH * p.cW * p.cCin * 4 < (1LL << 31), CAPMI_ERANGE);
+    // the kernel advances each pixel walk by a 32-pixel k-tile with at most two wraps of the output row
+    CAPMI_REQUIRE(p.cWo > 0 && p.cHo > 0 && 32 / p.cWo + 1 < 2 * p.cHo, CAPMI_ERANGE);
   } else {
     CAPMI_REQUIRE(p.ldb % 4 == 0 && p.ldb >= p.N, CAPMI_EALIGN);
     CAPMI_REQUIRE((long long)p.K * p.ldb * 4 < (1LL << 31), CAPMI_ERANGE);
@@ -1184,12 +1170,10 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
                                 void* workspace, long long ws_bytes, void* stream) {
   GemmPlan g;
   bool sk = false;
-  // the fused bottleneck tail (ABI 20) is a CAPMI_GEMM_X3D form only
-  CAPMI_REQUIRE(prob == nullptr || flags == CAPMI_GEMM_X3D || !has_tail(*prob), CAPMI_EINVAL);
   if (flags == CAPMI_GEMM_BF16_IO) return gemm_bf16_io(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3) return gemm_x3(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3P) return gemm_x3p(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
-  if (flags == CAPMI_GEMM_X3D) return gemm_x3d(prob, amode, bmode, tile, workspace, ws_bytes, as_stream(stream));
+  if (flags == CAPMI_GEMM_X3D) return gemm_x3d(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3S) return gemm_x3s(prob, amode, bmode, as_stream(stream));
   if (flags == CAPMI_GEMM_X3W) return gemm_x3w(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
   int terms = flag_terms(flags);

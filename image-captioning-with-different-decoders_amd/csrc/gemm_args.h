@@ -93,11 +93,6 @@ inline int plain_epilogue(const capmi_gemm_problem& p, int bn) {
   return ok ? (p.beta == 0.f ? 1 : 2) : 0;
 }
 
-// Host: does problem p carry any field of the fused bottleneck tail (ABI 20, CAPMI_GEMM_X3D only)?
-inline bool has_tail(const capmi_gemm_problem& p) {
-  return p.in_res || p.in_res_scale || p.in_res_shift || p.in_out;
-}
-
 // v2 kernel: A K-major dense / NHWC conv / NHWC4 conv1 / M-major (k rows), B = W[N][K] or k rows;
 // BM x BN in {128x128, 128x64, 64x64}
 int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int blocks, hipStream_t s,
@@ -112,8 +107,7 @@ int gemm_x3_launch(const GemmArgs& a, int amode, int bn, int blocks, hipStream_t
 // of GemmArgs::sk_nkt for it
 int gemm_x3p_launch(const GemmArgs& a, int amode, int bk, int blocks, hipStream_t s);
 // x3p with A fp32 split in-kernel ("x3d": register-staged A + optional conv BN prologue, LDS-DMA B)
-// wide: 128 x 256 tiles (dense rows)
-int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s, bool wide = false);
+int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s);
 // short-k streaming x3 GEMM (gemm_x3s.hip): K = 64, N in {64, 128, 256}, dense rows of lda floats
 // (optional BN prologue), store-only epilogue; persistent grid over 64-row tiles
 int gemm_x3s_launch(const capmi_gemm_problem& p, long long lda, int tiles, int grid, hipStream_t s);

@@ -476,9 +476,9 @@ gemm_x3_kernel(const GemmArgs args) {
   }
   const long long ub = grp * T / ngrp * nkt, U = ((grp + 1) * T / ngrp) * nkt - ub;
   const long long u0 = ub + w * U / G, u1 = ub + (w + 1) * U / G;
-  if (u0 >= u1) return;
   constexpr int PART = BM * BN;
   int* flags = args.sk_flags;
+  if (u0 >= u1) return;
   for (long long t = (u1 - 1) / nkt; t >= u0 / nkt; --t) {
     const long long tb = t * nkt;
     const int ks = (int)(max(u0, tb) - tb), ke = (int)(min(u1, tb + nkt) - tb);

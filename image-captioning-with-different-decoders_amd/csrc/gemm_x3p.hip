@@ -36,11 +36,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_p(const void* p, unsigned
 
 // BK = 32: 72 KiB per LDS buffer, one workgroup per CU; BK = 16: 36 KiB, two workgroups per CU (their
 // barriers and DMA waits fall at different times, so one's MFMAs cover the other's stalls)
-// tile: 256 x 128 (M x N), or WIDE 128 x 256 (round 4: a 1x1 conv whose N fits one column tile stages each
-// A element once)
-template <int PBK, bool WIDE = false>
+// tile: 256 x 128 (M x N)
+template <int PBK>
 struct X3pGeo {
-  static constexpr int BM = WIDE ? 128 : 256, BN = WIDE ? 256 : 128;
+  static constexpr int BM = 256, BN = 128;
   static constexpr int PROWB = PBK * 2;             // bytes per LDS row
   static constexpr int CPR = PBK / 8;               // 16-B chunks per row
   static constexpr int RPB = 1024 / PROWB;          // rows per 1 KiB LDS-DMA block (16 or 32)
@@ -49,7 +48,7 @@ struct X3pGeo {
   static constexpr int PB_BYTES = 3 * BN * PROWB;
   static constexpr int PBUF = PA_BYTES + PB_BYTES;  // 72 / 36 KiB per buffer
   static constexpr int NAB = BM / RPB / 8;          // A row blocks per wave (2 / 1)
-  static constexpr int NBB = BN / RPB;              // B row blocks (8 / 4 / 16): waves 0 .. NBB-1, or 2 per wave
+  static constexpr int NBB = BN / RPB;              // B row blocks (8 / 4): waves 0 .. NBB-1
   static constexpr int WPE = PBK == 16 ? 4 : 2;     // waves per SIMD: two workgroups per CU at BK = 16
 };
 
@@ -75,18 +74,12 @@ __device__ __forceinline__ int swz(int r) {
 // + ReLU prologue PRO), loaded to registers one k-tile ahead and split into the three swizzled LDS
 // planes after the k-tile's MFMAs; B stays LDS-DMA. It replaces gemm_x3 (both operands through
 // registers) and the separate split pass of x3p (BK = 32 only).
-// TAIL (round 4, dense rows): A is the previous bottleneck block's conv3 output y and the A element the
-// block output relu(fma(y, s, b) + r'), r' = res (TAIL 1) or fma(res, rs, rb) (TAIL 2, downsample BN) --
-// capmi_bn_add_relu's arithmetic -- which the first column tile's workgroups also store to in_out (each
-// (row, k) is staged by exactly one of them, whatever the stream-K split of the k range)
-template <int AMODE, bool SK, int PBK, bool ASPLIT = false, bool PRO = false, bool WIDE = false, int TAIL = 0>
+template <int AMODE, bool SK, int PBK, bool ASPLIT = false, bool PRO = false>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(X3pGeo<PBK>::WPE)))
 gemm_x3p_kernel(const GemmArgs args) {
   static_assert(!ASPLIT || PBK == 32, "x3d: 32-deep k-tiles");
   static_assert(!PRO || ASPLIT, "prologue: x3d (conv, or dense rows whose k is the channel: 1x1 convs)");
-  static_assert(!WIDE || (ASPLIT && PBK == 32 && AMODE == 0), "wide tiles: x3d on dense rows");
-  static_assert(!TAIL || (PRO && AMODE == 0), "fused bottleneck tail: x3d prologue on dense rows");
-  using G_ = X3pGeo<PBK, WIDE>;
+  using G_ = X3pGeo<PBK>;
   constexpr int PBM = G_::BM, PBN = G_::BN;
   constexpr int JN = 64 / 16;    // 16x16x32: 16-column blocks per wave (wave tile 64 x 64)
   constexpr int JN32 = 64 / 32;  // 32x32x16: 32-column blocks per wave
@@ -96,8 +89,7 @@ gemm_x3p_kernel(const GemmArgs args) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases in SGPRs
-  // waves as 4 x 2 (256 x 128) or 2 x 4 (WIDE 128 x 256), wave tile 64 x 64
-  const int wm0 = (WIDE ? wid >> 2 : wid >> 1) * 64, wn0 = (WIDE ? wid & 3 : wid & 1) * 64;
+  const int wm0 = (wid >> 1) * 64, wn0 = (wid & 1) * 64;  // waves as 4 x 2, wave tile 64 x 64
   const int lr = lane & 31, lh = lane >> 5;
   // DMA lane geometry: row lane / CPR of an RPB-row block, slot lane % CPR
   const int drow = lane / CPR, dslot = lane % CPR;
@@ -137,12 +129,6 @@ gemm_x3p_kernel(const GemmArgs args) {
     const unsigned ss_bytes = PRO ? (unsigned)((AMODE == 2 ? cCin : P.K) * 4) : 0u;
     const auto rsc_p = rsrc_p(PRO ? (const void*)P.in_scale : P.B, ss_bytes);
     const auto rsh_p = rsrc_p(PRO ? (const void*)P.in_shift : P.B, ss_bytes);
-    // TAIL: the residual (A's layout), its BN (TAIL 2) and the block output; the output descriptor has no
-    // records outside the first column tile (its stores are dropped there)
-    const auto rr_p = rsrc_p(TAIL ? (const void*)P.in_res : P.B, TAIL ? (unsigned)(planeA * 4) : 0u);
-    const auto rrs_p = rsrc_p(TAIL == 2 ? (const void*)P.in_res_scale : P.B, TAIL == 2 ? ss_bytes : 0u);
-    const auto rrb_p = rsrc_p(TAIL == 2 ? (const void*)P.in_res_shift : P.B, TAIL == 2 ? ss_bytes : 0u);
-    const auto ro_p = rsrc_p(TAIL ? (const void*)P.in_out : P.B, TAIL && n0 == 0 ? (unsigned)(planeA * 4) : 0u);
     // this lane's two A rows (row blocks 2 wid, 2 wid + 1) and one B row (row block wid)
     // (arrays sized 2 >= NAB: a dependent bound in the nested lambda loses the host launch stub)
     unsigned a_base[2];  // dense: byte offset of (row, chunk) in plane 0; conv: pixel index of (n, 0, 0)
@@ -167,19 +153,13 @@ gemm_x3p_kernel(const GemmArgs args) {
         a_base[i] = (unsigned)(n * cH * cW);
       }
     }
-    // B row blocks wid (and wid + 8 for 16 blocks: WIDE)
-    constexpr int NBW = NBB > 8 ? 2 : 1;
+    // B row block wid
     const bool bw = wid < NBB;
-    unsigned b_base[NBW];
-    bool b_ok[NBW];
-#pragma unroll
-    for (int j = 0; j < NBW; ++j) {
-      const int br = ((wid + 8 * j) % NBB) * RPB + drow;
-      const int b_ch = dslot ^ swz<PBK>(br);
-      b_ok[j] = bw && n0 + br < N;
-      b_base[j] = (unsigned)(((long long)(b_ok[j] ? n0 + br : 0) * P.ldb + b_ch * 8) * 2);
-    }
-    // x3d: fp32 float4 slots per thread (4; WIDE 2), slot i = row (tid + 512 i) / 8, k 4 ((tid + 512 i) % 8)
+    const int br = wid * RPB + drow;
+    const int b_ch = dslot ^ swz<PBK>(br);
+    const bool b_ok = bw && n0 + br < N;
+    const unsigned b_base = (unsigned)(((long long)(b_ok ? n0 + br : 0) * P.ldb + b_ch * 8) * 2);
+    // x3d: four fp32 float4 slots per thread, slot i = row (tid + 512 i) / 8, k 4 ((tid + 512 i) % 8)
     constexpr int NSA = ASPLIT ? PBM / 64 : 1;
     const int aq = tid & 7;
     unsigned s_base[NSA];
@@ -210,9 +190,6 @@ gemm_x3p_kernel(const GemmArgs args) {
     float4 areg[NSA];
     float4 a_sc = make_float4(1.f, 1.f, 1.f, 1.f), a_sh = make_float4(0.f, 0.f, 0.f, 0.f);
     unsigned a_msk = 0;
-    float4 rreg[TAIL ? NSA : 1];  // TAIL: residual slots, their BN, the slots' offsets (kOOBp: none)
-    float4 r_sc = make_float4(1.f, 1.f, 1.f, 1.f), r_sh = make_float4(0.f, 0.f, 0.f, 0.f);
-    unsigned o_off[TAIL ? NSA : 1];
     // conv k order (ci / 32, kh, kw, ci % 32): the taps of one 32-channel slice are consecutive
     // k-tiles, so the input rows a tile re-reads for its KH*KW taps are re-read within KH*KW k-tiles
     // (L2-resident) instead of once per full sweep over Cin; the weights are packed to match
@@ -244,10 +221,6 @@ gemm_x3p_kernel(const GemmArgs args) {
           const unsigned ch = (unsigned)((AMODE == 2 ? c_ci : k) + aq * 4) * 4u;  // dense rows: channel = k
           a_sc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsc_p, ch, 0, 0));
           a_sh = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsh_p, ch, 0, 0));
-          if (TAIL == 2) {
-            r_sc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rrs_p, ch, 0, 0));
-            r_sh = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rrb_p, ch, 0, 0));
-          }
         }
 #pragma unroll
         for (int i = 0; i < NSA; ++i) {
@@ -263,10 +236,6 @@ gemm_x3p_kernel(const GemmArgs args) {
           }
           areg[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off : kOOBp, 0, 0));
           a_msk |= (unsigned)ok << i;
-          if constexpr (TAIL != 0) {
-            rreg[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rr_p, ok ? off : kOOBp, 0, 0));
-            o_off[i] = ok ? off : kOOBp;
-          }
         }
       }
       unsigned aoff[2];
@@ -301,15 +270,11 @@ gemm_x3p_kernel(const GemmArgs args) {
               ra, (lds_ptr_t)(base + p * PBM * PROWB + (NAB * wid + i) * RPB * PROWB), 16,
               aoff[i] == kOOBp ? kOOBp : aoff[i] + p * pA2, 0, 0, 0);
       if (bw) {
+        const unsigned boff = b_ok && kok ? b_base + (unsigned)k * 2 : kOOBp;
 #pragma unroll
-        for (int j = 0; j < NBW; ++j) {
-          const unsigned boff = b_ok[j] && kok ? b_base[j] + (unsigned)k * 2 : kOOBp;
-#pragma unroll
-          for (int p = 0; p < 3; ++p)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + (wid + 8 * j) * RPB * PROWB), 16,
-                boff == kOOBp ? kOOBp : boff + p * pB2, 0, 0, 0);
-        }
+        for (int p = 0; p < 3; ++p)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * RPB * PROWB),
+                                                   16, boff == kOOBp ? kOOBp : boff + p * pB2, 0, 0, 0);
       }
     };
     // x3d: fp32 A registers of one k-tile -> (prologue) -> three planes
@@ -319,14 +284,8 @@ gemm_x3p_kernel(const GemmArgs args) {
 #pragma unroll
       for (int i = 0; i < NSA; ++i) {
         float4 v = ar[i];
-        if constexpr (TAIL != 0) {  // the block output, bit for bit capmi_bn_add_relu's
-          const float4 r = TAIL == 2 ? fma4(rreg[i], r_sc, r_sh) : rreg[i];
-          v = relu4(fma4(v, sc, sh) + r);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_p, v), ro_p, o_off[i], 0, 0);
-        } else if (PRO) {
-          v = make_float4(fmaxf(fmaf(v.x, sc.x, sh.x), 0.f), fmaxf(fmaf(v.y, sc.y, sh.y), 0.f),
-                          fmaxf(fmaf(v.z, sc.z, sh.z), 0.f), fmaxf(fmaf(v.w, sc.w, sh.w), 0.f));
-        }
+        if (PRO) v = make_float4(fmaxf(fmaf(v.x, sc.x, sh.x), 0.f), fmaxf(fmaf(v.y, sc.y, sh.y), 0.f),
+                                 fmaxf(fmaf(v.z, sc.z, sh.z), 0.f), fmaxf(fmaf(v.w, sc.w, sh.w), 0.f));
         if (!((msk >> i) & 1u)) v = make_float4(0.f, 0.f, 0.f, 0.f);  // padding taps: zeros AFTER the BN
         unsigned lo[3], hi[3];
         split3_pair(v.x, v.y, lo);
@@ -431,6 +390,150 @@ gemm_x3p_kernel(const GemmArgs args) {
           }
       }
     };
+#ifndef X3D_PIPE
+#define X3D_PIPE 1
+#endif
+    if constexpr (ASPLIT && M16 && X3D_PIPE) {
+      // x3d, round 4: A two k-tiles deep in ONE register set. During tile kt's MFMAs each of the thread's four
+      // float4 slots is split into the other buffer for tile kt + 1 and at once reloaded with tile kt + 2's
+      // (its BN scale / shift and the conv walk follow after the fourth slot): the A load has a whole k-tile to
+      // land, and the split's VALU and ds_writes interleave with the MFMAs instead of standing between two
+      // k-tiles with the load latency in front of them (the one-deep form: issue, MFMAs, wait, split, barrier)
+      auto b_dma = [&](int kt, int buf) {  // B planes of tile kt (past the end: zeros) into buffer buf
+        const int k = k_lo + kt * PBK;
+        unsigned char* base = lds + buf * PBUF;
+        if (bw) {
+          const unsigned boff = b_ok && k < k_hi ? b_base + (unsigned)k * 2 : kOOBp;
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * RPB * PROWB),
+                                                     16, boff == kOOBp ? kOOBp : boff + p * pB2, 0, 0, 0);
+        }
+      };
+      auto a_load = [&](int kt, int i) {  // slot i of tile kt (the conv walk at tile kt)
+        const int k = k_lo + kt * PBK;
+        const bool kok = k < k_hi;
+        unsigned off;
+        bool ok;
+        if (AMODE == 0) {
+          ok = s_ok[i] && kok;
+          off = s_base[i] + (unsigned)k * 4;
+        } else {
+          const int ih = s_ih0[i] + c_kh, iw = s_iw0[i] + c_kw;
+          ok = s_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
+          off = ((s_base[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + aq * 4)) * 4u;
+        }
+        areg[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off : kOOBp, 0, 0));
+        a_msk = (a_msk & ~(1u << i)) | ((unsigned)ok << i);
+      };
+      auto a_next = [&](int kt) {  // after tile kt's four slots: its BN scale / shift, then the walk advances
+        const int k = k_lo + kt * PBK;
+        if (PRO) {  // always two loads (the step's vmcnt count relies on it); past the last k-tile the walk is
+                    // past Cin: an out-of-range offset, zeros
+          const unsigned ch = k < k_hi ? (unsigned)((AMODE == 2 ? c_ci : k) + aq * 4) * 4u : kOOBp;
+          a_sc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsc_p, ch, 0, 0));
+          a_sh = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsh_p, ch, 0, 0));
+        }
+        if (AMODE == 2 && ++c_kw == cKW) {  // (32-deep k-tiles: one (channel slice, tap) chunk per tile)
+          c_kw = 0;
+          if (++c_kh == P.cKH) {
+            c_kh = 0;
+            c_ci += 32;
+          }
+        }
+      };
+      auto a_split = [&](int buf, int i) {  // slot i -> (prologue) -> three planes of buffer buf
+        unsigned char* base = lds + buf * PBUF;
+        float4 v = areg[i];
+        if (PRO) v = make_float4(fmaxf(fmaf(v.x, a_sc.x, a_sh.x), 0.f), fmaxf(fmaf(v.y, a_sc.y, a_sh.y), 0.f),
+                                 fmaxf(fmaf(v.z, a_sc.z, a_sh.z), 0.f), fmaxf(fmaf(v.w, a_sc.w, a_sh.w), 0.f));
+        const bool keep = (a_msk >> i) & 1u;  // padding taps / rows past M: zeros AFTER the BN
+        v.x = keep ? v.x : 0.f;
+        v.y = keep ? v.y : 0.f;
+        v.z = keep ? v.z : 0.f;
+        v.w = keep ? v.w : 0.f;
+        unsigned lo[3], hi[3];
+        split3_pair(v.x, v.y, lo);
+        split3_pair(v.z, v.w, hi);
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          *reinterpret_cast<uint2*>(base + p * PBM * PROWB + s_lds[i]) = make_uint2(lo[p], hi[p]);
+      };
+      const int c16 = lane >> 4, rl16 = lane & 15;
+      auto frag = [&](const unsigned char* plane, int r) {  // 16x16x32 fragment of row r, chunk c16
+        return *reinterpret_cast<const bf16x8_p*>(plane + r * PROWB + ((c16 ^ swz<PBK>(r)) << 4));
+      };
+      auto step = [&](int kt, int buf) {
+        b_dma(kt + 1, buf ^ 1);  // buffer buf ^ 1 was last read by the previous step (barrier since)
+        const unsigned char* A_ = lds + buf * PBUF;
+        const unsigned char* B_ = A_ + PA_BYTES;
+        bf16x8_p b[JN][3], a[3];
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) b[j][p] = frag(B_ + p * PBN * PROWB, wn0 + 16 * j + rl16);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) a[p] = frag(A_ + p * PBM * PROWB, wm0 + rl16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          bf16x8_p an[3];
+          if (i + 1 < 4) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) an[p] = frag(A_ + p * PBM * PROWB, wm0 + 16 * (i + 1) + rl16);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          a_split(buf ^ 1, i);
+          a_load(kt + 2, i);
+          if (i == 3) a_next(kt + 2);
+          // per accumulator the six products smallest terms first (the one-deep form's order)
+#pragma unroll
+          for (int j = 0; j < JN; ++j) {
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][1], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][2], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[j][0], acc4[i][j], 0, 0, 0);
+          }
+#pragma unroll
+          for (int j = 0; j < JN; ++j) {
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][1], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][0], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][0], acc4[i][j], 0, 0, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 24; ++r) {  // one MFMA, then up to two VALU (the slot's split)
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (i + 1 < 4) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) a[p] = an[p];
+          }
+        }
+        // the B DMA of tile kt + 1 was issued before the four A loads (and the two scale / shift loads) of
+        // tile kt + 2: waiting until that many remain drains it
+        if (PRO)
+          asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        __syncthreads();
+      };
+      // tile 0: A loaded, split into buffer 0 with its B planes; tile 1's A loaded; then one step per tile
+      b_dma(0, 0);
+#pragma unroll
+      for (int i = 0; i < NSA; ++i) a_load(0, i);
+      a_next(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < NSA; ++i) a_split(0, i);
+#pragma unroll
+      for (int i = 0; i < NSA; ++i) a_load(1, i);
+      a_next(1);
+      __syncthreads();
+      for (int kt = 0; kt < nkt; ++kt) step(kt, kt & 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the loads and DMA past the end drained)
+      __syncthreads();  // (the next tile's prologue rewrites buffer 0, which the last step may have read)
+      return;
+    }
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     store_a(0);
@@ -729,37 +832,12 @@ __global__ void __launch_bounds__(256) bn_relu_split3_kernel(const float4* __res
 
 }  // namespace
 
-int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s, bool wide) {
+int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
   const dim3 g(blocks), b(PNT);
   const bool sk = a.sk_workers > 0;
   const bool pro = a.p[0].in_scale != nullptr;
-  const int tail = a.p[0].in_res == nullptr ? 0 : a.p[0].in_res_scale ? 2 : 1;
 #define X3D_GO(M, S, PR) CAPMI_KLAUNCH((gemm_x3p_kernel<M, S, 32, true, PR>), g, b, 0, s, a)
-#define X3D_GOW(S, PR) CAPMI_KLAUNCH((gemm_x3p_kernel<0, S, 32, true, PR, true>), g, b, 0, s, a)
-#define X3D_GOT(S, W, T) CAPMI_KLAUNCH((gemm_x3p_kernel<0, S, 32, true, true, W, T>), g, b, 0, s, a)
-  if (tail) {  // the fused bottleneck tail (dense rows, the prologue set: x3d_plan checks)
-    CAPMI_REQUIRE(amode == 0 && pro, CAPMI_EINVAL);
-    if (wide) {
-      if (tail == 2) {
-        if (sk) X3D_GOT(true, true, 2); else X3D_GOT(false, true, 2);
-      } else {
-        if (sk) X3D_GOT(true, true, 1); else X3D_GOT(false, true, 1);
-      }
-    } else {
-      if (tail == 2) {
-        if (sk) X3D_GOT(true, false, 2); else X3D_GOT(false, false, 2);
-      } else {
-        if (sk) X3D_GOT(true, false, 1); else X3D_GOT(false, false, 1);
-      }
-    }
-  } else if (wide) {  // 128 x 256 tiles, dense rows
-    CAPMI_REQUIRE(amode == 0, CAPMI_EINVAL);
-    if (pro) {
-      if (sk) X3D_GOW(true, true); else X3D_GOW(false, true);
-    } else {
-      if (sk) X3D_GOW(true, false); else X3D_GOW(false, false);
-    }
-  } else if (amode == 2) {
+  if (amode == 2) {
     if (pro) {
       if (sk) X3D_GO(2, true, true); else X3D_GO(2, false, true);
     } else {
@@ -771,8 +849,6 @@ int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s, boo
     if (sk) X3D_GO(0, true, false); else X3D_GO(0, false, false);
   }
 #undef X3D_GO
-#undef X3D_GOW
-#undef X3D_GOT
   CAPMI_LAUNCH_CHECK();
   return 0;
 }

@@ -109,8 +109,7 @@ gemm_x3s_kernel(const capmi_gemm_problem P, long long lda, int tiles) {
     }
   };
 
-  int t = blockIdx.x;
-  if (t >= tiles) return;
+  int t = blockIdx.x;  // (the host launches at most `tiles` workgroups)
   load_a(t);
   store_a(0);
   __syncthreads();
@@ -187,14 +186,15 @@ gemm_x3s_kernel(const capmi_gemm_problem P, long long lda, int tiles) {
 }  // namespace
 
 int gemm_x3s_launch(const capmi_gemm_problem& p, long long lda, int tiles, int grid, hipStream_t s) {
+  CAPMI_REQUIRE(grid >= 1 && grid <= tiles, CAPMI_EINVAL);
   const bool pro = p.in_scale != nullptr;
   const dim3 g(grid), b(SNT);
 #define X3S_GO(NCB)                                                                    \
   do {                                                                                 \
     if (pro)                                                                           \
-      CAPMI_KLAUNCH((gemm_x3s_kernel<NCB, true>), g, b, 0, s, p, lda, tiles);         \
-    else                                                                               \
-      CAPMI_KLAUNCH((gemm_x3s_kernel<NCB, false>), g, b, 0, s, p, lda, tiles);        \
+      CAPMI_KLAUNCH((gemm_x3s_kernel<NCB, true>), g, b, 0, s, p, lda, tiles);  \
+    else                                                                      \
+      CAPMI_KLAUNCH((gemm_x3s_kernel<NCB, false>), g, b, 0, s, p, lda, tiles); \
   } while (0)
   if (p.N == 64)
     X3S_GO(1);

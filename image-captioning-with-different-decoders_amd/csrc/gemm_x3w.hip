@@ -98,119 +98,170 @@ gemm_x3w_kernel(const GemmArgs args) {
       sc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsc, (unsigned)b_ci * 4u, 0, 0));
       sh = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsh, (unsigned)b_ci * 4u, 0, 0));
     }
-    const int hw = P.cHo * P.cWo;
-    float4 ar[4], br[2];
-    unsigned bmask = 0;
-    auto load = [&](int kt) {
-      const int k = k_lo + kt * WBK;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = k + a_r0 + 8 * i;
-        const bool ok = a_mok && row < k_hi;
-        ar[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                               ra, ok ? (unsigned)(((long long)row * P.lda + m0 + 4 * a_c4) * 4) : kOOBw, 0, 0));
-      }
-      bmask = 0;
+    // conv B: each of the thread's two k-rows walks pixels k_lo + b_r0 + 16 i, + 32 per k-tile; its (image,
+    // oh, ow) advances by 32 pixels = dq output rows + dr columns without a division (the load past the
+    // last k-tile may step past the last image: it is masked by pix < k_hi)
+    const int dq = WBK / max(P.cWo, 1), dr = WBK - dq * max(P.cWo, 1);
+    int pn[2] = {0, 0}, poh[2] = {0, 0}, pow_[2] = {0, 0};
+    if (BMODE == 2) {
+      const int hw = P.cHo * P.cWo;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int pix = k + b_r0 + 16 * i;
-        unsigned off = kOOBw;
-        if (b_nok && pix < k_hi) {
-          if (BMODE == 2) {
-            const int n_img = pix / hw, rem = pix - n_img * hw;
-            const int oh = rem / P.cWo, ow = rem - oh * P.cWo;
-            const int ih = oh * P.cStride - P.cPad + b_kh, iw = ow * P.cStride - P.cPad + b_kw;
-            if ((unsigned)ih < (unsigned)P.cH && (unsigned)iw < (unsigned)P.cW)
-              off = (unsigned)(((long long)(n_img * P.cH + ih) * P.cW + iw) * P.cCin + b_ci) * 4u;
-          } else {
-            off = (unsigned)(((long long)pix * P.ldb + b_n) * 4);
-          }
-        }
-        br[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, 0));
-        bmask |= (unsigned)(off != kOOBw) << i;
+        const int pix = k_lo + b_r0 + 16 * i;
+        pn[i] = pix / hw;
+        const int rem = pix - pn[i] * hw;
+        poh[i] = rem / P.cWo;
+        pow_[i] = rem - poh[i] * P.cWo;
       }
+    }
+    // one register set, two k-tiles deep (round 4): during tile kt's MFMAs each of the thread's six float4
+    // pieces (4 of dY, 2 of the input) is split from its register into LDS for tile kt + 1 and at once reloaded
+    // with tile kt + 2's -- the load has a whole k-tile to land, and the split's VALU / ds_writes interleave with
+    // the MFMAs instead of standing between two k-tiles
+    float4 ra4[4], rb4[2];
+    unsigned bmask = 0;
+    auto load_piece = [&](int kt, int pc) {
+      const int k = k_lo + kt * WBK;
+      if (pc < 4) {
+        const int row = k + a_r0 + 8 * pc;
+        const bool ok = a_mok && row < k_hi;
+        ra4[pc] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 ra, ok ? (unsigned)(((long long)row * P.lda + m0 + 4 * a_c4) * 4) : kOOBw, 0, 0));
+        return;
+      }
+      const int i = pc - 4;
+      const int pix = k + b_r0 + 16 * i;
+      unsigned off = kOOBw;
+      if (BMODE == 2) {
+        const int ih = poh[i] * P.cStride - P.cPad + b_kh, iw = pow_[i] * P.cStride - P.cPad + b_kw;
+        if (b_nok && pix < k_hi && (unsigned)ih < (unsigned)P.cH && (unsigned)iw < (unsigned)P.cW)
+          off = (unsigned)(((pn[i] * P.cH + ih) * P.cW + iw) * P.cCin + b_ci) * 4u;
+        // the next k-tile's pixel (a piece's loads are issued in k-tile order)
+        // (selects, no branch: the host guarantees dq + 1 < 2 Ho, so two wraps of oh suffice)
+        pow_[i] += dr;
+        poh[i] += dq;
+        const bool cw = pow_[i] >= P.cWo;
+        pow_[i] -= cw ? P.cWo : 0;
+        poh[i] += cw;
+#pragma unroll
+        for (int w2 = 0; w2 < 2; ++w2) {
+          const bool ch = poh[i] >= P.cHo;
+          poh[i] -= ch ? P.cHo : 0;
+          pn[i] += ch;
+        }
+      } else if (b_nok && pix < k_hi) {
+        off = (unsigned)(((long long)pix * P.ldb + b_n) * 4);
+      }
+      rb4[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rb, off, 0, 0));
+      bmask = (bmask & ~(1u << i)) | ((unsigned)(off != kOOBw) << i);
     };
     // registers -> (B: BN-apply + ReLU, padding taps zero AFTER it) -> three swizzled bf16 planes
-    auto store = [&](int buf) {
+    auto store_piece = [&](int buf, int pc) {
       unsigned char* base = lds + buf * WBUF;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = a_r0 + 8 * i;
+      if (pc < 4) {
+        const int r = a_r0 + 8 * pc;
         const int o = r * WA_ROWB + (((a_c4 >> 1) ^ wsw(r)) << 4) + (a_c4 & 1) * 8;
         unsigned lo[3], hi[3];
-        split3_pair(ar[i].x, ar[i].y, lo);
-        split3_pair(ar[i].z, ar[i].w, hi);
+        split3_pair(ra4[pc].x, ra4[pc].y, lo);
+        split3_pair(ra4[pc].z, ra4[pc].w, hi);
 #pragma unroll
         for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(base + p * WA_PLANE + o) = make_uint2(lo[p], hi[p]);
+        return;
       }
+      const int i = pc - 4;
+      const int r = b_r0 + 16 * i;
+      const int o = r * WB_ROWB + (((b_c4 >> 1) ^ wsw(r)) << 4) + (b_c4 & 1) * 8;
+      // (no branch: the piece shares a scheduling region with MFMAs; without the prologue sc / sh are 1 / 0,
+      // and relu(x) could differ from x -- so select)
+      const float4 u = rb4[i];
+      const float4 f = make_float4(fmaxf(fmaf(u.x, sc.x, sh.x), 0.f), fmaxf(fmaf(u.y, sc.y, sh.y), 0.f),
+                                   fmaxf(fmaf(u.z, sc.z, sh.z), 0.f), fmaxf(fmaf(u.w, sc.w, sh.w), 0.f));
+      const bool keep = (bmask >> i) & 1u;
+      float4 v;
+      v.x = keep ? (pro ? f.x : u.x) : 0.f;
+      v.y = keep ? (pro ? f.y : u.y) : 0.f;
+      v.z = keep ? (pro ? f.z : u.z) : 0.f;
+      v.w = keep ? (pro ? f.w : u.w) : 0.f;
+      unsigned lo[3], hi[3];
+      split3_pair(v.x, v.y, lo);
+      split3_pair(v.z, v.w, hi);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int r = b_r0 + 16 * i;
-        const int o = r * WB_ROWB + (((b_c4 >> 1) ^ wsw(r)) << 4) + (b_c4 & 1) * 8;
-        float4 v = br[i];
-        if (pro) v = make_float4(fmaxf(fmaf(v.x, sc.x, sh.x), 0.f), fmaxf(fmaf(v.y, sc.y, sh.y), 0.f),
-                                 fmaxf(fmaf(v.z, sc.z, sh.z), 0.f), fmaxf(fmaf(v.w, sc.w, sh.w), 0.f));
-        if (!((bmask >> i) & 1u)) v = make_float4(0.f, 0.f, 0.f, 0.f);
-        unsigned lo[3], hi[3];
-        split3_pair(v.x, v.y, lo);
-        split3_pair(v.z, v.w, hi);
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          *reinterpret_cast<uint2*>(base + WA_BYTES + p * WB_PLANE + o) = make_uint2(lo[p], hi[p]);
-      }
+      for (int p = 0; p < 3; ++p)
+        *reinterpret_cast<uint2*>(base + WA_BYTES + p * WB_PLANE + o) = make_uint2(lo[p], hi[p]);
     };
     // transposed fragment reads: lane l of group g = l / 16 takes k-rows 8g + (l & 15) / 4 (+ 4), columns
     // base + 4 (l & 3); it receives column l & 15 of those 4 rows, k = 8g .. 8g + 3 (+ 4 .. 7)
     const int g8 = (lane >> 4) * 8, q = (lane & 15) >> 2, c4 = (lane & 3) * 4;
-    auto compute = [&](int buf) {
+    // tile kt from buffer buf: its fragments, then four 24-MFMA blocks with the six pieces of tile kt + 1 split
+    // into buffer buf ^ 1 (last read by the previous step; barrier since) and reloaded with tile kt + 2
+    auto step = [&](int kt, int buf) {
       const unsigned char* A_ = lds + buf * WBUF;
       const unsigned char* B_ = A_ + WA_BYTES;
-      bf16x8_w a[4][3], b[4][3];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          const s16x4_w lo = tr_read(A_ + p * WA_PLANE, WA_ROWB, g8 + q, wm0 + 16 * i + c4);
-          const s16x4_w hi = tr_read(A_ + p * WA_PLANE, WA_ROWB, g8 + 4 + q, wm0 + 16 * i + c4);
-          a[i][p] = __builtin_bit_cast(bf16x8_w, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-        }
+      auto frag = [&](const unsigned char* plane, int rowb, int col) {
+        const s16x4_w lo = tr_read(plane, rowb, g8 + q, col);
+        const s16x4_w hi = tr_read(plane, rowb, g8 + 4 + q, col);
+        return __builtin_bit_cast(bf16x8_w, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      };
+      bf16x8_w b[4][3];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          const s16x4_w lo = tr_read(B_ + p * WB_PLANE, WB_ROWB, g8 + q, wn0 + 16 * j + c4);
-          const s16x4_w hi = tr_read(B_ + p * WB_PLANE, WB_ROWB, g8 + 4 + q, wn0 + 16 * j + c4);
-          b[j][p] = __builtin_bit_cast(bf16x8_w, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-        }
-      // smallest terms first into each fp32 accumulator (gemm_x3p.hip's order)
+        for (int p = 0; p < 3; ++p) b[j][p] = frag(B_ + p * WB_PLANE, WB_ROWB, wn0 + 16 * j + c4);
+      // A fragments one 16-row block at a time (12 VGPRs live instead of 48)
+      bf16x8_w a[3];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int p = 0; p < 3; ++p) a[p] = frag(A_ + p * WA_PLANE, WA_ROWB, wm0 + c4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bf16x8_w an[3];
+        if (i + 1 < 4) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) an[p] = frag(A_ + p * WA_PLANE, WA_ROWB, wm0 + 16 * (i + 1) + c4);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // pieces i (and 2 + i for i >= 2: the input's two) of tile kt + 1 -> LDS, then their tile kt + 2 loads
+        store_piece(buf ^ 1, i);
+        if (i >= 2) store_piece(buf ^ 1, 2 + i);
+        load_piece(kt + 2, i);
+        if (i >= 2) load_piece(kt + 2, 2 + i);
+        // per accumulator the six products smallest terms first (gemm_x3p.hip's order)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][1], acc4[i][j], 0, 0, 0);
-          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][2], acc4[i][j], 0, 0, 0);
-          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[j][0], acc4[i][j], 0, 0, 0);
+          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][1], acc4[i][j], 0, 0, 0);
+          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][2], acc4[i][j], 0, 0, 0);
+          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[j][0], acc4[i][j], 0, 0, 0);
         }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][1], acc4[i][j], 0, 0, 0);
-          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][0], acc4[i][j], 0, 0, 0);
-          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][0], acc4[i][j], 0, 0, 0);
+          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][1], acc4[i][j], 0, 0, 0);
+          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][0], acc4[i][j], 0, 0, 0);
+          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][0], acc4[i][j], 0, 0, 0);
         }
-    };
-    load(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    store(0);
-    __syncthreads();
-    for (int kt = 0; kt < nkt; ++kt) {
-      load(kt + 1);  // past the end: OOB loads (zeros), stored into the idle buffer
-      compute(kt & 1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      store((kt + 1) & 1);  // buffer (kt + 1) & 1 was last read by compute(kt - 1)
+#pragma unroll
+        for (int r = 0; r < 24; ++r) {  // one MFMA, then up to two VALU (the piece's split)
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (i + 1 < 4) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) a[p] = an[p];
+        }
+      }
       __syncthreads();
-    }
+    };
+    // tile 0 split into buffer 0 up front, tile 1 loaded; the last step splits the (all-zero, OOB) tile past the
+    // end into the idle buffer, and its loads past the end read zeros
+#pragma unroll
+    for (int pc = 0; pc < 6; ++pc) load_piece(0, pc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int pc = 0; pc < 6; ++pc) store_piece(0, pc);
+#pragma unroll
+    for (int pc = 0; pc < 6; ++pc) load_piece(1, pc);
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) step(kt, kt & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the loads past the end: drained before the epilogue)
   };
 
   // epilogue: C (fp32, ldc) = alpha A.B (+ beta C); 16x16 blocks: lane l holds rows 4 (l / 16) .. + 3 of

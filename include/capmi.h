@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 20
+#define CAPMI_ABI_VERSION 22
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -60,7 +60,7 @@ enum capmi_bmode {
  * CAPMI_TILE_128_W8: 128x128 with 512-thread workgroups (8 waves, one workgroup per CU), forward
  * modes (A row-major / conv x W[N][K]) of capmi_gemm_sk only */
 enum capmi_tile { CAPMI_TILE_128 = 0, CAPMI_TILE_64 = 1, CAPMI_TILE_128x64 = 2, CAPMI_TILE_AUTO = 3,
-                  CAPMI_TILE_128_W8 = 4, CAPMI_TILE_128x256 = 5 /* CAPMI_GEMM_X3D on dense rows only */ };
+                  CAPMI_TILE_128_W8 = 4 };
 
 typedef struct capmi_gemm_problem {
   int M, N, K;
@@ -78,14 +78,6 @@ typedef struct capmi_gemm_problem {
   int cN, cH, cW, cCin, cKH, cKW, cStride, cPad, cHo, cWo;
   const float* in_scale; /* NULL or [Cin]: A element := relu(x*in_scale[ci] + in_shift[ci]) in-bounds (BN-apply+ReLU prologue) */
   const float* in_shift;
-  /* fused bottleneck tail (CAPMI_GEMM_X3D on dense rows only, ABI 20): with in_res set, the A element is
-   * relu(fma(A, in_scale, in_shift) + r') with r' = in_res, or fma(in_res, in_res_scale, in_res_shift) when
-   * those are set (capmi_bn_add_relu's arithmetic; in_res in A's layout), and it is also stored to in_out
-   * (same layout): the block output, written once. NULL elsewhere. */
-  const float* in_res;
-  const float* in_res_scale;
-  const float* in_res_shift;
-  float* in_out;
 } capmi_gemm_problem;
 
 int capmi_gemm(const capmi_gemm_problem* problems, int nprob, int amode, int bmode, int tile,
@@ -144,9 +136,7 @@ int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int t
 /* CAPMI_GEMM_X3D (alone): the CAPMI_GEMM_X3P kernel with A the fp32 operand itself (CAPMI_A_KMAJOR,
  * lda % 4 == 0, or CAPMI_A_CONV_NHWC, Cin % 32 == 0, with the optional BN-apply + ReLU prologue),
  * split into the three bf16 planes in-kernel while B (pre-split, x3p k order) is LDS-DMA staged;
- * 256x128 tiles (128x256 for CAPMI_TILE_128x256, dense rows), k-tiles of 32, one workgroup per CU,
- * stream-K as capmi_gemm_sk. Dense rows with the prologue (lda == K: k is the channel) also take the fused
- * bottleneck tail (in_res / in_out, ABI 20). */
+ * 256x128 tiles, k-tiles of 32, one workgroup per CU, stream-K as capmi_gemm_sk. */
 #define CAPMI_GEMM_X3D 32
 /* CAPMI_GEMM_X3S (alone, ABI 17): the CAPMI_GEMM_X3 arithmetic for the short-k convs (layer1's K = 64):
  * K == 64, N in {64, 128, 256}; A fp32 dense rows (CAPMI_A_KMAJOR, lda % 4 == 0) or a 1x1 / stride-1 /
@@ -215,10 +205,9 @@ int capmi_conv_weight_pack_pad(const float* w, int Cout, int Cin, int KH, int KW
 int capmi_image_nhwc4(const float* in, int N, int C, int H, int W, float* out, void* stream);
 /* BatchNorm2d(train) finalize from capmi_gemm stats: mean/var over `count` rows, then
  * scale = gamma*rsqrt(var+eps), shift = beta - mean*scale; running stats updated in place
- * (momentum, unbiased var) when running_mean != NULL. mean/var out (may be NULL).
- * work: CAPMI_BN_WORK_DOUBLES(C) doubles of scratch, ZEROED by the caller before first use (it
- * holds per-channel-block arrival counters the kernel re-arms to zero; one work buffer per
- * concurrently running stream). */
+ * (momentum, unbiased var) when running_mean != NULL. mean/var out (may be NULL). The fp64 sums run
+ * in one canonical order (csrc/bn_final.h), reproducible op for op on the host.
+ * work: CAPMI_BN_WORK_DOUBLES(C) doubles, 16-B aligned (unused since round 4; kept in the signature). */
 #define CAPMI_BN_WORK_DOUBLES(C) (64 + 64 * (long long)(C)) /* C <= 8192 */
 int capmi_bn_finalize(const float* stats, int tiles, int C, long long count, const float* gamma,
                       const float* beta, float* running_mean, float* running_var, float momentum,

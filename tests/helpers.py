@@ -83,7 +83,7 @@ def _oracle_att_preacts(p, enc, caps, lengths, dtype):
     import torch.nn.functional as F
     from oracle import decoder_ref as R
     q = {k: v.to(dtype) for k, v in p.items()}
-    e = enc.to(dtype)
+    e = enc.to(dtype).reshape(enc.shape[0], -1, enc.shape[-1])  # (B, P, D), as forward() flattens it (:231)
     emb = F.embedding(caps, q["embedding.weight"]).to(dtype)
     h, c = R.init_hidden_state(q, e)
     ae = R._lin(e, q, "attention.enc_att")  # loop-invariant (models/attention.py:54, recomputed there)

@@ -376,96 +376,3 @@ def test_x3d_prologue_scale_shift_at_allocation_end():
         K.sk_check([ws])
         assert bool(torch.isfinite(outs[1]).all())
         assert torch.equal(outs[0], outs[1])
-
-
-@pytest.mark.parametrize("M,C,N,rbn,wide", [(12544, 1024, 256, False, True), (50176, 512, 128, True, False),
-                                            (1000, 256, 256, False, True), (777, 512, 512, True, False),
-                                            (3136, 1024, 256, True, True), (12544, 1024, 256, True, False)])
-def test_x3d_fused_tail_bit_identical(M, C, N, rbn, wide):
-    """gemm_x3d dense rows with the fused bottleneck tail (in_res, ABI 20) == capmi_bn_add_relu followed by the
-    plain x3d GEMM on its output, bit for bit: the block output it stores (in_out), the GEMM output and the BN
-    statistics; stream-K and data-parallel grids, 256 x 128 and 128 x 256 tiles, ragged M, several column tiles
-    (only the first stores), and the downsample-BN residual (rbn)."""
-    K = _K()
-    from capmi._lib import CAPMI_TILE_128x256
-    tile = CAPMI_TILE_128x256 if wide else K.TILE_AUTO
-    y, res = rnd(M, C, seed=41).to(DEV), rnd(M, C, seed=42).to(DEV)
-    s, b = (rnd(C, seed=43) + 1.0).to(DEV), rnd(C, seed=44).to(DEV)
-    rs, rb = ((rnd(C, seed=45) + 1.0).to(DEV), rnd(C, seed=46).to(DEV)) if rbn else (None, None)
-    w3 = split3((rnd(N, C, seed=47) * (2.0 / C) ** 0.5).to(DEV))
-    ws = K.gemm_workspace(DEV)
-    # reference: the separate tail pass, then the plain GEMM on its output
-    x_ref = torch.empty(M, C, device=DEV)
-    K.bn_add_relu(y, s, b, res, x_ref, M, C, res_scale=rs, res_shift=rb)
-    c_ref = torch.empty(M, N, device=DEV)
-    st_ref = torch.zeros(2 * K.stat_tiles(M) * N, device=DEV)
-    p_ref = K.problem(M, N, C, x_ref, C, w3, C, c_ref, N, stats=st_ref)
-    K.gemm_x3d(p_ref, 0, ws, tile=tile)
-    # fused
-    x_f = torch.full((M + 3, C), float("nan"), device=DEV)  # NaN rows past M stay untouched
-    c_f = torch.empty(M, N, device=DEV)
-    st_f = torch.zeros(2 * K.stat_tiles(M) * N, device=DEV)
-    p_f = K.problem(M, N, C, y, C, w3, C, c_f, N, stats=st_f, in_scale=s, in_shift=b, in_res=res,
-                    in_res_scale=rs, in_res_shift=rb, in_out=x_f)
-    K.gemm_x3d(p_f, 0, ws, tile=tile)
-    torch.cuda.synchronize()
-    K.sk_check([ws])
-    assert torch.equal(x_f[:M], x_ref)
-    assert bool(torch.isnan(x_f[M:]).all())
-    assert torch.equal(c_f, c_ref)
-    assert torch.equal(st_f, st_ref)
-
-
-def test_x3d_fused_tail_rejected_elsewhere():
-    """The tail fields are a CAPMI_GEMM_X3D dense-rows form only: gemm_x3 / x3p, a conv-mode x3d, a tail without
-    the prologue or without in_out raise EINVAL instead of silently dropping the block output."""
-    K = _K()
-    M, C, N = 256, 64, 128
-    y, res, x_o = (torch.zeros(M, C, device=DEV) for _ in range(3))
-    s, b = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
-    w3 = split3(torch.zeros(N, C, device=DEV))
-    c = torch.empty(M, N, device=DEV)
-    ws = K.gemm_workspace(DEV)
-    full = dict(in_scale=s, in_shift=b, in_res=res, in_out=x_o)
-    with pytest.raises(RuntimeError):
-        K.gemm_x3(K.problem(M, N, C, y, C, w3, C, c, N, **full), 0, ws)
-    with pytest.raises(RuntimeError):
-        K.gemm_x3d(K.problem(M, N, C, y, C, w3, C, c, N, in_res=res, in_out=x_o), 0, ws)
-    with pytest.raises(RuntimeError):
-        K.gemm_x3d(K.problem(M, N, C, y, C, w3, C, c, N, in_scale=s, in_shift=b, in_res=res), 0, ws)
-    geo = dict(N=1, H=16, W=16, Cin=C, KH=1, KW=1, stride=1, pad=0, Ho=16, Wo=16)
-    with pytest.raises(RuntimeError):
-        K.gemm_x3d(K.problem(M, N, C, y, 0, w3, C, c, N, conv=geo, **full), 2, ws)
-    torch.cuda.synchronize()
-
-
-def test_encoder_x3_fused_tails_bit_identical(monkeypatch):
-    """The x3 encoder forward (batch 2, 224 x 224, train mode) with the bottleneck tails of layer2 / layer3 fused
-    into the next conv1 (the default) == with every tail as the separate pass (CAPMI_X3_TAIL=0), bit for bit:
-    features, and the BN running statistics every layer updated."""
-    import gen
-    from capmi import resnet as RN
-    from helpers import t
-    from models.encoder import EncoderAttention
-    names = ["conv1", "bn1", "relu", "maxpool", "layer1", "layer2", "layer3", "layer4"]
-    seed = 79
-    params = gen.resnet101_params(seed)
-    x = t(gen.images(seed, 2, 224, 224), DEV)
-    outs = []
-    for fused in (True, False):
-        monkeypatch.setattr(RN, "_X3_TAIL", fused)
-        enc = EncoderAttention()
-        sd = enc.state_dict()
-        for k_, v in params.items():
-            head, rest = k_.split(".", 1)
-            sd[f"resnet.{names.index(head)}.{rest}"] = t(v).clone()
-        enc.load_state_dict(sd)
-        enc = enc.to(DEV).train()
-        enc.set_compute_precision("fp32-x3")
-        with torch.no_grad():
-            y = enc(x)
-        torch.cuda.synchronize()
-        outs.append((y.cpu(), {k: v.cpu() for k, v in enc.state_dict().items() if "running" in k}))
-    assert torch.equal(outs[0][0], outs[1][0])
-    for k in outs[0][1]:
-        assert torch.equal(outs[0][1][k], outs[1][1][k]), k

@@ -31,11 +31,8 @@ def test_struct_layout():
     from capmi._lib import GemmProblem
     # 4 ints, 15 pointer/longlong, 2 floats + int, 10 ints -> layout checked via offsets of anchors
     assert GemmProblem.A.offset == 16
+    assert GemmProblem.in_shift.offset + 8 == ctypes.sizeof(GemmProblem)
     assert GemmProblem.in_shift.offset == GemmProblem.in_scale.offset + 8
-    # ABI 20: the fused bottleneck tail's four pointers follow in_shift, in_out last
-    assert GemmProblem.in_res.offset == GemmProblem.in_shift.offset + 8
-    assert GemmProblem.in_out.offset == GemmProblem.in_res.offset + 24
-    assert GemmProblem.in_out.offset + 8 == ctypes.sizeof(GemmProblem)
 
 
 def test_abi_and_errors():

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--x3p", action="store_true", help="x3 with the A operand pre-split too (CAPMI_GEMM_X3P)")
     ap.add_argument("--x3d", action="store_true", help="x3 with the fp32 A split in-kernel, B by LDS-DMA (CAPMI_GEMM_X3D)")
     ap.add_argument("--x3s", action="store_true", help="short-k streaming x3 kernel (gemm_x3s.hip)")
+    ap.add_argument("--x3w", action="store_true", help="the conv's WEIGHT gradient on gemm_x3w.hip (dW = dY^T im2col(X))")
     a = ap.parse_args()
     dev = "cuda"
     ci, H, W, co, k, pro, *st = SHAPES[a.shape]
@@ -93,6 +94,18 @@ def main():
         prob.B = w3.data_ptr()
         print("x3s kernel:", K.gemm_x3s_kernel_name(prob, mode))
         run = lambda: K.gemm_x3s(prob, mode)  # noqa: E731
+    elif a.x3w:  # dW[co][k*k*ci] = sum over output pixels of dY[p][co] x im2col(relu(bn(x)))[p][n]
+        from capmi._lib import CAPMI_B_CONV_NHWC, CAPMI_B_KROWS
+        dy = torch.rand(M, co, device=dev, generator=g) - 0.5
+        dw = torch.empty(co, Kd, device=dev)
+        bmode = CAPMI_B_KROWS if (k == 1 and stride == 1 and not pro) else CAPMI_B_CONV_NHWC
+        if bmode == CAPMI_B_KROWS:
+            prob = K.problem(co, Kd, M, dy, co, x, ci, dw, Kd)
+        else:
+            prob = K.problem(co, Kd, M, dy, co, x, 0, dw, Kd, conv=geo, in_scale=sc if pro else None,
+                             in_shift=sh if pro else None)
+        print("x3w kernel:", K.gemm_x3w_kernel_name(prob, bmode))
+        run = lambda: K.gemm_x3w(prob, bmode, ws)  # noqa: E731
     elif a.x3:
         w3 = torch.empty(3 * w.numel(), device=dev, dtype=torch.bfloat16)
         K.split3_bf16(w, w3)

@@ -23,10 +23,9 @@ def routed(tag, rows, Cin, Cout, k, st, pro):
     if kd == 64 and k == 1 and st == 1 and Cout in (64, 128, 256) and os.environ.get("CAPMI_X3S", "1") != "0":
         return "x3s"
     if Cin % 32 == 0 and kd % 32 == 0 and (st == 2 or (k == 1 and not in_ss and Cin == 2 * Cout)
-                                           or (rows <= 3136 and not (k == 1 and not in_ss))
-                                           or (k == 1 and in_ss and Cout == 4 * Cin and rows <= 12544)):
-        return "x3d"
-    if in_ss and (Cout >= 128 or (Cout == 64 and k == 3)) and Cin % 32 == 0 and kd >= 128 and rows >= 12544:
+                                           or rows <= 3136 or (k == 1 and in_ss and Cout == 4 * Cin)):
+        return "x3d"  # (round 4 rule)
+    if in_ss and Cout >= 128 and Cin % 32 == 0 and kd >= 128 and rows >= 12544:
         return "x3p"
     return "x3"
 
