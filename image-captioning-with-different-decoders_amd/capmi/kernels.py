@@ -9,8 +9,8 @@ import weakref
 import torch
 
 from ._lib import DstepEpi, DstepSeg
-from ._lib import (CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_GEMM_BF16_IO, CAPMI_GEMM_X3, CAPMI_GEMM_X3P,
-                   CAPMI_GEMM_SPLIT3, CAPMI_GEMM_X3D, CAPMI_GEMM_X3S, CAPMI_GEMM_X3W,
+from ._lib import (CAPMI_A_CONV_NHWC, CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_GEMM_BF16_IO, CAPMI_GEMM_X3, CAPMI_GEMM_X3P,
+                   CAPMI_GEMM_SPLIT3, CAPMI_GEMM_X3C, CAPMI_GEMM_X3D, CAPMI_GEMM_X3S, CAPMI_GEMM_X3W,
                    CAPMI_COLSUM_GROUPS, CAPMI_TILE_128, CAPMI_TILE_64,
                    CAPMI_TILE_128x64, CAPMI_TILE_AUTO, GemmProblem, call, lib)
 
@@ -199,6 +199,24 @@ def gemm_x3s(prob, amode):
     B = three bf16 planes (split3_bf16), store-only epilogue; persistent, no workspace."""
     call("capmi_gemm_sk_ex", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3S,
          None, 0, stream())
+
+
+def gemm_x3c(prob):
+    """CAPMI_GEMM_X3C: the direct 3x3 / stride-1 conv (N = 64, Cin % 32 == 0, W <= 64, optional BN prologue) x
+    B = three bf16 planes in the x3p k order; store-only epilogue, no workspace."""
+    call("capmi_gemm_sk_ex", ctypes.byref(prob), CAPMI_A_CONV_NHWC, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3C,
+         None, 0, stream())
+
+
+def gemm_x3c_ok(prob):
+    """True when CAPMI_GEMM_X3C takes this conv problem (its planner accepts it)."""
+    v = [ctypes.c_int(0) for _ in range(5)]
+    return lib.capmi_gemm_sk_plan(ctypes.byref(prob), CAPMI_A_CONV_NHWC, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO,
+                                  CAPMI_GEMM_X3C, *[ctypes.byref(x) for x in v]) == 0
+
+
+def gemm_x3c_kernel_name(prob):
+    return f"gemm_x3c_kernel<{'true' if prob.in_scale else 'false'}>"
 
 
 def gemm_x3w(prob, bmode, workspace):

@@ -147,6 +147,9 @@ _X3_SMALLK = int(os.environ.get("CAPMI_X3_SMALLK", "0"))
 _X3D = os.environ.get("CAPMI_X3D", "1") != "0"
 # x3 mode: layer1's K = 64 1x1 convs on the short-k streaming kernel (CAPMI_X3S=0: off, A/B)
 _X3S = os.environ.get("CAPMI_X3S", "1") != "0"
+# x3 mode (round 4): layer1's 3x3 on the direct conv (gemm_x3c.hip: each input element split once per 32-channel
+# slice instead of once per tap; CAPMI_X3C=0: gemm_x3, A/B)
+_X3C = os.environ.get("CAPMI_X3C", "1") != "0"
 
 class EncoderRunner:
     """Launch plan for the frozen ResNet-101 conv stack (children()[:-2] of torchvision's
@@ -258,6 +261,18 @@ class EncoderRunner:
             launch = lambda: K.gemm_x3s(prob, mode)  # noqa: E731
             if self.conv_hook is not None:
                 self.conv_hook(tag, 2.0 * rows * co * Kd, launch, K.gemm_x3s_kernel_name(prob, mode))
+            else:
+                launch()
+            return Ho, Wo, rows
+        x3c = (_X3C and x3 and not nchw and kh == 3 and kw == 3 and st == 1 and pd == 1 and co == 64
+               and ci % 32 == 0 and W <= 64 and rows * co * 4 < (1 << 31))
+        if x3c:
+            w3 = self._packed_x3(conv, tap_inner=True)
+            sc, sh = in_ss if in_ss is not None else (None, None)
+            prob = K.problem(rows, co, Kd, x, 0, w3, Kd, out, co, conv=geo, in_scale=sc, in_shift=sh, **kw_)
+            launch = lambda: K.gemm_x3c(prob)  # noqa: E731
+            if self.conv_hook is not None:
+                self.conv_hook(tag, 2.0 * rows * co * Kd, launch, K.gemm_x3c_kernel_name(prob))
             else:
                 launch()
             return Ho, Wo, rows

@@ -5,7 +5,8 @@
 //
 // Canonical order for channel c over the T statistic slices (rows of stats[T][C][2]):
 //   q_l = sum of slice t = l, l + 64, l + 128, ... in ascending t   (l = 0..63, fp64)
-//   sum = q_0 + q_1 + ... + q_63                                       (fp64, in order)
+//   r_w = q_8w + q_8w+1 + ... + q_8w+7                                 (w = 0..7, in order)
+//   sum = r_0 + r_1 + ... + r_7                                        (in order)
 // Threads: a wave covers 8 channels x 8 slice lanes (one 64-B row segment per slice); the 64 lane groups
 // l = 8 w + s of a channel are 8 (virtual) waves w x 8 lanes s.
 #pragma once
@@ -48,7 +49,7 @@ __device__ __forceinline__ void bnf_apply(const BnFinArgs& f, int c, double s, d
 }
 
 // Finalize channel group g (channels [8 g, 8 g + 8) below C) with the calling workgroup's NT threads.
-// scratch: 64 x 8 double2 in LDS (8 KiB), free on entry; the workgroup meets twice.
+// scratch: 72 x 8 double2 in LDS (9 KiB), free on entry; the workgroup meets three times.
 template <int NT>
 __device__ __forceinline__ void bnf_group(const BnFinArgs& f, const float* __restrict__ stats, int T, int C, int g,
                                           double2* scratch) {
@@ -81,10 +82,23 @@ __device__ __forceinline__ void bnf_group(const BnFinArgs& f, const float* __res
     scratch[l * BNF_CG + cl] = make_double2(sm, sq);
   }
   __syncthreads();
+  if (tid < 64) {  // r_w for (w, channel) = (tid / 8, tid % 8): two serial chains of 8 instead of one of 64
+    const int w8 = tid >> 3, cc = tid & 7;
+    double sm = 0.0, sq = 0.0;
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8) {
+      const double2 v = scratch[(8 * w8 + s8) * BNF_CG + cc];
+      sm += v.x;
+      sq += v.y;
+    }
+    scratch[(64 + w8) * BNF_CG + cc] = make_double2(sm, sq);
+  }
+  __syncthreads();
   if (tid < BNF_CG && g * BNF_CG + tid < C) {
     double sm = 0.0, sq = 0.0;
-    for (int l = 0; l < 64; ++l) {
-      const double2 v = scratch[l * BNF_CG + tid];
+#pragma unroll
+    for (int w8 = 0; w8 < 8; ++w8) {
+      const double2 v = scratch[(64 + w8) * BNF_CG + tid];
       sm += v.x;
       sq += v.y;
     }

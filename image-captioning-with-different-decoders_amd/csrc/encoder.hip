@@ -77,64 +77,8 @@ extern "C" int capmi_image_nhwc4(const float* in, int N, int C, int H, int W, fl
 // ---------------------------------------------------------------------------------
 __global__ void __launch_bounds__(512) bn_finalize_kernel(const float* __restrict__ stats, int tiles, int C,
                                                           BnFinArgs f) {
-  __shared__ double2 scratch[64 * BNF_CG];
+  __shared__ double2 scratch[72 * BNF_CG];
   bnf_group<512>(f, stats, tiles, C, blockIdx.x, scratch);
-}
-
-// (temporary A/B, round 4) the round-3 direct finalize: each 1024-thread block reads every slice of its CW
-// channels (CW = 64 / 16 / 4 by slice count) -- CAPMI_BNF_OLD=1
-template <int CW, int U>
-__global__ void __launch_bounds__(1024)
-bn_finalize_direct_kernel(const float* __restrict__ stats, int tiles, int C, BnFinArgs f) {
-  constexpr int TS = 64 / CW, ROWS = 16 * TS;
-  __shared__ double rs[16][CW], rq[16][CW];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int cl = lane % CW, ts = lane / CW;
-  const int c = blockIdx.x * CW + cl;
-  double s = 0.0, q = 0.0;
-  if (c < C) {
-    for (int t = w * TS + ts; t < tiles; t += ROWS * U) {
-      float2 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int tt = t + ROWS * u;
-        v[u] = tt < tiles ? *reinterpret_cast<const float2*>(stats + ((long long)tt * C + c) * 2)
-                          : make_float2(0.f, 0.f);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        s += v[u].x;
-        q += v[u].y;
-      }
-    }
-  }
-#pragma unroll
-  for (int o = CW; o < 64; o <<= 1) {
-    s += __shfl_xor(s, o);
-    q += __shfl_xor(q, o);
-  }
-  if (ts == 0) {
-    rs[w][cl] = s;
-    rq[w][cl] = q;
-  }
-  __syncthreads();
-  if (w != 0 || ts != 0 || c >= C) return;
-  s = 0.0;
-  q = 0.0;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    s += rs[r][cl];
-    q += rq[r][cl];
-  }
-  bnf_apply(f, c, s, q);
-}
-
-bool bnf_old() {
-  static const bool on = [] {
-    const char* e = getenv("CAPMI_BNF_OLD");
-    return e && e[0] == '1';
-  }();
-  return on;
 }
 
 extern "C" int capmi_bn_finalize(const float* stats, int tiles, int C, long long count,
@@ -148,19 +92,6 @@ extern "C" int capmi_bn_finalize(const float* stats, int tiles, int C, long long
   CAPMI_REQUIRE(((uintptr_t)stats & 7) == 0 && ((uintptr_t)work & 15) == 0, CAPMI_EALIGN);
   CAPMI_REQUIRE(C <= 8192, CAPMI_ERANGE);
   const BnFinArgs f{gamma, beta, running_mean, running_var, scale, shift, save_mean, save_var, momentum, eps, count};
-  if (bnf_old()) {
-    if (tiles <= 64)
-      hipLaunchKernelGGL((bn_finalize_direct_kernel<64, 8>), dim3(cdiv(C, 64)), dim3(1024), 0, as_stream(stream), stats,
-                         tiles, C, f);
-    else if (tiles <= 256)
-      hipLaunchKernelGGL((bn_finalize_direct_kernel<16, 4>), dim3(cdiv(C, 16)), dim3(1024), 0, as_stream(stream), stats,
-                         tiles, C, f);
-    else
-      hipLaunchKernelGGL((bn_finalize_direct_kernel<4, 16>), dim3(cdiv(C, 4)), dim3(1024), 0, as_stream(stream), stats,
-                         tiles, C, f);
-    CAPMI_LAUNCH_CHECK();
-    return 0;
-  }
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, BNF_CG)), dim3(512), 0, as_stream(stream), stats, tiles, C, f);
   CAPMI_LAUNCH_CHECK();
   return 0;

@@ -689,6 +689,7 @@ int x3p_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
              int& bk);
 int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, bool& sk, long long& total);
 int x3s_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long& lda, int& tiles, int& grid);
+int x3c_plan(const capmi_gemm_problem* prob, int amode, int bmode, int& tiles);
 int x3w_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long ws_floats, GemmArgs& a, int& S,
              long long& tiles);
 }  // namespace
@@ -734,6 +735,17 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
     if (bn) *bn = 128;
     if (stream_k) *stream_k = S > 1 ? 1 : 0;
     if (generic) *generic = S;  // CAPMI_GEMM_X3W: the k-splits
+    return 0;
+  }
+  if (flags == CAPMI_GEMM_X3C) {
+    int tiles = 0;
+    const int rc = x3c_plan(prob, amode, bmode, tiles);
+    if (rc) return rc;
+    if (threads) *threads = 512;
+    if (bm) *bm = 256;
+    if (bn) *bn = 64;
+    if (stream_k) *stream_k = 0;
+    if (generic) *generic = tiles;
     return 0;
   }
   if (flags == CAPMI_GEMM_X3S) {
@@ -1004,6 +1016,17 @@ int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
   a.tiles_m[0] = (int)cdiv(p.M, 256);
   a.tiles_n[0] = (int)cdiv(p.N, 128);
   a.plain_epi = plain_epilogue(p, 128);
+  // the two-deep A pipeline (round 4, per-conv A/B at batch 64, one box): 4-9 % faster without the BN
+  // prologue and on the conv-mode prologue above layer4's 3136 rows; 1-5 % slower on the dense-row prologue
+  // (layer2/3 c3) and layer4's 3x3 -- those keep the one-deep loop. CAPMI_X3D_PIPE=0 / 1: off / on everywhere
+  {
+    static const int force = [] {
+      const char* e = getenv("CAPMI_X3D_PIPE");
+      return e ? atoi(e) : -1;
+    }();
+    const bool pro = p.in_scale != nullptr;
+    a.x3d_pipe = force >= 0 ? force : (!pro || (amode == CAPMI_A_CONV_NHWC && p.M > 3136)) ? 1 : 0;
+  }
   total = (long long)a.tiles_m[0] * a.tiles_n[0];
   a.tiles_begin[1] = (int)total;
   const long long slots = sk_cus();
@@ -1132,6 +1155,37 @@ int x3s_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long& ld
   return 0;
 }
 
+// CAPMI_GEMM_X3C (gemm_x3c.hip, round 4): the direct 3x3 conv for short channel axes (layer1)
+int x3c_plan(const capmi_gemm_problem* prob, int amode, int bmode, int& tiles) {
+  CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
+  const capmi_gemm_problem& p = *prob;
+  CAPMI_REQUIRE(amode == CAPMI_A_CONV_NHWC && bmode == CAPMI_B_NMAJOR_W, CAPMI_EINVAL);
+  CAPMI_REQUIRE(p.A && p.B && p.C && p.M >= 0 && p.N == 64 && p.ksplit == 1, CAPMI_EINVAL);
+  CAPMI_REQUIRE(p.cKH == 3 && p.cKW == 3 && p.cStride == 1 && p.cPad == 1 && p.cHo == p.cH && p.cWo == p.cW &&
+                    p.cCin % 32 == 0 && p.K == 9 * p.cCin && p.M == p.cN * p.cH * p.cW &&
+                    p.cW <= gemm_x3c_max_width(),
+                CAPMI_EINVAL);
+  CAPMI_REQUIRE(p.alpha == 1.f && p.alpha_ptr == nullptr && p.bias == nullptr && p.bias2 == nullptr && p.beta == 0.f &&
+                    !p.relu && p.c_r1 <= 0 && p.a_r1 <= 0 && p.ldc >= p.N && (long long)p.M * p.ldc * 4 < (1LL << 31),
+                CAPMI_EINVAL);
+  CAPMI_REQUIRE((p.in_scale == nullptr) == (p.in_shift == nullptr), CAPMI_EINVAL);
+  CAPMI_REQUIRE(aligned16(p.A) && aligned16(p.B) && p.ldb == p.K, CAPMI_EALIGN);
+  CAPMI_REQUIRE(p.in_scale == nullptr || (aligned16(p.in_scale) && aligned16(p.in_shift)), CAPMI_EALIGN);
+  CAPMI_REQUIRE((reinterpret_cast<uintptr_t>(p.stats) & 7u) == 0, CAPMI_EALIGN);
+  CAPMI_REQUIRE((long long)p.cN * p.cH * p.cW * p.cCin * 4 < (1LL << 31) && 3LL * p.N * p.ldb * 2 < (1LL << 31),
+                CAPMI_ERANGE);
+  tiles = (int)cdiv(p.M, 256);
+  return 0;
+}
+
+int gemm_x3c(const capmi_gemm_problem* prob, int amode, int bmode, hipStream_t s) {
+  int tiles = 0;
+  const int rc = x3c_plan(prob, amode, bmode, tiles);
+  if (rc) return rc;
+  if (prob->M == 0) return 0;
+  return gemm_x3c_launch(*prob, tiles, s);
+}
+
 int gemm_x3s(const capmi_gemm_problem* prob, int amode, int bmode, hipStream_t s) {
   long long lda = 0;
   int tiles = 0, grid = 0;
@@ -1176,6 +1230,7 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   if (flags == CAPMI_GEMM_X3D) return gemm_x3d(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3S) return gemm_x3s(prob, amode, bmode, as_stream(stream));
   if (flags == CAPMI_GEMM_X3W) return gemm_x3w(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
+  if (flags == CAPMI_GEMM_X3C) return gemm_x3c(prob, amode, bmode, as_stream(stream));
   int terms = flag_terms(flags);
   CAPMI_REQUIRE(terms >= 0, CAPMI_EINVAL);
   CAPMI_REQUIRE(terms_mode_ok(terms, amode, bmode), CAPMI_EINVAL);

@@ -24,6 +24,8 @@ struct GemmArgs {
   // stored through one buffer descriptor with per-row 32-bit offsets computed once per tile -- no
   // per-element 64-bit address, bounds branch, alpha / bias / beta / relu (round 3)
   int plain_epi;
+  // x3d (round 4): the two-deep A pipeline for this launch (the planner's rule, gemm.hip x3d_plan)
+  int x3d_pipe;
 };
 
 // Exact three-term bf16 split of two fp32 values (the x3 arithmetic: h0 = RNE(e), h1 = RNE(e - h0),
@@ -114,6 +116,10 @@ int gemm_x3s_launch(const capmi_gemm_problem& p, long long lda, int tiles, int g
 // conv weight gradients (gemm_x3w.hip): A = dY fp32 k rows, B = fp32 k rows (bmode 1) or the NHWC conv input's
 // implicit im2col (bmode 2), both split in-kernel; grid = tiles x S k-splits (a.kchunk[0] k-tiles each)
 int gemm_x3w_launch(const GemmArgs& a, int bmode, int blocks, hipStream_t s);
+// direct 3x3 conv (gemm_x3c.hip): N = 64, stride 1, pad 1, Cin % 32 == 0, W <= gemm_x3c_max_width(); one
+// workgroup per 256-pixel tile
+int gemm_x3c_launch(const capmi_gemm_problem& p, int tiles, hipStream_t s);
+int gemm_x3c_max_width();
 // resident workgroups per CU of the NT kernel for a tile shape (LDS / register bound)
 // (terms 3: three bf16 LDS planes per operand, 60 KB for 64x64 and >= 90 KB for the larger tiles)
 inline int gemm_nt_wg_per_cu(int bm, int bn, int terms = 0) {

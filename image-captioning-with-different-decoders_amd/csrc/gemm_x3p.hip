@@ -393,7 +393,7 @@ gemm_x3p_kernel(const GemmArgs args) {
 #ifndef X3D_PIPE
 #define X3D_PIPE 1
 #endif
-    if constexpr (ASPLIT && M16 && X3D_PIPE) {
+    if (ASPLIT && M16 && X3D_PIPE && args.x3d_pipe) {
       // x3d, round 4: A two k-tiles deep in ONE register set. During tile kt's MFMAs each of the thread's four
       // float4 slots is split into the other buffer for tile kt + 1 and at once reloaded with tile kt + 2's
       // (its BN scale / shift and the conv walk follow after the fourth slot): the A load has a whole k-tile to

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 22
+#define CAPMI_ABI_VERSION 23
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -156,6 +156,13 @@ int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int t
  * capmi_gemm_sk's) and are summed in a fixed order (capmi_splitk_reduce); capmi_gemm_sk_plan reports the
  * split count in `generic`. */
 #define CAPMI_GEMM_X3W 128
+/* CAPMI_GEMM_X3C (alone, ABI 23): DIRECT 3x3 convolution in the CAPMI_GEMM_X3 arithmetic for short-channel
+ * layers (layer1's 3x3): CAPMI_A_CONV_NHWC with KH = KW = 3, stride 1, pad 1, Cin % 32 == 0, W <= 64, the
+ * optional BN-apply + ReLU prologue; N == 64; B = the weight's three bf16 planes in CAPMI_GEMM_X3P's packed k
+ * order (ldb == K); C = A.B only (alpha 1, no bias / beta / relu / remap / ksplit) with the optional `stats`.
+ * Each tile of 256 output pixels splits the input rows it touches once per 32-channel slice and reads the nine
+ * taps from that image (the k order and products of CAPMI_GEMM_X3P). The workspace is not used (may be NULL). */
+#define CAPMI_GEMM_X3C 256
 /* CAPMI_GEMM_SPLIT3 (alone): fp32 A and B, both split exactly into three bf16 terms when staged to
  * LDS (the CAPMI_GEMM_X3 arithmetic with no pre-split operand: fp32-accurate on the bf16 matrix
  * cores). Dense modes only: CAPMI_A_KMAJOR x CAPMI_B_NMAJOR_W / CAPMI_B_KROWS and CAPMI_A_MMAJOR x

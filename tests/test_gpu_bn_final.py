@@ -17,15 +17,22 @@ def _K():
 
 def bn_final_ref(stats, count, gamma, beta, rm, rv, momentum, eps):
     """numpy restatement of csrc/bn_final.h (bnf_group + bnf_apply): q_l = sum over slices t = l (mod 64) in
-    ascending t, sum = q_0 + ... + q_63 (fp64, sequential), then the finalize arithmetic op by op."""
+    ascending t, r_w = q_8w + ... + q_8w+7, sum = r_0 + ... + r_7 (fp64, each sequential), then the finalize
+    arithmetic op by op."""
     st = stats.astype(np.float64)  # (T, C, 2)
     T, C, _ = st.shape
-    tot = np.zeros((C, 2))
+    q = []
     for l_ in range(64):
         acc = np.zeros((C, 2))
         for t in range(l_, T, 64):
             acc = acc + st[t]
-        tot = tot + acc
+        q.append(acc)
+    tot = np.zeros((C, 2))
+    for w in range(8):
+        r = np.zeros((C, 2))
+        for s8 in range(8):
+            r = r + q[8 * w + s8]
+        tot = tot + r
     n = float(count)
     mean = tot[:, 0] / n
     var = tot[:, 1] / n - mean * mean

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--x3p", action="store_true", help="x3 with the A operand pre-split too (CAPMI_GEMM_X3P)")
     ap.add_argument("--x3d", action="store_true", help="x3 with the fp32 A split in-kernel, B by LDS-DMA (CAPMI_GEMM_X3D)")
     ap.add_argument("--x3s", action="store_true", help="short-k streaming x3 kernel (gemm_x3s.hip)")
+    ap.add_argument("--x3c", action="store_true", help="the direct 3x3 conv (gemm_x3c.hip; N = 64, stride 1)")
     ap.add_argument("--x3w", action="store_true", help="the conv's WEIGHT gradient on gemm_x3w.hip (dW = dY^T im2col(X))")
     a = ap.parse_args()
     dev = "cuda"
@@ -94,6 +95,12 @@ def main():
         prob.B = w3.data_ptr()
         print("x3s kernel:", K.gemm_x3s_kernel_name(prob, mode))
         run = lambda: K.gemm_x3s(prob, mode)  # noqa: E731
+    elif a.x3c:
+        w3 = torch.empty(3 * w.numel(), device=dev, dtype=torch.bfloat16)
+        K.split3_bf16(K.conv_weight_order_x3p(w, k, k, ci).contiguous(), w3)
+        prob.B = w3.data_ptr()
+        print("x3c kernel:", K.gemm_x3c_kernel_name(prob))
+        run = lambda: K.gemm_x3c(prob)  # noqa: E731
     elif a.x3w:  # dW[co][k*k*ci] = sum over output pixels of dY[p][co] x im2col(relu(bn(x)))[p][n]
         from capmi._lib import CAPMI_B_CONV_NHWC, CAPMI_B_KROWS
         dy = torch.rand(M, co, device=dev, generator=g) - 0.5

@@ -40,18 +40,27 @@ def main():
     a = ap.parse_args()
     f = per_kernel(a.fetch_db, "FETCH_SIZE")
     w = per_kernel(a.write_db, "WRITE_SIZE")
-    out = {}
+    out, dropped = {}, {}
     for k in sorted(set(f) & set(w), key=lambda k: -(f[k][1] + w[k][1])):
         nf, vf = f[k]
         nw, vw = w[k]
         fkb, wkb = vf / nf, vw / nw
+        # (round 4) a kernel whose FETCH or WRITE counter did not land in its pass reads as
+        # ~0 KB per launch although every kernel here reads its operands: such rows are not evidence -- drop
+        # them (listed under "dropped") instead of reporting a traffic figure built from one counter
+        if fkb < 1.0 or nf != nw:
+            dropped[k] = {"launches_fetch_pass": nf, "launches_write_pass": nw, "fetch_kb_per_launch": round(fkb, 3),
+                          "write_kb_per_launch": round(wkb, 1), "reason": "FETCH_SIZE not landed (< 1 KB per launch)"
+                          if fkb < 1.0 else "launch counts differ between the passes"}
+            continue
+        hbm = round((2 * round(fkb, 1) + round(wkb, 1)) * 1024)  # exactly 2 F + W of the printed F and W
         out[k] = {"launches": nf, "fetch_kb_per_launch": round(fkb, 1), "write_kb_per_launch": round(wkb, 1),
-                  "hbm_bytes_per_launch": round((2 * fkb + wkb) * 1024)}
+                  "hbm_bytes_per_launch": hbm}
     print(json.dumps({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes)",
                       "command": a.command,
                       "formula": "2*FETCH_SIZE + WRITE_SIZE (KB -> bytes), gfx950 FETCH_SIZE = half the bytes "
                                  "of wide coalesced reads; Infinity-Cache hits included",
-                      "kernels": out}, indent=1))
+                      "kernels": out, "dropped": dropped}, indent=1))
 
 
 if __name__ == "__main__":
