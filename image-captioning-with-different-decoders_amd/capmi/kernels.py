@@ -202,7 +202,7 @@ def gemm_x3s(prob, amode):
 
 
 def gemm_x3c(prob):
-    """CAPMI_GEMM_X3C: the direct 3x3 / stride-1 conv (N = 64, Cin % 32 == 0, W <= 64, optional BN prologue) x
+    """CAPMI_GEMM_X3C: the direct 3x3 / stride-1 conv (N = 64, Cin % 32 == 0, W <= 64, the staged band within LDS, optional BN prologue) x
     B = three bf16 planes in the x3p k order; store-only epilogue, no workspace."""
     call("capmi_gemm_sk_ex", ctypes.byref(prob), CAPMI_A_CONV_NHWC, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3C,
          None, 0, stream())

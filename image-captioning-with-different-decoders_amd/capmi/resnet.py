@@ -270,6 +270,8 @@ class EncoderRunner:
             w3 = self._packed_x3(conv, tap_inner=True)
             sc, sh = in_ss if in_ss is not None else (None, None)
             prob = K.problem(rows, co, Kd, x, 0, w3, Kd, out, co, conv=geo, in_scale=sc, in_shift=sh, **kw_)
+            x3c = K.gemm_x3c_ok(prob)  # (the planner also bounds the staged band: many tiny images do not fit)
+        if x3c:
             launch = lambda: K.gemm_x3c(prob)  # noqa: E731
             if self.conv_hook is not None:
                 self.conv_hook(tag, 2.0 * rows * co * Kd, launch, K.gemm_x3c_kernel_name(prob))

@@ -1174,6 +1174,7 @@ int x3c_plan(const capmi_gemm_problem* prob, int amode, int bmode, int& tiles) {
   CAPMI_REQUIRE((reinterpret_cast<uintptr_t>(p.stats) & 7u) == 0, CAPMI_EALIGN);
   CAPMI_REQUIRE((long long)p.cN * p.cH * p.cW * p.cCin * 4 < (1LL << 31) && 3LL * p.N * p.ldb * 2 < (1LL << 31),
                 CAPMI_ERANGE);
+  CAPMI_REQUIRE(gemm_x3c_band_fits(p), CAPMI_EINVAL);  // (e.g. many 1-row images per tile)
   tiles = (int)cdiv(p.M, 256);
   return 0;
 }

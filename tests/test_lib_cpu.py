@@ -139,6 +139,25 @@ def test_gemm_sk_plan_on_host():
     assert wgrad_plan(256, 256, 3)[:2] == (128, 128)  # wide 3x3 weight gradient
     assert wgrad_plan(1024, 256, 1)[:2] == (128, 64)  # 1x1 weight gradient
 
+    def x3c_plan(n, h, w, Cin=64):
+        # CAPMI_GEMM_X3C (256): layer1's direct 3x3; the padded band of a 256-pixel tile must fit its LDS
+        p = GemmProblem()
+        p.M, p.N, p.K, p.ksplit = n * h * w, 64, 9 * Cin, 1
+        p.A = p.B = p.C = 256
+        p.ldb, p.ldc, p.alpha = 9 * Cin, 64, 1.0
+        p.cN, p.cH, p.cW, p.cCin, p.cKH, p.cKW = n, h, w, Cin, 3, 3
+        p.cStride, p.cPad, p.cHo, p.cWo = 1, 1, h, w
+        v = [c_int(0) for _ in range(5)]
+        rc = lib.capmi_gemm_sk_plan(ctypes.byref(p), 2, 0, 3, 256, *[ctypes.byref(x) for x in v])
+        return rc, tuple(x.value for x in v)
+
+    rc, (bm, bn, sk, tiles, nt) = x3c_plan(50, 56, 56)
+    assert rc == 0 and (bm, bn, sk, nt) == (256, 64, 0, 512) and tiles == 50 * 3136 // 256 + 1
+    assert x3c_plan(5, 7, 7)[0] == 0 and x3c_plan(1, 64, 64)[0] == 0
+    assert x3c_plan(2, 66, 66)[0] == 1001  # W > 64
+    assert x3c_plan(64, 1, 32)[0] == 1001  # eight 1-row images per tile: 24 padded rows x 34 > 640 positions
+    assert x3c_plan(4, 56, 56, Cin=48)[0] == 1001  # Cin % 32 != 0
+
 
 def test_device_tensors_required():
     from capmi import kernels as K
