@@ -47,6 +47,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_c(const void* p, unsigned
 // exhaustive check over the 64 shifts); gemm_x3p's row swizzle, conflict-free for 16-aligned rows, is not here
 // (SQ: 37.6 % LDS bank conflicts, 119-121 us), nor was c ^ (q & 3)
 __device__ __forceinline__ int apos_off(int q, int c) { return q * 64 + ((c ^ (((q >> 2) & 1) << 1)) << 4); }
+// The workgroup barrier of the tap loop. __syncthreads() here compiled to `s_waitcnt vmcnt(0)` + s_barrier
+// (its release fence waits for the LDS-DMA and the next slice's staging loads), so every tap drained the DMAs
+// issued two taps ahead and the staging loads at once; this barrier waits only for the wave's LDS operations
+// (its ds_writes / ds_reads), the counted `s_waitcnt vmcnt` before it retiring the DMA the next tap reads.
+// The asm's memory clobber keeps the compiler from moving LDS accesses across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 // weight rows: gemm_x3p's 16x16x32 swizzle (slot pattern [0, 2, 3, 1][(r >> 2) & 3])
 __device__ __forceinline__ int bswz(int r) { return (0x1320 >> (4 * ((r >> 2) & 3))) & 3; }
 
@@ -221,11 +227,11 @@ gemm_x3c_kernel(const capmi_gemm_problem P) {
       } else {
         asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
       }
-      __syncthreads();
+      lds_barrier();
     }
     if (s + 1 < nslice) {  // every wave is past the slice's last tap (barrier above): the band is free
       stage_write();
-      __syncthreads();
+      lds_barrier();
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the DMAs past the last tap)
