@@ -201,18 +201,11 @@ def gemm_x3s(prob, amode):
          None, 0, stream())
 
 
-def gemm_x3c(prob, workspace=None):
-    """CAPMI_GEMM_X3C: the direct 3x3 / stride-1 conv (Cin % 32 == 0, the staged band within LDS, optional BN
-    prologue) x B = three bf16 planes in the x3p k order; store-only epilogue. N = 64: no workspace; N % 128 == 0
-    (the wide form): stream-K over (tile, channel slice) units, parked partials in `workspace`
-    (gemm_workspace)."""
-    if prob.N != 64:
-        _cuda(workspace, dtype=torch.int32)
-        wp, wb = ptr(workspace), workspace.numel() * 4
-    else:
-        wp, wb = None, 0
+def gemm_x3c(prob):
+    """CAPMI_GEMM_X3C: the direct 3x3 / stride-1 conv (N = 64, Cin % 32 == 0, W <= 64, the staged band within LDS, optional BN prologue) x
+    B = three bf16 planes in the x3p k order; store-only epilogue, no workspace."""
     call("capmi_gemm_sk_ex", ctypes.byref(prob), CAPMI_A_CONV_NHWC, CAPMI_B_NMAJOR_W, CAPMI_TILE_AUTO, CAPMI_GEMM_X3C,
-         wp, wb, stream())
+         None, 0, stream())
 
 
 def gemm_x3c_ok(prob):
@@ -223,7 +216,7 @@ def gemm_x3c_ok(prob):
 
 
 def gemm_x3c_kernel_name(prob):
-    return f"gemm_x3c{'' if prob.N == 64 else 'w'}_kernel<{'true' if prob.in_scale else 'false'}>"
+    return f"gemm_x3c_kernel<{'true' if prob.in_scale else 'false'}>"
 
 
 def gemm_x3w(prob, bmode, workspace):

@@ -741,10 +741,10 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
     int tiles = 0;
     const int rc = x3c_plan(prob, amode, bmode, tiles);
     if (rc) return rc;
-    if (threads) *threads = prob->N == 64 ? 512 : 256;
+    if (threads) *threads = 512;
     if (bm) *bm = 256;
-    if (bn) *bn = prob->N == 64 ? 64 : 128;
-    if (stream_k) *stream_k = prob->N == 64 ? 0 : 1;
+    if (bn) *bn = 64;
+    if (stream_k) *stream_k = 0;
     if (generic) *generic = tiles;
     return 0;
   }
@@ -1155,15 +1155,12 @@ int x3s_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long& ld
   return 0;
 }
 
-// CAPMI_GEMM_X3C (gemm_x3c.hip, round 4): the direct 3x3 / stride-1 conv. N = 64 (layer1): one workgroup per
-// 256-pixel tile (`tiles`); N % 128 == 0 (layers 2-4, the wide form): 256 x 128 tiles, stream-K over
-// (tile, 32-channel slice) units on `tiles` = min(CUs, units) workers, parked partials in the workspace
+// CAPMI_GEMM_X3C (gemm_x3c.hip, round 4): the direct 3x3 conv for short channel axes (layer1)
 int x3c_plan(const capmi_gemm_problem* prob, int amode, int bmode, int& tiles) {
   CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
   const capmi_gemm_problem& p = *prob;
   CAPMI_REQUIRE(amode == CAPMI_A_CONV_NHWC && bmode == CAPMI_B_NMAJOR_W, CAPMI_EINVAL);
-  CAPMI_REQUIRE(p.A && p.B && p.C && p.M >= 0 && (p.N == 64 || (p.N > 0 && p.N % 128 == 0)) && p.ksplit == 1,
-                CAPMI_EINVAL);
+  CAPMI_REQUIRE(p.A && p.B && p.C && p.M >= 0 && p.N == 64 && p.ksplit == 1, CAPMI_EINVAL);
   CAPMI_REQUIRE(p.cKH == 3 && p.cKW == 3 && p.cStride == 1 && p.cPad == 1 && p.cHo == p.cH && p.cWo == p.cW &&
                     p.cCin % 32 == 0 && p.K == 9 * p.cCin && p.M == p.cN * p.cH * p.cW &&
                     p.cW <= gemm_x3c_max_width(),
@@ -1179,33 +1176,15 @@ int x3c_plan(const capmi_gemm_problem* prob, int amode, int bmode, int& tiles) {
                 CAPMI_ERANGE);
   CAPMI_REQUIRE(gemm_x3c_band_fits(p), CAPMI_EINVAL);  // (e.g. many 1-row images per tile)
   tiles = (int)cdiv(p.M, 256);
-  if (p.N != 64) {
-    const long long units = (long long)tiles * (p.N / 128) * (p.cCin / 32);
-    tiles = (int)std::min<long long>(sk_cus(), units);
-  }
   return 0;
 }
 
-int gemm_x3c(const capmi_gemm_problem* prob, int amode, int bmode, void* workspace, long long ws_bytes,
-             hipStream_t s) {
+int gemm_x3c(const capmi_gemm_problem* prob, int amode, int bmode, hipStream_t s) {
   int tiles = 0;
   const int rc = x3c_plan(prob, amode, bmode, tiles);
   if (rc) return rc;
   if (prob->M == 0) return 0;
-  if (prob->N == 64) return gemm_x3c_launch(*prob, tiles, s);
-  CAPMI_REQUIRE(workspace != nullptr && aligned16(workspace), CAPMI_EINVAL);
-  CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
-  GemmArgs a;
-  memset(&a, 0, sizeof(a));
-  a.nprob = 1;
-  a.p[0] = *prob;
-  a.tiles_m[0] = (int)cdiv(prob->M, 256);
-  a.tiles_n[0] = prob->N / 128;
-  a.sk_units = (long long)a.tiles_m[0] * a.tiles_n[0] * (prob->cCin / 32);
-  a.sk_workers = tiles;
-  a.sk_flags = static_cast<int*>(workspace);
-  a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cu_count()));
-  return gemm_x3cw_launch(a, tiles, s);
+  return gemm_x3c_launch(*prob, tiles, s);
 }
 
 int gemm_x3s(const capmi_gemm_problem* prob, int amode, int bmode, hipStream_t s) {
@@ -1252,7 +1231,7 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   if (flags == CAPMI_GEMM_X3D) return gemm_x3d(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3S) return gemm_x3s(prob, amode, bmode, as_stream(stream));
   if (flags == CAPMI_GEMM_X3W) return gemm_x3w(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
-  if (flags == CAPMI_GEMM_X3C) return gemm_x3c(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
+  if (flags == CAPMI_GEMM_X3C) return gemm_x3c(prob, amode, bmode, as_stream(stream));
   int terms = flag_terms(flags);
   CAPMI_REQUIRE(terms >= 0, CAPMI_EINVAL);
   CAPMI_REQUIRE(terms_mode_ok(terms, amode, bmode), CAPMI_EINVAL);

@@ -120,8 +120,6 @@ int gemm_x3w_launch(const GemmArgs& a, int bmode, int blocks, hipStream_t s);
 // workgroup per 256-pixel tile
 int gemm_x3c_launch(const capmi_gemm_problem& p, int tiles, hipStream_t s);
 int gemm_x3c_max_width();
-// its wide form (N % 128 == 0): 256 x 128 tiles, stream-K over (tile, slice) units on `workers` workgroups
-int gemm_x3cw_launch(const GemmArgs& a, int workers, hipStream_t s);
 bool gemm_x3c_band_fits(const capmi_gemm_problem& p);
 // resident workgroups per CU of the NT kernel for a tile shape (LDS / register bound)
 // (terms 3: three bf16 LDS planes per operand, 60 KB for 64x64 and >= 90 KB for the larger tiles)

@@ -278,328 +278,6 @@ gemm_x3c_kernel(const capmi_gemm_problem P) {
   }
 }
 
-
-// ---------------------------------------------------------------------------------------------------------------
-// The wide form ("x3cw", round 4): the 3x3 / stride-1 convs of layers 2-4 (N a multiple of 128; layer3's 3x3
-// is the headline's dominant conv), in place of bn_relu_split3 + gemm_x3p. gemm_x3p's implicit GEMM re-stages
-// the A operand for every tap by LDS-DMA: 72 KiB per 32-deep k-tile and CU (48 KiB of A, 24 of B), 508 MB per
-// layer3 launch through L2 / MALL; timed with zero-size descriptors (no memory traffic, same instructions) the
-// launch fell from 89.9 to 69.1 us (tools/r04/run12.sh). Here the band is staged once per 32-channel slice
-// (from the fp32 input, BN-applied and split in registers as above: no separate split pass) and only the
-// weight's 128 x 32 tap block (24 KiB) streams per k-tile: 2.3 instead of 5.2 MB per tile and launch.
-// Tile 256 x 128 on FOUR waves (one per SIMD), wave tile 64 x 128: per tap 12 + 24 ds_read_b128 feed 192 MFMAs,
-// and the 512-entry register file of a lone wave holds the 128 accumulators, 24 weight fragments and the
-// next slice's staged band (eight waves of 64 x 64 spilled at their 256-register cap).
-// Work unit = (tile, slice); stream-K over the units with gemm_x3p's parked-partial hand-off (sk_publish /
-// sk_consume), one workgroup per CU.
-constexpr int WNT = 256;                          // threads
-constexpr int WBN = 128;
-constexpr int WCPOS = 464;                        // staged band positions (LDS: 3 x 29 KiB + 72 KiB weight ring)
-constexpr int WCA_PLANE = WCPOS * 64;
-constexpr int WCB_PLANE = WBN * 64;               // 128 x 32 bf16 per plane
-constexpr int WCB_BUF = 3 * WCB_PLANE;            // 24 KiB
-constexpr int WCPF = (WCPOS * 8 + WNT - 1) / WNT;  // float4 loads per thread per slice (15)
-constexpr int WDMA = 3 * WBN / 16 / 4;            // weight DMA wave-instructions per wave and tap (6)
-
-template <bool PRO>
-__global__ void __launch_bounds__(WNT) __attribute__((amdgpu_waves_per_eu(1)))
-gemm_x3cw_kernel(const GemmArgs args) {
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[3 * WCA_PLANE + CB_NBUF * WCB_BUF];
-  unsigned char* const Al = lds;
-  unsigned char* const Bl = lds + 3 * WCA_PLANE;
-  const capmi_gemm_problem& P = args.p[0];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm0 = wid * 64;
-  const int M = P.M, N = P.N, H = P.cH, W = P.cW, Cin = P.cCin;
-  const int Hp = H + 2, Wp = W + 2;
-  const int c16 = lane >> 4, r16 = lane & 15;
-  const int nslice = Cin / 32;
-  const int tiles_n = args.tiles_n[0];
-
-  const auto rx = rsrc_c(P.A, (unsigned)((long long)P.cN * H * W * Cin * 4));
-  const auto rb = rsrc_c(P.B, (unsigned)(3LL * N * P.ldb * 2));
-  const unsigned ss_bytes = PRO ? (unsigned)(Cin * 4) : 0u;
-  const auto rsc = rsrc_c(PRO ? (const void*)P.in_scale : P.B, ss_bytes);
-  const auto rsh = rsrc_c(PRO ? (const void*)P.in_shift : P.B, ss_bytes);
-  const unsigned pB2 = (unsigned)((long long)N * P.ldb * 2);
-  // weight DMA: wave w moves row blocks 2 w, 2 w + 1 (16 rows x 64 B each: row 16 b + lane / 4, slot lane % 4)
-  // of each plane
-  const int drow = lane >> 2, dslot = lane & 3;
-  const int ch8 = (tid & 7) * 4;
-
-  auto prow = [&](int p) {
-    const int g = p / W, n = g / H;
-    return n * Hp + (g - n * H) + 1;
-  };
-
-  f32x4_c acc[4][8];
-  float4 pf[WCPF];
-  float4 pf_sc = make_float4(1.f, 1.f, 1.f, 1.f), pf_sh = make_float4(0.f, 0.f, 0.f, 0.f);
-  unsigned soff[WCPF];
-  int fq[4];
-
-  // one segment: slices [ks, ke) of tile (tm, tn) into acc
-  auto segment = [&](int tm, int tn, int ks, int ke) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_c{0.f, 0.f, 0.f, 0.f};
-    const int p0 = tm * CBM, n0 = tn * WBN;
-    const int rmin = prow(p0) - 1;
-    const int npos = (prow(min(p0 + CBM, M) - 1) + 2 - rmin) * Wp;
-    // (an opaque copy of the thread index: the per-slot position arithmetic below is the same for every
-    // segment, and hoisted out of the stream-K loop it held ~50 registers for the whole kernel)
-    int tq = tid;
-    asm volatile("" : "+v"(tq));
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int p = p0 + wm0 + 16 * i + (tq & 15);
-      fq[i] = p < M ? (prow(p) - rmin) * Wp + (p % W) + 1 : Wp + 1;
-    }
-#pragma unroll
-    for (int j = 0; j < WCPF; ++j) {
-      const int q = (tq >> 3) + (WNT / 8) * j;
-      const int br = q / Wp, c = q - br * Wp;
-      const int R = rmin + br, n = R / Hp, ih = R - n * Hp - 1, iw = c - 1;
-      const bool ok = q < npos && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W && n < P.cN;
-      soff[j] = ok ? (unsigned)((((long long)(n * H + ih) * W + iw) * Cin + ch8) * 4) : kOOBc;
-    }
-    unsigned b_base[2];
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int r = (2 * wid + b) * 16 + drow;
-      b_base[b] = (unsigned)(((long long)(n0 + r) * P.ldb + ((dslot ^ bswz(r)) * 8)) * 2);
-    }
-    auto b_dma = [&](int kt, int buf) {
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const unsigned off = b_base[b] + (unsigned)(kt * 32) * 2u;
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              rb, (lds_ptr_c)(Bl + buf * WCB_BUF + p * WCB_PLANE + (2 * wid + b) * 1024), 16, off + p * pB2, 0, 0, 0);
-      }
-    };
-    auto stage_load = [&](int s) {
-      if (PRO) {
-        const unsigned ch = (unsigned)(s * 32 + ch8) * 4u;
-        pf_sc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsc, ch, 0, 0));
-        pf_sh = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsh, ch, 0, 0));
-      }
-#pragma unroll
-      for (int j = 0; j < WCPF; ++j)
-        pf[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                                               rx, soff[j] == kOOBc ? kOOBc : soff[j] + (unsigned)s * 128u, 0, 0));
-    };
-    auto stage_write = [&]() {
-#pragma unroll
-      for (int j = 0; j < WCPF; ++j) {
-        const int q = (tid >> 3) + (WNT / 8) * j;
-        if (q >= npos) break;
-        float4 x = pf[j];
-        if (PRO) x = make_float4(fmaxf(fmaf(x.x, pf_sc.x, pf_sh.x), 0.f), fmaxf(fmaf(x.y, pf_sc.y, pf_sh.y), 0.f),
-                                 fmaxf(fmaf(x.z, pf_sc.z, pf_sh.z), 0.f), fmaxf(fmaf(x.w, pf_sc.w, pf_sh.w), 0.f));
-        if (soff[j] == kOOBc) x = make_float4(0.f, 0.f, 0.f, 0.f);
-        unsigned lo[3], hi[3];
-        split3_pair(x.x, x.y, lo);
-        split3_pair(x.z, x.w, hi);
-        const int c8 = tid & 7;
-        const int o = apos_off(q, c8 >> 1) + (c8 & 1) * 8;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(Al + p * WCA_PLANE + o) = make_uint2(lo[p], hi[p]);
-      }
-    };
-    const int kt0 = ks * 9, kt1 = ke * 9;
-    b_dma(kt0, 0);
-    b_dma(kt0 + 1, 1);  // (a segment has at least one slice: nine taps)
-    stage_load(ks);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stage_write();
-    lds_barrier();
-    // one wave per SIMD: every LDS read is issued a pair of column blocks (48 MFMAs) ahead of its use -- the
-    // next pair's weight fragments during this pair's MFMAs, the next tap's A fragments (the band does not
-    // change within a slice) during the last pair's
-    bf16x8_c a[4][3], an[4][3];
-    auto a_read = [&](bf16x8_c (&dst)[4][3], int tap) {
-      const int kh = tap / 3, kw = tap - kh * 3;
-      const int dq = (kh - 1) * Wp + (kw - 1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int o = apos_off(fq[i] + dq, c16);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) dst[i][p] = *reinterpret_cast<const bf16x8_c*>(Al + p * WCA_PLANE + o);
-      }
-    };
-    auto b_read = [&](bf16x8_c (&dst)[2][3], const unsigned char* B_, int jp) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int r = 32 * jp + 16 * j + r16;
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          dst[j][p] = *reinterpret_cast<const bf16x8_c*>(B_ + p * WCB_PLANE + r * 64 + ((c16 ^ bswz(r)) << 4));
-      }
-    };
-    a_read(a, 0);
-    int bcur = 0, kt = kt0;
-#pragma nounroll
-    for (int s = ks; s < ke; ++s) {
-#pragma nounroll
-      for (int tap = 0; tap < 9; ++tap, ++kt) {
-        const int buf = bcur;
-        const int bnext = bcur == 0 ? 2 : bcur - 1;
-        b_dma(kt + 2 < kt1 ? kt + 2 : 1 << 20, bnext);
-        bcur = bcur == 2 ? 0 : bcur + 1;
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        if (tap == 0 && s + 1 < ke) stage_load(s + 1);
-        const unsigned char* B_ = Bl + buf * WCB_BUF;
-        bf16x8_c b[2][3], bn[2][3];
-        b_read(b, B_, 0);
-#pragma unroll
-        for (int jp = 0; jp < 4; ++jp) {
-          __builtin_amdgcn_sched_barrier(0);
-          if (jp < 3)
-            b_read(bn, B_, jp + 1);
-          else if (tap < 8)
-            a_read(an, tap + 1);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {  // gemm_x3p's product order per accumulator
-              f32x4_c& c = acc[i][2 * jp + j];
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][1], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][2], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[j][0], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][1], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][0], c, 0, 0, 0);
-              c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][0], c, 0, 0, 0);
-            }
-          }
-          if (jp < 3) {
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-              for (int p = 0; p < 3; ++p) b[j][p] = bn[j][p];
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        // the next tap's weight block (WDMA wave-instructions) was issued before this tap's DMA and, in the
-        // slice's first two taps, before the next slice's WCPF (+ 2) staging loads
-        if (tap <= 1 && s + 1 < ke) {
-          if (PRO)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WDMA + WCPF + 2) : "memory");
-          else
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WDMA + WCPF) : "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WDMA) : "memory");
-        }
-        lds_barrier();
-        if (tap < 8) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int p = 0; p < 3; ++p) a[i][p] = an[i][p];
-        }
-      }
-      if (s + 1 < ke) {
-        stage_write();
-        lds_barrier();
-        a_read(a, 0);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the DMAs past the segment's last tap)
-  };
-
-  // store-only epilogue with the per-64-row statistics (rows past M read band data: zeroed, stores dropped)
-  auto epilogue = [&](int tm, int tn) {
-    const int p0 = tm * CBM, n0 = tn * WBN;
-    const auto rc = rsrc_c(P.C, (unsigned)((long long)M * P.ldc * 4));
-    const int cl = lane & 15, rq = lane >> 4;
-    unsigned roff[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = p0 + wm0 + 16 * i + 4 * rq + r;
-        roff[i][r] = row < M ? (unsigned)row * (unsigned)P.ldc * 4u : kOOBc;
-      }
-    float* __restrict__ stats = P.stats;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const unsigned cb = (unsigned)(n0 + 16 * j + cl) * 4u;
-      float cs = 0.f, cq = 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = roff[i][r] == kOOBc ? 0.f : acc[i][j][r];
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, roff[i][r] + cb, 0, 0);
-          cs += v;
-          cq = fmaf(v, v, cq);
-        }
-      if (stats != nullptr) {
-        cs += __shfl_xor(cs, 16, 64);
-        cq += __shfl_xor(cq, 16, 64);
-        cs += __shfl_xor(cs, 32, 64);
-        cq += __shfl_xor(cq, 32, 64);
-        if (rq == 0 && p0 + wm0 < M) {
-          const long long sl = (p0 + wm0) >> 6;
-          const int col = n0 + 16 * j + cl;
-          stats[(sl * N + col) * 2 + 0] = cs;
-          stats[(sl * N + col) * 2 + 1] = cq;
-        }
-      }
-    }
-  };
-
-  // stream-K over the (tile, slice) units: worker w takes units [w U / G, (w + 1) U / G) (workers numbered so
-  // that neighbours -- the partners of a split tile -- sit on one XCD), its tiles from the last to the first:
-  // a segment that ends inside its tile parks its partial, the segment that ends the tile adds the parked
-  // partials of the workers before it (x3p's schedule and hand-off)
-  const int nwg = gridDim.x;
-  int w;
-  {
-    const int q = nwg >> 3, r = nwg & 7, x = blockIdx.x & 7;
-    w = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (blockIdx.x >> 3);
-  }
-  const int U = (int)args.sk_units;  // (host: units < 2^31 / 256)
-  const int u0 = w * U / nwg, u1 = (w + 1) * U / nwg;
-  constexpr int PART = CBM * WBN;
-  int* flags = args.sk_flags;
-  if (u0 >= u1) return;
-  for (int t = (u1 - 1) / nslice; t >= u0 / nslice; --t) {
-    const int tb = t * nslice;
-    const int ks = max(u0, tb) - tb, ke = min(u1, tb + nslice) - tb;
-    const int tm = t / tiles_n, tn = t - tm * tiles_n;
-    segment(tm, tn, ks, ke);
-    if (ke < nslice) {
-      const auto rs = rsrc_c(args.sk_part + (long long)w * PART, PART * 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c, acc[i][j]), rs,
-                                                 ((i * 8 + j) * WNT + tid) * 16, 0, 16 /* SC1: write-through */);
-      sk_publish(flags + w, tid);
-      continue;
-    }
-    if (ks > 0) {
-      for (int w2 = w - 1;; --w2) {
-        sk_consume(flags + w2, flags + nwg, tid);
-        const auto rs = rsrc_c(args.sk_part + (long long)w2 * PART, PART * 4);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            acc[i][j] += __builtin_bit_cast(
-                f32x4_c, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i * 8 + j) * WNT + tid) * 16, 0, 16));
-        if (w2 * U / nwg <= tb) break;
-      }
-    }
-    epilogue(tm, tn);
-  }
-}
 }  // namespace
 
 int gemm_x3c_launch(const capmi_gemm_problem& p, int tiles, hipStream_t s) {
@@ -612,22 +290,11 @@ int gemm_x3c_launch(const capmi_gemm_problem& p, int tiles, hipStream_t s) {
   return 0;
 }
 
-int gemm_x3cw_launch(const GemmArgs& a, int workers, hipStream_t s) {
-  const dim3 g(workers), b(WNT);
-  if (a.p[0].in_scale)
-    CAPMI_KLAUNCH((gemm_x3cw_kernel<true>), g, b, 0, s, a);
-  else
-    CAPMI_KLAUNCH((gemm_x3cw_kernel<false>), g, b, 0, s, a);
-  CAPMI_LAUNCH_CHECK();
-  return 0;
-}
-
 int gemm_x3c_max_width() { return CW_MAX; }
 
 // every tile's staged band (its padded rows x (W + 2)) fits the CPOS positions of LDS -- the kernel's npos, for
 // each tile (a few hundred tiles; the host runs it once per plan)
 bool gemm_x3c_band_fits(const capmi_gemm_problem& p) {
-  const int cpos = p.N == CBN ? CPOS : WCPOS;
   const long long H = p.cH, W = p.cW, Hp = H + 2, Wp = W + 2, M = p.M;
   auto prow = [&](long long q) {
     const long long g = q / W, n = g / H;
@@ -635,7 +302,7 @@ bool gemm_x3c_band_fits(const capmi_gemm_problem& p) {
   };
   for (long long p0 = 0; p0 < M; p0 += CBM) {
     const long long last = (p0 + CBM < M ? p0 + CBM : M) - 1;
-    if ((prow(last) + 2 - (prow(p0) - 1)) * Wp > cpos) return false;
+    if ((prow(last) + 2 - (prow(p0) - 1)) * Wp > CPOS) return false;
   }
   return true;
 }

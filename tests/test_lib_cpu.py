@@ -158,23 +158,6 @@ def test_gemm_sk_plan_on_host():
     assert x3c_plan(64, 1, 32)[0] == 1001  # eight 1-row images per tile: 24 padded rows x 34 > 640 positions
     assert x3c_plan(4, 56, 56, Cin=48)[0] == 1001  # Cin % 32 != 0
 
-    def x3cw_plan(n, h, Cin, N):
-        p = GemmProblem()
-        p.M, p.N, p.K, p.ksplit = n * h * h, N, 9 * Cin, 1
-        p.A = p.B = p.C = 256
-        p.ldb, p.ldc, p.alpha = 9 * Cin, N, 1.0
-        p.cN, p.cH, p.cW, p.cCin, p.cKH, p.cKW = n, h, h, Cin, 3, 3
-        p.cStride, p.cPad, p.cHo, p.cWo = 1, 1, h, h
-        v = [c_int(0) for _ in range(5)]
-        rc = lib.capmi_gemm_sk_plan(ctypes.byref(p), 2, 0, 3, 256, *[ctypes.byref(x) for x in v])
-        return rc, tuple(x.value for x in v)
-
-    # the wide form (N % 128 == 0): 256 x 128 tiles, 256 threads, stream-K on min(CUs, tiles x slices) workers
-    assert x3cw_plan(64, 14, 256, 256) == (0, (256, 128, 1, 256, 256))  # layer3: 98 tiles x 8 slices
-    assert x3cw_plan(1, 14, 32, 256) == (0, (256, 128, 1, 2, 256))
-    assert x3cw_plan(64, 7, 512, 512)[0] == 1001  # layer4 at batch 64: 6 images' padded rows exceed the band
-    assert x3cw_plan(64, 14, 256, 192)[0] == 1001  # N neither 64 nor a multiple of 128
-
 
 def test_device_tensors_required():
     from capmi import kernels as K
