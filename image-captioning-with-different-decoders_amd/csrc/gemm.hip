@@ -1033,6 +1033,16 @@ int x3d_plan(const capmi_gemm_problem* prob, int amode, int bmode, GemmArgs& a, 
   const int nkt = p.K / 32;
   const long long rounds = (total + slots - 1) / slots;
   sk = !sk_off() && !sk_family_off(4) && total > 0 && nkt >= 8 && (double)total / (double)(rounds * slots) < 0.9;
+  // C = A.B + beta C (the fine-tune 1x1 data gradients accumulating into the block input's gradient): the
+  // data-parallel form, whose epilogue loads each column block of C ahead of its stores (the stream-K forms sit
+  // at the register cap and keep the interleaved load / store); CAPMI_X3D_BETA_SK=1 keeps stream-K (A/B)
+  {
+    static const bool beta_sk = [] {
+      const char* e = getenv("CAPMI_X3D_BETA_SK");
+      return e && e[0] == '1';
+    }();
+    if (a.plain_epi == 2 && !beta_sk) sk = false;
+  }
   return 0;
 }
 

@@ -336,6 +336,18 @@ gemm_x3_kernel(const GemmArgs args) {
             roff[i][r] = row < M ? (unsigned)row * (unsigned)ldc * 4u : kOOBx;
           }
         const unsigned cb = (unsigned)(n0 + wn0 + (lane & 15)) * 4u;
+        // + beta C: every C value loaded before the first store (interleaved, each load waited for the store
+        // before it -- they may alias through the one descriptor -- a serial memory round trip per element)
+        float cold[2][TN16][4];
+        if (args.plain_epi == 2) {
+#pragma unroll
+          for (int j = 0; j < TN16; ++j)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                cold[i][j][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rc, roff[i][r] + cb + 64u * j, 0, 0));
+        }
 #pragma unroll
         for (int j = 0; j < TN16; ++j) {
           csum[j] = 0.f;
@@ -345,8 +357,7 @@ gemm_x3_kernel(const GemmArgs args) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               float v = acc4[i][j][r];
-              if (args.plain_epi == 2)  // + beta C (the general epilogue's fmaf(beta, C, v), bit for bit)
-                v = fmaf(beta, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rc, roff[i][r] + cb + 64u * j, 0, 0)), v);
+              if (args.plain_epi == 2) v = fmaf(beta, cold[i][j][r], v);  // (the general epilogue's fmaf, bit for bit)
               __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, roff[i][r] + cb + 64u * j, 0, 0);
               csum[j] += v;
               csq[j] = fmaf(v, v, csq[j]);

@@ -576,17 +576,32 @@ gemm_x3p_kernel(const GemmArgs args) {
             roff[i][r] = row < M ? (unsigned)row * (unsigned)ldc * 4u : kOOBp;
           }
         const unsigned cb = (unsigned)(n0 + wn0 + cl) * 4u;
+        // + beta C (plain_epi 2): each column block's 16 C values loaded before its first store. Interleaved, each
+        // load waited for the store before it (they may alias through the one descriptor): 64 serial round trips
+        // to memory per lane -- the fine-tune 1x1 data gradients ran 92 us against 51 for the same GEMM shape.
+        // (All 64 ahead of the stores spilled this kernel's registers.)
+        // The stream-K forms sit at the 256-register cap and spill with those loads in flight: they keep the
+        // interleaved form, and the planner runs beta problems data-parallel (x3d_plan).
 #pragma unroll
         for (int j = 0; j < JN; ++j) {
           csum4[j] = 0.f;
           csq4[j] = 0.f;
+          float cold[4][4];
+          if (!SK && args.plain_epi == 2) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                cold[i][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rc, roff[i][r] + cb + 64u * j, 0, 0));
+          }
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               float v = acc4[i][j][r];
-              if (args.plain_epi == 2)  // + beta C (the general epilogue's fmaf(beta, C, v), bit for bit)
-                v = fmaf(beta, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rc, roff[i][r] + cb + 64u * j, 0, 0)), v);
+              if (args.plain_epi == 2)  // (the general epilogue's fmaf(beta, C, v), bit for bit)
+                v = fmaf(beta, SK ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rc, roff[i][r] + cb + 64u * j, 0, 0))
+                                  : cold[i][r], v);
               __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, roff[i][r] + cb + 64u * j, 0, 0);
               csum4[j] += v;
               csq4[j] = fmaf(v, v, csq4[j]);

@@ -285,6 +285,16 @@ gemm_x3w_kernel(const GemmArgs args) {
           roff[i][r] = row < M ? (unsigned)row * (unsigned)ldc * 4u : kOOBw;
         }
       const unsigned cb = (unsigned)(n0 + wn0 + cl) * 4u;
+      float cold[4][4][4];  // + beta C: all loads before the first store (they may alias: no interleaving)
+      if (args.plain_epi == 2) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              cold[i][j][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rc, roff[i][r] + cb + 64u * j, 0, 0));
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -292,8 +302,7 @@ gemm_x3w_kernel(const GemmArgs args) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float v = acc4[i][j][r];
-            if (args.plain_epi == 2)
-              v = fmaf(beta, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rc, roff[i][r] + cb + 64u * j, 0, 0)), v);
+            if (args.plain_epi == 2) v = fmaf(beta, cold[i][j][r], v);
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rc, roff[i][r] + cb + 64u * j, 0, 0);
           }
       return;
