@@ -423,3 +423,28 @@ def test_x3c_direct_conv(N, H, Cin, pro):
     ref_abs = F.conv2d(xi.abs(), wt.abs(), padding=1).permute(0, 2, 3, 1).reshape(rows, Cout)
     r3, _ = _errs(out_c[:rows], ref, ref_abs)
     assert r3 <= 1.0, r3
+
+
+@pytest.mark.parametrize("M,N,Kd", [(12544, 1024, 256), (3137, 256, 512), (777, 128, 64 * 9)])
+def test_beta_epilogue_batched_loads(M, N, Kd):
+    """C = A.B + beta C (the store-only epilogue with beta, round 4: C loaded ahead of the stores) on x3d (dense
+    rows, data-parallel for beta problems) and gemm_x3: bit-identical to the product (beta onto zeros) plus C0 in
+    fp32 (fmaf(1, c, v) rounds v + c once), rows past M untouched (NaN sentinels)."""
+    K = _K()
+    A, W = rnd(M, Kd, seed=91), rnd(N, Kd, seed=92)
+    C0 = rnd(M, N, seed=93)
+    Ad, w3 = A.to(DEV), split3(W.to(DEV))
+    ws = K.gemm_workspace(DEV)
+    for name in ("x3d", "x3"):
+        run = (lambda p: K.gemm_x3d(p, 0, ws)) if name == "x3d" else (lambda p: K.gemm_x3(p, 0, ws))
+        c_beta = torch.full((M + 3, N), float("nan"), device=DEV)
+        c_beta[:M] = C0.to(DEV)
+        run(K.problem(M, N, Kd, Ad, Kd, w3, Kd, c_beta, N, beta=1.0))
+        # the reference with the same schedule (x3d takes beta problems data-parallel, plain ones stream-K):
+        # beta = 1 onto zeros, fmaf(1, 0, v) = v
+        c_plain = torch.zeros(M, N, device=DEV)
+        run(K.problem(M, N, Kd, Ad, Kd, w3, Kd, c_plain, N, beta=1.0))
+        torch.cuda.synchronize()
+        K.sk_check([ws])
+        assert torch.equal(c_beta[:M].cpu(), c_plain.cpu() + C0), name
+        assert bool(torch.isnan(c_beta[M:]).all()), name
