@@ -77,6 +77,16 @@ __device__ __forceinline__ int swz(int r) {
 template <int AMODE, bool SK, int PBK, bool ASPLIT = false, bool PRO = false>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(X3pGeo<PBK>::WPE)))
 gemm_x3p_kernel(const GemmArgs args) {
+#if X3P_CLOCK  // diagnostic build only (tools/r04/run27.sh): the clock this workgroup ran at, by device printf
+  const long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+  auto clk_report = [&]() {
+    const long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0 && blockIdx.x % 16 == 0)
+      printf("x3pclk %d %lld %lld\n", (int)blockIdx.x, t1 - clk_t0, r1 - clk_r0);
+  };
+#else
+  auto clk_report = [] {};
+#endif
   static_assert(!ASPLIT || PBK == 32, "x3d: 32-deep k-tiles");
   static_assert(!PRO || ASPLIT, "prologue: x3d (conv, or dense rows whose k is the channel: 1x1 convs)");
   using G_ = X3pGeo<PBK>;
@@ -720,6 +730,7 @@ gemm_x3p_kernel(const GemmArgs args) {
     const int tm = args.tile_cols_first ? bid % tiles_m : bid / tiles_n;
     mainloop(P, tm * PBM, tn * PBN, 0, P.K);
     epilogue(P, tm, tn);
+    clk_report();
     return;
   }
 
@@ -822,6 +833,7 @@ gemm_x3p_kernel(const GemmArgs args) {
     }
     epilogue(P, tm, tn);
   }
+  clk_report();
 }
 
 // x = relu(y * scale[c] + shift[c]) split into three bf16 planes out[p][i] (the x3p A operand)
