@@ -178,21 +178,6 @@ def _traffic(kernel, config="attention"):
     return None if ent is None else ent.get("hbm_bytes_per_launch")
 
 
-def _held_clock_mhz(kernel):
-    """The clock the headline conv kernel's workgroups held under the bench's grid, measured in-kernel
-    (profiles/r04_x3p_clock.txt: s_memtime / s_memrealtime in a diagnostic build), or None."""
-    if not kernel.startswith("gemm_x3p_kernel<2, true, 32, false, false"):
-        return None
-    try:
-        with open(os.path.join(REPO, "profiles", "r04_x3p_clock.txt")) as f:
-            for line in f:
-                if line.startswith("stream-K, 256 workers"):
-                    return int(line.split("MHz")[0].split()[-1])
-    except (OSError, ValueError, IndexError):
-        return None
-    return None
-
-
 def _cgroup_cpus():
     """CPUs this process's cgroup may use (cgroup v2 cpu.max quota / period), or None (no quota)."""
     try:
@@ -522,13 +507,6 @@ def main():
                 # stream, as the rocprofv3 kernel trace runs the bench) unless the steps themselves were eager;
                 # in_pipeline below is the same kernel with the decoder stream beside it
                 "frac_pass": "timed eager steps" if args.eager else "serialized timing pass (after the timed region)"}
-        mhz = _held_clock_mhz(key)
-        if mhz:
-            # the same fraction against the bound at the clock the chip holds under this kernel's load
-            # (DVFS give-back, MI355X_MICROARCH.md)
-            held = peak * mhz / 2400.0
-            roof["held_clock"] = {"mhz": mhz, "peak_at_held_clock": round(held, 1), "frac": round(ach / held, 4),
-                                  "source": "profiles/r04_x3p_clock.txt (in-kernel s_memtime / s_memrealtime)"}
         if timer_pipe is not None:
             pp = timer_pipe.result().get(key)
             if pp:

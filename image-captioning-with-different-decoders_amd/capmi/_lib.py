@@ -166,13 +166,14 @@ class CapmiError(RuntimeError):
     pass
 
 
-def _load():
-    if not os.path.exists(LIB_PATH):
+def _load(path=LIB_PATH):
+    """Bind libcapmi.so at ``path`` (the in-tree build; tools load A/B builds side by side through it)."""
+    if not os.path.exists(path):
         raise ImportError(
-            f"libcapmi.so not found at {LIB_PATH}: build it with "
+            f"libcapmi.so not found at {path}: build it with "
             "`python -c 'import __graft_entry__ as g; g.build()'` (the HIP kernels are the only "
             "compute path; there is no fallback)")
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     for name, args in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = args

@@ -28,7 +28,7 @@ struct BnFinArgs {
 };
 
 // every operation rounded on its own (no contraction into fma): the result is a function of the sums alone,
-// reproducible by any IEEE implementation (tests/test_gpu_gemm.py::test_bn_finalize_canonical_order)
+// reproducible by any IEEE implementation (tests/test_gpu_bn_final.py)
 __device__ __forceinline__ void bnf_apply(const BnFinArgs& f, int c, double s, double q) {
 #pragma clang fp contract(off)
   const double n = (double)f.count;

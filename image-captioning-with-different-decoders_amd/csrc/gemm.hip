@@ -1077,7 +1077,8 @@ int x3w_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long ws_
   CAPMI_REQUIRE(prob != nullptr, CAPMI_EINVAL);
   const capmi_gemm_problem& p = *prob;
   CAPMI_REQUIRE(amode == CAPMI_A_MMAJOR && (bmode == CAPMI_B_KROWS || bmode == CAPMI_B_CONV_NHWC), CAPMI_EINVAL);
-  CAPMI_REQUIRE(p.A && p.B && p.C && p.M > 0 && p.N > 0 && p.K >= 0 && p.ksplit == 1, CAPMI_EINVAL);
+  // K = 0 is refused: the kernel would leave C untouched where C = beta C is the contract
+  CAPMI_REQUIRE(p.A && p.B && p.C && p.M > 0 && p.N > 0 && p.K > 0 && p.ksplit == 1, CAPMI_EINVAL);
   CAPMI_REQUIRE(!p.bias && !p.bias2 && !p.relu && !p.stats && p.a_r1 <= 0 && p.c_r1 <= 0, CAPMI_EINVAL);
   CAPMI_REQUIRE((p.in_scale == nullptr) == (p.in_shift == nullptr), CAPMI_EINVAL);
   CAPMI_REQUIRE(p.M % 4 == 0 && p.N % 4 == 0 && p.lda >= p.M && p.lda % 4 == 0 && p.ldc >= p.N, CAPMI_EALIGN);
@@ -1124,7 +1125,6 @@ int gemm_x3w(const capmi_gemm_problem* prob, int amode, int bmode, void* workspa
   long long tiles = 0;
   const int rc = x3w_plan(prob, amode, bmode, part_floats, a, S, tiles);
   if (rc) return rc;
-  if (prob->K == 0) return 0;  // (dW = 0 is the caller's: nothing to multiply)
   CAPMI_REQUIRE(workspace == nullptr || aligned16(workspace), CAPMI_EINVAL);
   if (S > 1) a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
   int e = gemm_x3w_launch(a, bmode, (int)(tiles * S), s);

@@ -21,6 +21,9 @@
 // the 16-lane groups of ds_read_b128 hit 64 distinct banks). Epilogue, BN statistics per 64-row
 // slice and the stream-K hand-off are those of gemm_nt.hip.
 #include "gemm_args.h"
+#include "stamp.h"
+
+STAMP_BUFFER(capmi_x3_stamps)
 
 #ifndef X3_VARIANT
 #define X3_VARIANT 0
@@ -87,6 +90,9 @@ gemm_x3_kernel(const GemmArgs args) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
+  STAMP_DECL;
+  STAMP(capmi_x3_stamps, kStStart, 0);
+  STAMP_REAL(capmi_x3_stamps, kStRStart);
   const int lr = lane & 31, lh = lane >> 5;
   const int kq = (tid & 7) * 4;  // k of this thread's A float4 inside a k-tile
   (void)NB;
@@ -465,8 +471,13 @@ gemm_x3_kernel(const GemmArgs args) {
     const capmi_gemm_problem& P = args.p[0];
     const int tiles_n = args.tiles_n[0];
     const int tn = bid % tiles_n, tm = bid / tiles_n;
+    STAMP(capmi_x3_stamps, kStSeg, P.K / XBK);
     mainloop(P, tm * BM, tn * BN, 0, P.K);
+    STAMP(capmi_x3_stamps, kStMain, 0);
     epilogue(P, tm, tn);
+    STAMP(capmi_x3_stamps, kStEpi, 0);
+    STAMP(capmi_x3_stamps, kStEnd, 0);
+    STAMP_REAL(capmi_x3_stamps, kStREnd);
     return;
   }
 

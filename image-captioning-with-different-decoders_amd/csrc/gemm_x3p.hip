@@ -19,6 +19,9 @@
 // per-64-row BN statistics: a wave's 64 rows are one slice) and the stream-K / hybrid schedule with
 // the write-through hand-off are those of gemm_nt.hip.
 #include "gemm_args.h"
+#include "stamp.h"
+
+STAMP_BUFFER(capmi_x3p_stamps)
 
 namespace {
 
@@ -87,6 +90,12 @@ gemm_x3p_kernel(const GemmArgs args) {
 #else
   auto clk_report = [] {};
 #endif
+#if X3P_PRIO  // A/B: the second-dispatched half of the workgroup at issue priority 1 (MI355X_MICROARCH.md, item 4)
+  if (threadIdx.x >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
+  STAMP_DECL;
+  STAMP(capmi_x3p_stamps, kStStart, 0);
+  STAMP_REAL(capmi_x3p_stamps, kStRStart);
   static_assert(!ASPLIT || PBK == 32, "x3d: 32-deep k-tiles");
   static_assert(!PRO || ASPLIT, "prologue: x3d (conv, or dense rows whose k is the channel: 1x1 convs)");
   using G_ = X3pGeo<PBK>;
@@ -164,7 +173,7 @@ gemm_x3p_kernel(const GemmArgs args) {
       }
     }
     // B row block wid
-    const bool bw = wid < NBB;
+    const bool bw = NBB == PNT / 64 || wid < NBB;  // (BK = 32: every wave issues one B row block)
     const int br = wid * RPB + drow;
     const int b_ch = dslot ^ swz<PBK>(br);
     const bool b_ok = bw && n0 + br < N;
@@ -248,17 +257,21 @@ gemm_x3p_kernel(const GemmArgs args) {
           a_msk |= (unsigned)ok << i;
         }
       }
-      unsigned aoff[2];
+      // plane-0 byte offset of this lane's A piece and its out-of-range bit (kOOBp: padding taps, rows past M, k past
+      // the end), combined per plane below without a branch (an exec-masked offset computation split the DMA issue
+      // into basic blocks of its own, out of reach of the MFMA interleave)
+      unsigned aoff[2], abad[2];
 #pragma unroll
       for (int i = 0; i < NAB; ++i) {
         if (ASPLIT) break;
         if (AMODE == 0) {
-          aoff[i] = a_ok[i] && kok ? a_base[i] + (unsigned)k * 2 : kOOBp;
+          aoff[i] = a_base[i] + (unsigned)k * 2;
+          abad[i] = a_ok[i] && kok ? 0u : kOOBp;
         } else {
           const int ih = a_ih0[i] + c_kh, iw = a_iw0[i] + c_kw;
           const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
-          aoff[i] = ok ? ((a_base[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + c_sub * PBK + a_ch[i] * 8)) * 2u
-                       : kOOBp;
+          aoff[i] = ((a_base[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + c_sub * PBK + a_ch[i] * 8)) * 2u;
+          abad[i] = ok ? 0u : kOOBp;
         }
       }
       if (AMODE == 2 && ++c_sub == SUB) {
@@ -278,13 +291,14 @@ gemm_x3p_kernel(const GemmArgs args) {
         for (int i = 0; i < (ASPLIT ? 0 : NAB); ++i)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
               ra, (lds_ptr_t)(base + p * PBM * PROWB + (NAB * wid + i) * RPB * PROWB), 16,
-              aoff[i] == kOOBp ? kOOBp : aoff[i] + p * pA2, 0, 0, 0);
+              PBK == 32 ? (aoff[i] + p * pA2) | abad[i] : (abad[i] ? kOOBp : aoff[i] + p * pA2), 0, 0, 0);
       if (bw) {
-        const unsigned boff = b_ok && kok ? b_base + (unsigned)k * 2 : kOOBp;
+        const unsigned boff = b_base + (unsigned)k * 2, bbad = b_ok && kok ? 0u : kOOBp;
+        // (BK = 16, at its 128-register cap, keeps the select form: the branch-free one spilled it)
 #pragma unroll
         for (int p = 0; p < 3; ++p)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * RPB * PROWB),
-                                                   16, boff == kOOBp ? kOOBp : boff + p * pB2, 0, 0, 0);
+                                                   16, PBK == 32 ? (boff + p * pB2) | bbad : (bbad ? kOOBp : boff + p * pB2), 0, 0, 0);
       }
     };
     // x3d: fp32 A registers of one k-tile -> (prologue) -> three planes
@@ -403,48 +417,115 @@ gemm_x3p_kernel(const GemmArgs args) {
 #ifndef X3D_PIPE
 #define X3D_PIPE 1
 #endif
-    if (ASPLIT && M16 && X3D_PIPE && args.x3d_pipe) {
-      // x3d, round 4: A two k-tiles deep in ONE register set. During tile kt's MFMAs each of the thread's four
-      // float4 slots is split into the other buffer for tile kt + 1 and at once reloaded with tile kt + 2's
-      // (its BN scale / shift and the conv walk follow after the fourth slot): the A load has a whole k-tile to
-      // land, and the split's VALU and ds_writes interleave with the MFMAs instead of standing between two
-      // k-tiles with the load latency in front of them (the one-deep form: issue, MFMAs, wait, split, barrier)
-      auto b_dma = [&](int kt, int buf) {  // B planes of tile kt (past the end: zeros) into buffer buf
-        const int k = k_lo + kt * PBK;
-        unsigned char* base = lds + buf * PBUF;
-        if (bw) {
-          const unsigned boff = b_ok && k < k_hi ? b_base + (unsigned)k * 2 : kOOBp;
+    // x3d staging helpers (round 4 pipelined loop, round 5 phase loop): B planes by LDS-DMA, A slots by register
+    auto b_dma = [&](int kt, int buf) {  // B planes of tile kt (past the end: zeros) into buffer buf
+      const int k = k_lo + kt * PBK;
+      unsigned char* base = lds + buf * PBUF;
+      if (bw) {
+        const unsigned boff = b_base + (unsigned)k * 2, bbad = b_ok && k < k_hi ? 0u : kOOBp;
 #pragma unroll
-          for (int p = 0; p < 3; ++p)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * RPB * PROWB),
-                                                     16, boff == kOOBp ? kOOBp : boff + p * pB2, 0, 0, 0);
+        for (int p = 0; p < 3; ++p)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * RPB * PROWB),
+                                                   16, (boff + p * pB2) | bbad, 0, 0, 0);
+      }
+    };
+    auto a_load = [&](int kt, int i) {  // slot i of tile kt (the conv walk at tile kt)
+      const int k = k_lo + kt * PBK;
+      const bool kok = k < k_hi;
+      unsigned off;
+      bool ok;
+      if (AMODE == 0) {
+        ok = s_ok[i] && kok;
+        off = s_base[i] + (unsigned)k * 4;
+      } else {
+        const int ih = s_ih0[i] + c_kh, iw = s_iw0[i] + c_kw;
+        ok = s_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
+        off = ((s_base[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + aq * 4)) * 4u;
+      }
+      areg[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, off | (ok ? 0u : kOOBp), 0, 0));
+      a_msk = (a_msk & ~(1u << i)) | ((unsigned)ok << i);
+    };
+    auto a_next = [&](int kt) {  // after tile kt's four slots: its BN scale / shift, then the walk advances
+      const int k = k_lo + kt * PBK;
+      if (PRO) {  // always two loads (the step's vmcnt count relies on it); past the last k-tile the walk is
+                  // past Cin: an out-of-range offset, zeros
+        const unsigned ch = k < k_hi ? (unsigned)((AMODE == 2 ? c_ci : k) + aq * 4) * 4u : kOOBp;
+        a_sc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsc_p, ch, 0, 0));
+        a_sh = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsh_p, ch, 0, 0));
+      }
+      if (AMODE == 2 && ++c_kw == cKW) {  // (32-deep k-tiles: one (channel slice, tap) chunk per tile)
+        c_kw = 0;
+        if (++c_kh == P.cKH) {
+          c_kh = 0;
+          c_ci += 32;
         }
+      }
+    };
+    auto a_split = [&](int buf, int i) {  // slot i -> (prologue) -> three planes of buffer buf
+      unsigned char* base = lds + buf * PBUF;
+      float4 v = areg[i];
+      if (PRO) v = make_float4(fmaxf(fmaf(v.x, a_sc.x, a_sh.x), 0.f), fmaxf(fmaf(v.y, a_sc.y, a_sh.y), 0.f),
+                               fmaxf(fmaf(v.z, a_sc.z, a_sh.z), 0.f), fmaxf(fmaf(v.w, a_sc.w, a_sh.w), 0.f));
+      const bool keep = (a_msk >> i) & 1u;  // padding taps / rows past M: zeros AFTER the BN
+      v.x = keep ? v.x : 0.f;
+      v.y = keep ? v.y : 0.f;
+      v.z = keep ? v.z : 0.f;
+      v.w = keep ? v.w : 0.f;
+      unsigned lo[3], hi[3];
+      split3_pair(v.x, v.y, lo);
+      split3_pair(v.z, v.w, hi);
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        *reinterpret_cast<uint2*>(base + p * PBM * PROWB + s_lds[i]) = make_uint2(lo[p], hi[p]);
+    };
+// X3P_PHASE (round 5, default 2): x3p's k-loop places its one barrier after this many row blocks' MFMAs and
+// issues the next-but-one tile's DMA behind it (see the x3p branch of mainloop); 0 = the round-4 loop
+#ifndef X3P_PHASE
+#define X3P_PHASE 2
+#endif
+#ifndef X3D_VPM
+#define X3D_VPM 2  // x3d round-5 loop: VALU per MFMA in the interleave
+#endif
+    // the six products of row block i of a k-tile, smallest terms first per accumulator
+    auto mm6 = [&](int i, const bf16x8_p (&a)[3], const bf16x8_p (&b)[JN][3]) {
+#pragma unroll
+      for (int j = 0; j < JN; ++j) {
+        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][1], acc4[i][j], 0, 0, 0);
+        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][2], acc4[i][j], 0, 0, 0);
+        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[j][0], acc4[i][j], 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < JN; ++j) {
+        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][1], acc4[i][j], 0, 0, 0);
+        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][0], acc4[i][j], 0, 0, 0);
+        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][0], acc4[i][j], 0, 0, 0);
+      }
+    };
+#ifndef X3D_V2
+#define X3D_V2 0
+#endif
+    if constexpr (ASPLIT && M16 && X3D_V2 != 0) {
+      // x3d, round 5: one barrier per k-tile, before row block 3's MFMAs (the A fragments are read one row block
+      // ahead, so every read of tile kt is issued by then). Behind it buffer kt & 1 is free and tile kt + 2 is
+      // staged into it over a whole k-tile -- its B planes by LDS-DMA at once, its four A slots (loaded a k-tile
+      // earlier) split one per row block: slot 0 during block 3 of tile kt, slots 1-3 during blocks 0-2 of tile
+      // kt + 1 (which read the other buffer), each register reloaded at once with tile kt + 3's -- so the split
+      // VALU is spread over all 96 MFMAs of a k-tile and every DMA and load has a k-tile to land. The BN scale /
+      // shift of the tile being split and of the next one are two register sets.
+      const int c16 = lane >> 4, rl16 = lane & 15;
+      auto frag = [&](const unsigned char* plane, int r) {
+        return *reinterpret_cast<const bf16x8_p*>(plane + r * PROWB + ((c16 ^ swz<PBK>(r)) << 4));
       };
-      auto a_load = [&](int kt, int i) {  // slot i of tile kt (the conv walk at tile kt)
-        const int k = k_lo + kt * PBK;
-        const bool kok = k < k_hi;
-        unsigned off;
-        bool ok;
-        if (AMODE == 0) {
-          ok = s_ok[i] && kok;
-          off = s_base[i] + (unsigned)k * 4;
-        } else {
-          const int ih = s_ih0[i] + c_kh, iw = s_iw0[i] + c_kw;
-          ok = s_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
-          off = ((s_base[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + aq * 4)) * 4u;
-        }
-        areg[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off : kOOBp, 0, 0));
-        a_msk = (a_msk & ~(1u << i)) | ((unsigned)ok << i);
-      };
-      auto a_next = [&](int kt) {  // after tile kt's four slots: its BN scale / shift, then the walk advances
-        const int k = k_lo + kt * PBK;
-        if (PRO) {  // always two loads (the step's vmcnt count relies on it); past the last k-tile the walk is
-                    // past Cin: an out-of-range offset, zeros
+      auto ss_load = [&](int kt, float4& sc, float4& sh) {  // BN scale / shift of tile kt (at the walk's channel)
+        if (PRO) {  // always two loads (the barrier's vmcnt relies on it); past the end: out of range, zeros
+          const int k = k_lo + kt * PBK;
           const unsigned ch = k < k_hi ? (unsigned)((AMODE == 2 ? c_ci : k) + aq * 4) * 4u : kOOBp;
-          a_sc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsc_p, ch, 0, 0));
-          a_sh = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsh_p, ch, 0, 0));
+          sc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsc_p, ch, 0, 0));
+          sh = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsh_p, ch, 0, 0));
         }
-        if (AMODE == 2 && ++c_kw == cKW) {  // (32-deep k-tiles: one (channel slice, tap) chunk per tile)
+      };
+      auto walk = [&] {  // the conv walk advances one k-tile (32-deep: one (channel slice, tap) chunk)
+        if (AMODE == 2 && ++c_kw == cKW) {
           c_kw = 0;
           if (++c_kh == P.cKH) {
             c_kh = 0;
@@ -452,16 +533,21 @@ gemm_x3p_kernel(const GemmArgs args) {
           }
         }
       };
-      auto a_split = [&](int buf, int i) {  // slot i -> (prologue) -> three planes of buffer buf
+      auto split = [&](int buf, int i, float4 sc, float4 sh) {  // slot i -> (prologue) -> three planes of buf
         unsigned char* base = lds + buf * PBUF;
         float4 v = areg[i];
-        if (PRO) v = make_float4(fmaxf(fmaf(v.x, a_sc.x, a_sh.x), 0.f), fmaxf(fmaf(v.y, a_sc.y, a_sh.y), 0.f),
-                                 fmaxf(fmaf(v.z, a_sc.z, a_sh.z), 0.f), fmaxf(fmaf(v.w, a_sc.w, a_sh.w), 0.f));
-        const bool keep = (a_msk >> i) & 1u;  // padding taps / rows past M: zeros AFTER the BN
-        v.x = keep ? v.x : 0.f;
-        v.y = keep ? v.y : 0.f;
-        v.z = keep ? v.z : 0.f;
-        v.w = keep ? v.w : 0.f;
+        if (PRO) v = make_float4(fmaxf(fmaf(v.x, sc.x, sh.x), 0.f), fmaxf(fmaf(v.y, sc.y, sh.y), 0.f),
+                                 fmaxf(fmaf(v.z, sc.z, sh.z), 0.f), fmaxf(fmaf(v.w, sc.w, sh.w), 0.f));
+        // padding taps / rows past M read zeros: with the prologue they must be zeros AFTER the BN (without it the
+        // zeros pass through the split as they are); unconditional, a uniform branch here would cut the block's
+        // MFMA interleave into separate scheduling regions
+        if (PRO) {
+          const bool keep = (a_msk >> i) & 1u;
+          v.x = keep ? v.x : 0.f;
+          v.y = keep ? v.y : 0.f;
+          v.z = keep ? v.z : 0.f;
+          v.w = keep ? v.w : 0.f;
+        }
         unsigned lo[3], hi[3];
         split3_pair(v.x, v.y, lo);
         split3_pair(v.z, v.w, hi);
@@ -469,6 +555,93 @@ gemm_x3p_kernel(const GemmArgs args) {
         for (int p = 0; p < 3; ++p)
           *reinterpret_cast<uint2*>(base + p * PBM * PROWB + s_lds[i]) = make_uint2(lo[p], hi[p]);
       };
+      // one k-step. (sc0, sh0): the BN scale / shift of tile kt + 1, whose slots 1-3 are split in blocks 0-2, then
+      // reloaded with tile kt + 3's in block 3; (sc1, sh1): tile kt + 2's, used from block 3 on. The caller swaps
+      // the two sets every step (the loop is unrolled by two so that neither is ever copied: a loop-carried copy of
+      // a register just loaded made the compiler drain vmcnt at the back edge)
+      auto kstep = [&](int kt, float4& sc0, float4& sh0, float4& sc1, float4& sh1) {
+        const unsigned char* A_ = lds + (kt & 1) * PBUF;
+        const unsigned char* B_ = A_ + PA_BYTES;
+        bf16x8_p b[JN][3], a[3];
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) b[j][p] = frag(B_ + p * PBN * PROWB, wn0 + 16 * j + rl16);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) a[p] = frag(A_ + p * PBM * PROWB, wm0 + rl16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          bf16x8_p an[3];
+          if (i < 3) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) an[p] = frag(A_ + p * PBM * PROWB, wm0 + 16 * (i + 1) + rl16);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (i < 3) {
+            // slot i + 1 of tile kt + 1 into buffer (kt + 1) & 1, then its register takes tile kt + 2's
+            split((kt + 1) & 1, i + 1, sc0, sh0);
+            a_load(kt + 2, i + 1);
+            if (i == 2) walk();  // (the walk now stands at tile kt + 3)
+          } else {
+            // tile kt + 1's B planes landed (only the 4 A loads and 2 scale / shift loads issued after its DMA are
+            // younger), this wave's reads of tile kt and split stores of tile kt + 1 are done: after the barrier
+            // tile kt + 1 is complete and buffer kt & 1 free for tile kt + 2
+            if constexpr (PRO)
+              asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            else
+              asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            b_dma(kt + 2, kt & 1);
+            __builtin_amdgcn_sched_barrier(0);  // (the DMA stays older than every register load after it)
+            split(kt & 1, 0, sc1, sh1);
+            a_load(kt + 3, 0);
+            ss_load(kt + 3, sc0, sh0);
+          }
+          mm6(i, a, b);
+#pragma unroll
+          for (int r = 0; r < 6 * JN; ++r) {  // the slot's split VALU among the block's MFMAs
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, X3D_VPM, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (i < 3) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) a[p] = an[p];
+          }
+        }
+      };
+      // prologue: tile 0 staged; tile 1's B DMA issued and its A loaded, slot 0 split ("block 3 of tile -1")
+      float4 scA = make_float4(1.f, 1.f, 1.f, 1.f), shA = make_float4(0.f, 0.f, 0.f, 0.f), scB = scA, shB = shA;
+      b_dma(0, 0);
+#pragma unroll
+      for (int i = 0; i < NSA; ++i) a_load(0, i);
+      ss_load(0, scA, shA);
+      walk();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < NSA; ++i) split(0, i, scA, shA);
+      b_dma(1, 1);
+#pragma unroll
+      for (int i = 0; i < NSA; ++i) a_load(1, i);
+      ss_load(1, scA, shA);
+      walk();
+      __syncthreads();  // tile 0 complete (its B DMA waited above, its split stores by the barrier's lgkmcnt)
+      split(1, 0, scA, shA);
+      a_load(2, 0);
+      ss_load(2, scB, shB);
+      for (int kt = 0; kt < nkt; kt += 2) {
+        kstep(kt, scA, shA, scB, shB);
+        if (kt + 1 < nkt) kstep(kt + 1, scB, shB, scA, shA);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the loads and DMA past the end drained)
+      __syncthreads();  // (the next tile's prologue rewrites buffers 0 and 1)
+      return;
+    }
+    if (ASPLIT && M16 && X3D_PIPE && args.x3d_pipe) {
+      // x3d, round 4: A two k-tiles deep in ONE register set. During tile kt's MFMAs each of the thread's four
+      // float4 slots is split into the other buffer for tile kt + 1 and at once reloaded with tile kt + 2's
+      // (its BN scale / shift and the conv walk follow after the fourth slot): the A load has a whole k-tile to
+      // land, and the split's VALU and ds_writes interleave with the MFMAs instead of standing between two
+      // k-tiles with the load latency in front of them (the one-deep form: issue, MFMAs, wait, split, barrier)
       const int c16 = lane >> 4, rl16 = lane & 15;
       auto frag = [&](const unsigned char* plane, int r) {  // 16x16x32 fragment of row r, chunk c16
         return *reinterpret_cast<const bf16x8_p*>(plane + r * PROWB + ((c16 ^ swz<PBK>(r)) << 4));
@@ -542,6 +715,71 @@ gemm_x3p_kernel(const GemmArgs args) {
       for (int kt = 0; kt < nkt; ++kt) step(kt, kt & 1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the loads and DMA past the end drained)
       __syncthreads();  // (the next tile's prologue rewrites buffer 0, which the last step may have read)
+      return;
+    }
+    if (!ASPLIT && M16 && X3P_PHASE) {
+      // x3p, round 5: the DMA of tile kt + 2 is issued right after the barrier that ends the reads of tile kt
+      // (into the buffer those reads used), interleaved with the second half of tile kt's MFMAs, so each tile's
+      // DMA has a whole k-tile to land; the one-barrier loop below issued it ahead of the reads and waited for
+      // it at the hoisted barrier, ~40 % of a k-tile later
+      issue(0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      issue(1, 1);
+      const int c = lane >> 4, rl = lane & 15;
+      for (int kt = 0; kt < nkt; ++kt) {
+        const unsigned char* A_ = lds + (kt & 1) * PBUF;
+        const unsigned char* B_ = A_ + PA_BYTES;
+        bf16x8_p a[4][3], b[JN][3];
+#pragma unroll
+        for (int j = 0; j < JN; ++j) {
+          const int r = wn0 + 16 * j + rl;
+          const int o = r * PROWB + ((c ^ swz<PBK>(r)) << 4);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) b[j][p] = *reinterpret_cast<const bf16x8_p*>(B_ + p * PBN * PROWB + o);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = wm0 + 16 * i + rl;
+          const int o = r * PROWB + ((c ^ swz<PBK>(r)) << 4);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) a[i][p] = *reinterpret_cast<const bf16x8_p*>(A_ + p * PBM * PROWB + o);
+        }
+        auto mm = [&](int i) {  // the six products of row block i, smallest terms first per accumulator
+#pragma unroll
+          for (int j = 0; j < JN; ++j) {
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][1], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][2], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[j][0], acc4[i][j], 0, 0, 0);
+          }
+#pragma unroll
+          for (int j = 0; j < JN; ++j) {
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][1], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][0], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][0], acc4[i][j], 0, 0, 0);
+          }
+        };
+        // X3P_PHASE = row blocks multiplied before the barrier (1-3)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (i == X3P_PHASE) {
+            __builtin_amdgcn_sched_barrier(0);
+            // tile kt + 1 landed (this wave's DMA), this wave's reads of tile kt done; the barrier makes both hold
+            // for every wave: buffer kt & 1 is free for tile kt + 2, buffer (kt + 1) & 1 readable
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            issue(kt + 2, kt & 1);  // (past the end: zeros, no memory traffic; keeps the DMA branch-free)
+          }
+          mm(i);
+        }
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {  // the DMA pieces spread over the MFMAs after the barrier
+          __builtin_amdgcn_sched_group_barrier(0x008, 2 * (4 - X3P_PHASE), 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __syncthreads();  // (the next tile's prologue rewrites buffer 0, which the last k-tile may have read)
       return;
     }
     issue(0, 0);
@@ -728,9 +966,14 @@ gemm_x3p_kernel(const GemmArgs args) {
     const int tiles_m = args.tiles_m[0];
     const int tn = args.tile_cols_first ? bid / tiles_m : bid % tiles_n;
     const int tm = args.tile_cols_first ? bid % tiles_m : bid / tiles_n;
+    STAMP(capmi_x3p_stamps, kStSeg, P.K / PBK);
     mainloop(P, tm * PBM, tn * PBN, 0, P.K);
+    STAMP(capmi_x3p_stamps, kStMain, 0);
     epilogue(P, tm, tn);
+    STAMP(capmi_x3p_stamps, kStEpi, 0);
     clk_report();
+    STAMP(capmi_x3p_stamps, kStEnd, 0);
+    STAMP_REAL(capmi_x3p_stamps, kStREnd);
     return;
   }
 
@@ -772,7 +1015,9 @@ gemm_x3p_kernel(const GemmArgs args) {
     }
     const long long tb = t * nkt;
     const int tm = cf ? (int)(t % tiles_m) : (int)(t / tiles_n), tn = cf ? (int)(t / tiles_m) : (int)(t % tiles_n);
+    STAMP(capmi_x3p_stamps, kStSeg, ke - ks);
     mainloop(P, tm * PBM, tn * PBN, ks * PBK, ke * PBK);
+    STAMP(capmi_x3p_stamps, kStMain, 0);
     if (ke < nkt) {
       const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + (long long)blockIdx.x * PART, 0,
                                                         PART * 4, 0x00020000);
@@ -799,6 +1044,7 @@ gemm_x3p_kernel(const GemmArgs args) {
           }
       }
       sk_publish(flags + blockIdx.x, tid);
+      STAMP(capmi_x3p_stamps, kStPub, 0);
       continue;
     }
     if (ks > 0) {
@@ -830,10 +1076,14 @@ gemm_x3p_kernel(const GemmArgs args) {
         }
         if (ub + w2 * U / G <= tb) break;
       }
+      STAMP(capmi_x3p_stamps, kStCons, 0);
     }
     epilogue(P, tm, tn);
+    STAMP(capmi_x3p_stamps, kStEpi, 0);
   }
   clk_report();
+  STAMP(capmi_x3p_stamps, kStEnd, 0);
+  STAMP_REAL(capmi_x3p_stamps, kStREnd);
 }
 
 // x = relu(y * scale[c] + shift[c]) split into three bf16 planes out[p][i] (the x3p A operand)

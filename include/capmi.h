@@ -149,7 +149,7 @@ int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int t
  * sum_k A[k][m] B[k][n] with k = output pixel: A = dY fp32 (CAPMI_A_MMAJOR, [K][lda], lda % 4 == 0) and B =
  * the conv input fp32 as k rows (CAPMI_B_KROWS, [K][ldb]) or through its implicit im2col (CAPMI_B_CONV_NHWC,
  * n = (kh, kw, ci), the packed [Cout][KH][KW][Cin] weight order, Cin % 4 == 0), with the optional BN-apply +
- * ReLU prologue on B (in_scale / in_shift [Cin]; padding taps zero after it); M % 4 == 0, N % 4 == 0; alpha /
+ * ReLU prologue on B (in_scale / in_shift [Cin]; padding taps zero after it); M % 4 == 0, N % 4 == 0, K > 0; alpha /
  * beta only, no bias / relu / stats / ksplit. Both operands are split into three bf16 terms in the kernel and
  * read back transposed (ds_read_b64_tr_b16); 256x128 tiles, 512 threads, one workgroup per CU. With alpha 1
  * and beta 0 the pixel range is split over several workgroups whose partial slabs go to the workspace (as
@@ -214,7 +214,8 @@ int capmi_image_nhwc4(const float* in, int N, int C, int H, int W, float* out, v
  * scale = gamma*rsqrt(var+eps), shift = beta - mean*scale; running stats updated in place
  * (momentum, unbiased var) when running_mean != NULL. mean/var out (may be NULL). The fp64 sums run
  * in one canonical order (csrc/bn_final.h), reproducible op for op on the host.
- * work: CAPMI_BN_WORK_DOUBLES(C) doubles, 16-B aligned (unused since round 4; kept in the signature). */
+ * work: unused since round 4 and may be NULL (kept in the signature; older callers pass
+ * CAPMI_BN_WORK_DOUBLES(C) doubles). */
 #define CAPMI_BN_WORK_DOUBLES(C) (64 + 64 * (long long)(C)) /* C <= 8192 */
 int capmi_bn_finalize(const float* stats, int tiles, int C, long long count, const float* gamma,
                       const float* beta, float* running_mean, float* running_var, float momentum,

@@ -30,6 +30,8 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 B, L, V = 64, 25, 8100
 
+FT_FLIP_FLOOR = 1e-3  # config 4: flipped ReLU decisions within this many rms of 0 always pass
+
 
 def _pooled(fmap, d=2):
     """(B, 7, 7, E) -> the (B, 196, E) map AdaptiveAvgPool2d(14) gives (exact 2x replicate)."""
@@ -134,8 +136,10 @@ def test_config4_glove_finetune_step_b64():
     worst, worst_cpu = worst_flip(masks), worst_flip(m32)
     print(f"config 4: ReLU flips gpu {n_gpu} cpu32 {n_cpu}; worst flipped |z|/rms gpu {worst:.2g} cpu32 "
           f"{worst_cpu:.2g}; loss gpu {loss:.6f} fp64 {float(o64_gpu['loss']):.6f} cpu32 {float(o32['loss']):.6f}")
-    # the flips' margin is the CPU fp32 path's own: no decision further from 0 than twice its worst one
-    assert n_gpu <= 2 * n_cpu + 2 and worst <= 2 * worst_cpu, (n_gpu, n_cpu, worst, worst_cpu)
+    # the flips' margin is the CPU fp32 path's own: no decision further from 0 than twice its worst one, with a
+    # floor of FT_FLIP_FLOOR rms (a rounding-level decision; DESIGN 4.6: every path's flips at full depth lie
+    # within 1e-3 of the rms of 0), so that a CPU path with no flip, or one far-out CPU flip, does not set the bound
+    assert n_gpu <= 2 * n_cpu + 2 and worst <= max(FT_FLIP_FLOOR, 2 * worst_cpu), (n_gpu, n_cpu, worst, worst_cpu)
     el = abs(loss - float(o64_gpu["loss"]))
     ec = abs(float(o32["loss"]) - float(o64_32["loss"]))
     assert el <= 2 * ec + 1e-5, (el, ec)

@@ -25,7 +25,7 @@ SHAPES = {  # name: (Cin, H, W, Cout, k, prologue[, stride]) -- ResNet-101 encod
     "ds4": (1024, 14, 14, 2048, 1, False, 2)}
 
 
-def main():
+def parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="l3c2")
     ap.add_argument("--reps", type=int, default=50)
@@ -40,7 +40,14 @@ def main():
     ap.add_argument("--x3s", action="store_true", help="short-k streaming x3 kernel (gemm_x3s.hip)")
     ap.add_argument("--x3c", action="store_true", help="the direct 3x3 conv (gemm_x3c.hip; N = 64, stride 1)")
     ap.add_argument("--x3w", action="store_true", help="the conv's WEIGHT gradient on gemm_x3w.hip (dW = dY^T im2col(X))")
-    a = ap.parse_args()
+    ap.add_argument("--dense", action="store_true",
+                    help="x3d on a 1x1 / stride-1 conv as dense rows with the BN prologue per k = channel "
+                         "(the bench's gemm_x3p_kernel<0, *, 32, true, true> form; default: conv mode)")
+    return ap
+
+
+def setup(a):
+    """(run, M, N, K) of one conv GEMM launch as the options describe (tensors held by the closure)."""
     dev = "cuda"
     ci, H, W, co, k, pro, *st = SHAPES[a.shape]
     stride = st[0] if st else 1
@@ -86,6 +93,9 @@ def main():
     elif a.x3d:
         w3 = torch.empty(3 * w.numel(), device=dev, dtype=torch.bfloat16)
         K.split3_bf16(K.conv_weight_order_x3p(w, k, k, ci).contiguous(), w3)
+        if a.dense and k == 1 and stride == 1:  # dense rows, the prologue per k = channel (EncoderRunner's 1x1 form)
+            prob, mode = K.problem(M, co, Kd, x, ci, w3, Kd, y, co, stats=stats, in_scale=sc if pro else None,
+                                   in_shift=sh if pro else None), CAPMI_A_KMAJOR
         prob.B = w3.data_ptr()
         print("x3d kernel:", K.gemm_x3d_kernel_name(prob, mode))
         run = lambda: K.gemm_x3d(prob, mode, ws)  # noqa: E731
@@ -122,6 +132,14 @@ def main():
     else:
         print("plan (bm, bn, stream_k, generic, threads):", K.gemm_sk_plan(prob, mode, a.tile, bf16=a.bf16, threads=True))
         run = lambda: K.gemm_sk(prob, mode, ws, a.tile, bf16=a.bf16)  # noqa: E731
+    keep = (x, w, y, stats, sc, sh, prob, ws, locals().get("w3"), locals().get("xp"), locals().get("dy"),
+            locals().get("dw"), locals().get("xb"), locals().get("wb"), locals().get("yb"))
+    return (lambda: (run(), keep)[0]), M, co, Kd
+
+
+def main():
+    a = parser().parse_args()
+    run, M, co, Kd = setup(a)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     run()
     torch.cuda.synchronize()
