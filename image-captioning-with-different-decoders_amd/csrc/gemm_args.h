@@ -43,23 +43,36 @@ __device__ __forceinline__ void split3_pair(float e0, float e1, unsigned (&w)[3]
   w[2] = __builtin_bit_cast(unsigned, __builtin_convertvector(r2, capmi_bf16x2));
 }
 
-// Stream-K hand-off of a parked k-prefix partial (round 4: ordered by the HIP memory model, not by
-// cache-policy bits; cdna_hip_programming.md §6 Guideline 16). The partial's stores keep the SC1
-// (write-through) policy as a performance hint only.
-// Producer, called by EVERY thread after its partial stores: each wave drains its stores, the
-// workgroup meets, then one lane releases at agent scope and raises the worker's flag.
+// Stream-K hand-off of a parked k-prefix partial. Two forms, both ordered without relying on cache-policy
+// accidents (MI355X_MICROARCH.md, "Workgroup dispatch, XCD placement & inter-workgroup visibility"):
+// * FENCED (round 4; the multi-workgroup-per-CU kernels gemm_nt / gemm_bf16): producer stores -> every wave's
+//   vmcnt(0) -> barrier -> one lane's agent-scope release (buffer_wbl2) -> relaxed agent flag store; consumer: one
+//   lane's relaxed poll -> agent-scope acquire (buffer_inv sc1) + vmcnt(0) -> barrier -> loads;
+// * SC1 (round 5; the one-workgroup-per-CU kernels x3p / x3d / gemm_x3): the same sequence without the two fences,
+//   which is the guide's measured-valid table row 1 ("Valid forms besides Guideline 16"): ONE lane of each storing
+//   workgroup signals for ALL its stores with an sc1 flag store (a relaxed agent-scope atomic store) after every
+//   storing wave's vmcnt(0) and a workgroup barrier; the consumer learns it by an sc1 poll (relaxed agent-scope
+//   atomic load) and its other waves load after a barrier that wave joins; hipMalloc memory, one workgroup per CU;
+//   every partial store and every partial load is a 16-B sc1 buffer access (kSc1 in the kernels). The release was
+//   an L2 write-back of every dirty line of the XCD (the conv outputs these kernels have just stored) at each
+//   hand-off, the acquire an L1 invalidate.
+// Producer, called by EVERY thread after its partial stores.
+template <bool kFenced = true>
 __device__ __forceinline__ void sk_publish(int* flag, int tid) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (ROCm 7.2 may drop the fence's own wait)
+    if constexpr (kFenced) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (ROCm 7.2 may drop the fence's own wait)
+    }
     __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
-// Consumer, called by EVERY thread: one lane polls the producer's flag (relaxed, bounded: a timeout
-// raises err and leaves the flag), re-arms it, acquires at agent scope and waits for the invalidate;
-// the workgroup barrier then orders every wave's partial loads after the acquire.
+// Consumer, called by EVERY thread: one lane polls the producer's flag (relaxed, bounded: a timeout raises err and
+// leaves the flag), re-arms it (and in the fenced form acquires at agent scope and waits for the invalidate); the
+// workgroup barrier then orders every wave's partial loads after the poll.
+template <bool kFenced = true>
 __device__ __forceinline__ void sk_consume(int* flag, int* err, int tid) {
   if (tid == 0) {
     int spins = 0;
@@ -69,11 +82,18 @@ __device__ __forceinline__ void sk_consume(int* flag, int* err, int tid) {
       __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else
       __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (kFenced) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   __syncthreads();
 }
+// the form the one-workgroup-per-CU x3 kernels use (A/B: -DSK_SC1=0 keeps the fences)
+#ifndef SK_SC1
+#define SK_SC1 1
+#endif
+constexpr bool kSkFenced1 = SK_SC1 == 0;
 
 __device__ __forceinline__ long long remap(long long r, long long r1, long long ld, long long s2) {
   return r1 > 0 ? (r % r1) * ld + (r / r1) * s2 : r * ld;

@@ -529,13 +529,13 @@ gemm_x3_kernel(const GemmArgs args) {
           __builtin_amdgcn_raw_buffer_store_b128(v, rs, ((j * 4 + q) * XNT + tid) * 16, 0, kSc1x);
         }
       }
-      sk_publish(flags + blockIdx.x, tid);
+      sk_publish<kSkFenced1>(flags + blockIdx.x, tid);
       continue;
     }
     if (ks > 0) {
       for (long long w2 = w - 1;; --w2) {
         const long long b2 = w2 * ngrp + grp;
-        sk_consume(flags + b2, flags + gridDim.x, tid);
+        sk_consume<kSkFenced1>(flags + b2, flags + gridDim.x, tid);
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + b2 * PART, 0, PART * 4, 0x00020000);
         if constexpr (X3_M16) {
 #pragma unroll

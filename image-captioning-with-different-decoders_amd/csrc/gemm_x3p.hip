@@ -73,6 +73,13 @@ __device__ __forceinline__ int swz(int r) {
     return (r / X3pGeo<PBK>::SWZ) % X3pGeo<PBK>::CPR;
 }
 
+// one 16x16x32 bf16 MFMA, c += a . b (round 5 measured the operand-swapped form, whose transposed accumulator
+// blocks the epilogue can store 16 B per lane: 16 rows per store instead of 4 made the epilogue slower, 6.9k -> 10.6k
+// cycles per 256 x 128 tile with the column statistics on DPP row sums; not kept)
+__device__ __forceinline__ f32x4_p mf16(bf16x8_p a, bf16x8_p b, f32x4_p c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
 // ASPLIT ("x3d"): A is the fp32 operand itself (dense, or the NHWC conv input with the optional BN-apply
 // + ReLU prologue PRO), loaded to registers one k-tile ahead and split into the three swizzled LDS
 // planes after the k-tile's MFMAs; B stays LDS-DMA. It replaces gemm_x3 (both operands through
@@ -348,17 +355,17 @@ gemm_x3p_kernel(const GemmArgs args) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < JN; ++j) {
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][1], acc4[i][j], 0, 0, 0);
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][2], acc4[i][j], 0, 0, 0);
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[j][0], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = mf16(a[i][1], b[j][1], acc4[i][j]);
+            acc4[i][j] = mf16(a[i][0], b[j][2], acc4[i][j]);
+            acc4[i][j] = mf16(a[i][2], b[j][0], acc4[i][j]);
           }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < JN; ++j) {
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][1], acc4[i][j], 0, 0, 0);
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][0], acc4[i][j], 0, 0, 0);
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][0], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = mf16(a[i][0], b[j][1], acc4[i][j]);
+            acc4[i][j] = mf16(a[i][1], b[j][0], acc4[i][j]);
+            acc4[i][j] = mf16(a[i][0], b[j][0], acc4[i][j]);
           }
         return;
       }
@@ -490,15 +497,15 @@ gemm_x3p_kernel(const GemmArgs args) {
     auto mm6 = [&](int i, const bf16x8_p (&a)[3], const bf16x8_p (&b)[JN][3]) {
 #pragma unroll
       for (int j = 0; j < JN; ++j) {
-        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][1], acc4[i][j], 0, 0, 0);
-        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][2], acc4[i][j], 0, 0, 0);
-        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[j][0], acc4[i][j], 0, 0, 0);
+        acc4[i][j] = mf16(a[1], b[j][1], acc4[i][j]);
+        acc4[i][j] = mf16(a[0], b[j][2], acc4[i][j]);
+        acc4[i][j] = mf16(a[2], b[j][0], acc4[i][j]);
       }
 #pragma unroll
       for (int j = 0; j < JN; ++j) {
-        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][1], acc4[i][j], 0, 0, 0);
-        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][0], acc4[i][j], 0, 0, 0);
-        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][0], acc4[i][j], 0, 0, 0);
+        acc4[i][j] = mf16(a[0], b[j][1], acc4[i][j]);
+        acc4[i][j] = mf16(a[1], b[j][0], acc4[i][j]);
+        acc4[i][j] = mf16(a[0], b[j][0], acc4[i][j]);
       }
     };
 #ifndef X3D_V2
@@ -671,15 +678,15 @@ gemm_x3p_kernel(const GemmArgs args) {
           // per accumulator the six products smallest terms first (the one-deep form's order)
 #pragma unroll
           for (int j = 0; j < JN; ++j) {
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][1], acc4[i][j], 0, 0, 0);
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][2], acc4[i][j], 0, 0, 0);
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[j][0], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = mf16(a[1], b[j][1], acc4[i][j]);
+            acc4[i][j] = mf16(a[0], b[j][2], acc4[i][j]);
+            acc4[i][j] = mf16(a[2], b[j][0], acc4[i][j]);
           }
 #pragma unroll
           for (int j = 0; j < JN; ++j) {
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][1], acc4[i][j], 0, 0, 0);
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][0], acc4[i][j], 0, 0, 0);
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][0], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = mf16(a[0], b[j][1], acc4[i][j]);
+            acc4[i][j] = mf16(a[1], b[j][0], acc4[i][j]);
+            acc4[i][j] = mf16(a[0], b[j][0], acc4[i][j]);
           }
 #pragma unroll
           for (int r = 0; r < 24; ++r) {  // one MFMA, then up to two VALU (the slot's split)
@@ -748,15 +755,15 @@ gemm_x3p_kernel(const GemmArgs args) {
         auto mm = [&](int i) {  // the six products of row block i, smallest terms first per accumulator
 #pragma unroll
           for (int j = 0; j < JN; ++j) {
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][1], acc4[i][j], 0, 0, 0);
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][2], acc4[i][j], 0, 0, 0);
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[j][0], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = mf16(a[i][1], b[j][1], acc4[i][j]);
+            acc4[i][j] = mf16(a[i][0], b[j][2], acc4[i][j]);
+            acc4[i][j] = mf16(a[i][2], b[j][0], acc4[i][j]);
           }
 #pragma unroll
           for (int j = 0; j < JN; ++j) {
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][1], acc4[i][j], 0, 0, 0);
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][0], acc4[i][j], 0, 0, 0);
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][0], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = mf16(a[i][0], b[j][1], acc4[i][j]);
+            acc4[i][j] = mf16(a[i][1], b[j][0], acc4[i][j]);
+            acc4[i][j] = mf16(a[i][0], b[j][0], acc4[i][j]);
           }
         };
         // X3P_PHASE = row blocks multiplied before the barrier (1-3)
@@ -1043,14 +1050,14 @@ gemm_x3p_kernel(const GemmArgs args) {
             __builtin_amdgcn_raw_buffer_store_b128(v, rs, (((i * JN32 + j) * 4 + q) * PNT + tid) * 16, 0, kSc1p);
           }
       }
-      sk_publish(flags + blockIdx.x, tid);
+      sk_publish<kSkFenced1>(flags + blockIdx.x, tid);
       STAMP(capmi_x3p_stamps, kStPub, 0);
       continue;
     }
     if (ks > 0) {
       for (long long w2 = w - 1;; --w2) {
         const long long b2 = w2 * ngrp + grp;
-        sk_consume(flags + b2, flags + gridDim.x, tid);
+        sk_consume<kSkFenced1>(flags + b2, flags + gridDim.x, tid);
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + b2 * PART, 0, PART * 4, 0x00020000);
         if constexpr (M16) {
 #pragma unroll
