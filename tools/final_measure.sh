@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 measurement set for one config ($CFG): the default bench line, a rocprofv3 kernel trace of the same
+# Closing measurement set for one config ($CFG): the default bench line, a rocprofv3 kernel trace of the same
 # command, and the FETCH_SIZE / WRITE_SIZE PMC passes (separate runs); the databases are summarised on the box
 # (gpurun_out/prof_$CFG.md, gpurun_out/pmc_traffic_$CFG.json) and removed (gpurun copies back <= 64 MiB)
 R=$GRAFT_REPO_ROOT

@@ -3,7 +3,7 @@ partial slabs' state; then per-shape time of x3w vs the split-staging nts weight
 import os
 import sys
 
-REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "image-captioning-with-different-decoders_amd"))
 import torch  # noqa: E402
 
