@@ -104,3 +104,60 @@ def conv_bn_stats_ref(y):
     mean = y.mean(dim=(0, 2, 3))
     var = y.var(dim=(0, 2, 3), unbiased=False)
     return mean, var, var * n / max(n - 1, 1)
+
+
+def _bf16(x):
+    """fp32 -> nearest bf16 (RNE) -> fp32."""
+    return x.to(torch.bfloat16).to(torch.float32)
+
+
+def _bn_train_fp64(y, bn):
+    """Train-mode BN scale / shift from the batch statistics of the STORED values y (NCHW fp32), summed in
+    fp64 and rounded as the GPU finalize rounds them (csrc/bn_final.h: var = E[y^2] - mean^2, clamped at 0)."""
+    yd = y.double()
+    n = yd.numel() // yd.shape[1]
+    s, q = yd.sum((0, 2, 3)), (yd * yd).sum((0, 2, 3))
+    mean = s / n
+    var = (q / n - mean * mean).clamp_min(0)
+    sc = (bn.weight.double() * (1.0 / torch.sqrt(var + bn.eps))).float()
+    sh = (bn.bias.double() - mean * sc.double()).float()
+    return sc.view(1, -1, 1, 1), sh.view(1, -1, 1, 1)
+
+
+@torch.no_grad()
+def encoder_forward_bf16_emulated(resnet, imgs):
+    """CPU restatement of the GPU bf16 encoder's ARITHMETIC (BASELINE config 5; capmi.resnet._forward_bf16),
+    for test infrastructure only: the layer4 map (N, 7, 7, 2048) NHWC fp32 of train-mode ResNet-101 where
+    * conv1 multiplies bf16-rounded images and weights with fp32 accumulation into an fp32 output, then BN + ReLU
+      + maxpool in fp32 and the result rounded to bf16 (capmi_bn_relu_maxpool, capmi_f32_to_bf16);
+    * every other conv multiplies bf16 activations by bf16-rounded weights with fp32 accumulation and stores
+      its output rounded to bf16 (CAPMI_GEMM_BF16_IO); BN statistics are those of the stored values;
+    * a conv input is bf16(relu(y * scale + shift)) (capmi_bn_relu_bf16), a block output
+      bf16(relu(y3 * s3 + b3 + res')) with res' = the bf16 block input, or yd * sd + bd for the downsample
+      branch (capmi_bn_add_relu_bf16).
+    The products of bf16 values are exact in fp32; only the fp32 summation order differs from the GPU's, so this
+    path's error against fp64 is the error the bf16 arithmetic itself makes."""
+    def conv(x, c):
+        return F.conv2d(x, _bf16(c.weight.float()), stride=c.stride, padding=c.padding)
+    r = resnet
+    y = F.conv2d(_bf16(imgs.float()), _bf16(r.conv1.weight.float()), stride=2, padding=3)
+    sc, sh = _bn_train_fp64(y, r.bn1)
+    x = _bf16(F.max_pool2d(torch.relu(y * sc + sh), 3, 2, 1))
+    for layer in (r.layer1, r.layer2, r.layer3, r.layer4):
+        for blk in layer:
+            y1 = _bf16(conv(x, blk.conv1))
+            s1, b1 = _bn_train_fp64(y1, blk.bn1)
+            y1 = _bf16(torch.relu(y1 * s1 + b1))
+            y2 = _bf16(conv(y1, blk.conv2))
+            s2, b2 = _bn_train_fp64(y2, blk.bn2)
+            y2 = _bf16(torch.relu(y2 * s2 + b2))
+            y3 = _bf16(conv(y2, blk.conv3))
+            s3, b3 = _bn_train_fp64(y3, blk.bn3)
+            if blk.downsample is not None:
+                yd = _bf16(conv(x, blk.downsample[0]))
+                sd, bd = _bn_train_fp64(yd, blk.downsample[1])
+                res = yd * sd + bd
+            else:
+                res = x
+            x = _bf16(torch.relu(y3 * s3 + b3 + res))
+    return x.permute(0, 2, 3, 1)

@@ -159,22 +159,25 @@ def named_keys(params):
 
 def test_config5_bert_bf16_step_b64():
     """bench.py's config 5: bf16 encoder, BERT-branch decoder (M = 768 word features) with bf16 GEMM
-    operands, pipelined graphs, dup = 2. (1) the bf16 encoder's 7x7 map at B = 64 vs the fp64 oracle
-    (train-mode BN; bn3.weight x 0.1 for conditioning, see tests/test_gpu_bf16.py) within 6e-2;
+    operands, pipelined graphs, dup = 2. (1) the bf16 encoder's 7x7 map at B = 64 on gen.resnet101_params as
+    generated (no re-conditioning): its rel. L2 error against the fp64 oracle at most 2x that of the CPU
+    restatement of the same bf16 arithmetic (oracle.resnet_ref.encoder_forward_bf16_emulated: bf16 operands,
+    fp32 accumulation, bf16-rounded conv outputs / inputs / block outputs, train-mode BN from the stored values),
+    on the full ResNet-101 (train-mode BN at random init amplifies the bf16 rounding to O(1) there: that path's
+    own error is ~0.8, so the rule is loose) and on a (1, 1, 1, 1) stack of the same generator (~0.04: the
+    rule has teeth);
     (2) the decoder on those features (fused_loss_and_grads, the call the step makes) vs the fp32 oracle
     BERT branch: loss rel. 2e-3, predictions / alphas rel. L2 1e-2, gradients rel. L2 3e-2 (1e-1 for
     the cancellation-heavy enc_att / dec_att); (3) the step itself (AttentionTrainStep, pipelined graphs):
     the same loss and gradients as (2), to fp32 summation noise."""
     from capmi import decoder_fn as DF
     from capmi.train_step import AttentionTrainStep
-    from oracle.resnet_ref import build_resnet101, encoder_attention_forward
+    from capmi.resnet import EncoderRunner, ResNet101
+    from oracle.resnet_ref import build_resnet101, encoder_attention_forward, encoder_forward_bf16_emulated
     from test_gpu_bert import _bert_decoder
     torch.set_num_threads(_threads())
     seed = 105
     params = gen.resnet101_params(seed)
-    for k in params:
-        if k.endswith("bn3.weight"):
-            params[k] = params[k] * 0.1
     enc = _encoder(params)
     enc.set_compute_precision("bf16")
     dec, p = _bert_decoder(512, 512, V, seed)
@@ -189,13 +192,33 @@ def test_config5_bert_bf16_step_b64():
     with torch.no_grad():
         twin.forward_into(x, fmap, pooled=False)
     torch.cuda.synchronize()
-    # (1) encoder
+    # (1) encoder: full depth, then a shallow stack of the same generator through the same runner
     r64 = build_resnet101(params).double().train()
     with torch.no_grad():
-        y64 = encoder_attention_forward(r64, x.cpu().double())
-    e = rel_err(_pooled(fmap).view(B, 14, 14, 2048), y64)
-    print(f"config 5 bf16 encoder B=64: rel L2 vs fp64 {e:.3g}")
-    assert e < 6e-2, e
+        y64 = encoder_attention_forward(r64, x.cpu().double(), out_hw=(7, 7))
+    emu = encoder_forward_bf16_emulated(build_resnet101(params).train(), x.cpu())
+    e, e_emu = rel_err(fmap, y64), rel_err(emu, y64)
+    print(f"config 5 bf16 encoder B=64: rel L2 vs fp64 {e:.3g} (CPU bf16 arithmetic {e_emu:.3g})")
+    assert e <= 2 * e_emu, (e, e_emu)
+    layers = (1, 1, 1, 1)
+    sp = gen.resnet101_params(seed, layers)
+    net = ResNet101(layers)
+    sd = net.state_dict()
+    for k, v in sp.items():
+        sd[k] = t(v).clone()
+    net.load_state_dict(sd)
+    runner = EncoderRunner()
+    runner.bf16 = True
+    with torch.no_grad():
+        sfmap = runner.forward(net.to(DEV).train(), x, out_hw=None)
+    torch.cuda.synchronize()
+    s64 = build_resnet101(sp, layers).double().train()
+    with torch.no_grad():
+        sy64 = encoder_attention_forward(s64, x.cpu().double(), out_hw=(7, 7))
+    semu = encoder_forward_bf16_emulated(build_resnet101(sp, layers).train(), x.cpu())
+    se, se_emu = rel_err(sfmap, sy64), rel_err(semu, sy64)
+    print(f"config 5 bf16 encoder {layers} B=64: rel L2 vs fp64 {se:.3g} (CPU bf16 arithmetic {se_emu:.3g})")
+    assert se <= 2 * se_emu, (se, se_emu)
     # (2) decoder on the same plan
     emb = dec.bert_embedder(t(caps, DEV))
     trainable = [n for n, q in dec.named_parameters() if q.requires_grad]

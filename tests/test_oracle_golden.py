@@ -251,3 +251,22 @@ def test_encoder_backward_masked_is_autograd_on_a_branch():
     # the forward moves by the flipped element's tiny value (layer4 barely changes); the gradients
     # routed through that decision move by a whole upstream element
     assert max(v for k, v in rel.items() if k.startswith("layer4")) < 1e-3 * rel["layer3.0.bn2.bias"], rel
+
+
+def test_bf16_emulation_is_the_fp32_forward_without_rounding(monkeypatch):
+    """oracle.resnet_ref.encoder_forward_bf16_emulated (the config-5 parity reference) restates the same
+    network as encoder_attention_forward: with its bf16 rounding made the identity it is the fp32 train-mode
+    forward (BN statistics in fp64 instead of torch's fp32: rounding-level differences only)."""
+    import gen
+    from oracle import resnet_ref as RR
+    layers = (1, 1, 1, 1)
+    params = gen.resnet101_params(31, layers)
+    x = torch.tensor(gen.images(31, 2))
+    ref = RR.encoder_attention_forward(RR.build_resnet101(params, layers).train(), x, out_hw=(7, 7)).detach()
+    monkeypatch.setattr(RR, "_bf16", lambda v: v)
+    got = RR.encoder_forward_bf16_emulated(RR.build_resnet101(params, layers).train(), x)
+    assert float((got - ref).norm() / ref.norm()) < 1e-5
+    monkeypatch.undo()
+    bf = RR.encoder_forward_bf16_emulated(RR.build_resnet101(params, layers).train(), x)
+    e = float((bf - ref).norm() / ref.norm())
+    assert 1e-3 < e < 0.2, e  # the rounding is applied (bf16: 2^-9 per rounding, amplified by train-mode BN)
