@@ -231,7 +231,7 @@ gemm_x3_kernel(const GemmArgs args) {
       }
 #pragma unroll
       for (int i = 0; i < NBr; ++i)
-        if (b_lds[i] >= 0) *reinterpret_cast<u32x4_x*>(&Bs[buf][0][b_lds[i]]) = st.b[i];
+        if ((3 * BN * 4) % XNT == 0 || b_lds[i] >= 0) *reinterpret_cast<u32x4_x*>(&Bs[buf][0][b_lds[i]]) = st.b[i];
     };
     auto compute = [&](int buf) {
       if constexpr (X3_M16) {

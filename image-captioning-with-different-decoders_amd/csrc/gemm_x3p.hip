@@ -155,36 +155,54 @@ gemm_x3p_kernel(const GemmArgs args) {
     const unsigned ss_bytes = PRO ? (unsigned)((AMODE == 2 ? cCin : P.K) * 4) : 0u;
     const auto rsc_p = rsrc_p(PRO ? (const void*)P.in_scale : P.B, ss_bytes);
     const auto rsh_p = rsrc_p(PRO ? (const void*)P.in_shift : P.B, ss_bytes);
-    // this lane's two A rows (row blocks 2 wid, 2 wid + 1) and one B row (row block wid)
-    // (arrays sized 2 >= NAB: a dependent bound in the nested lambda loses the host launch stub)
-    unsigned a_base[2];  // dense: byte offset of (row, chunk) in plane 0; conv: pixel index of (n, 0, 0)
-    int a_ih0[2], a_iw0[2], a_ch[2];
-    bool a_ok[2];
+    // X3P_LOADERS (A/B, BK = 32 x3p only): only waves 0 .. X3P_LOADERS-1 issue the LDS-DMA pieces, each also those
+    // of waves wid + X3P_LOADERS, ... (0: every wave its own). Piece k of a loader wave stands for wave vw(k).
+#ifndef X3P_LOADERS
+#define X3P_LOADERS 0
+#endif
+    constexpr int LW = (X3P_LOADERS > 0 && PBK == 32 && !ASPLIT) ? X3P_LOADERS : PNT / 64;
+    constexpr int REP = PNT / 64 / LW;
+    auto vw = [&](int k) { return wid + k * LW; };
+    // this lane's A rows (row blocks NAB vw(k) + i) and B row (row block vw(k)) per piece set k
+    // (fixed array bounds >= NAB * REP: a template-dependent bound used in the nested lambdas loses the host
+    // launch stub)
+    unsigned a_base[16];  // dense: byte offset of (row, chunk) in plane 0; conv: pixel index of (n, 0, 0)
+    int a_ih0[16], a_iw0[16], a_ch[16];
+    bool a_ok[16];
+#pragma unroll
+    for (int k = 0; k < REP; ++k)
 #pragma unroll
     for (int i = 0; i < NAB; ++i) {
-      const int r = (NAB * wid + i) * RPB + drow;
+      const int x = k * NAB + i;
+      const int r = (NAB * vw(k) + i) * RPB + drow;
       const int row = m0 + r;
-      a_ch[i] = dslot ^ swz<PBK>(r);
-      a_ok[i] = row < M;
+      a_ch[x] = dslot ^ swz<PBK>(r);
+      a_ok[x] = row < M;
       if (AMODE == 0) {
-        a_base[i] = (unsigned)(((long long)(a_ok[i] ? row : 0) * P.lda + a_ch[i] * 8) * 2);
-        a_ih0[i] = a_iw0[i] = 0;
+        a_base[x] = (unsigned)(((long long)(a_ok[x] ? row : 0) * P.lda + a_ch[x] * 8) * 2);
+        a_ih0[x] = a_iw0[x] = 0;
       } else {
         const int hw = P.cHo * P.cWo;
-        const int rr = a_ok[i] ? row : 0;
+        const int rr = a_ok[x] ? row : 0;
         const int n = rr / hw, rem = rr - n * hw;
         const int oh = rem / P.cWo, ow = rem - oh * P.cWo;
-        a_ih0[i] = oh * P.cStride - P.cPad;
-        a_iw0[i] = ow * P.cStride - P.cPad;
-        a_base[i] = (unsigned)(n * cH * cW);
+        a_ih0[x] = oh * P.cStride - P.cPad;
+        a_iw0[x] = ow * P.cStride - P.cPad;
+        a_base[x] = (unsigned)(n * cH * cW);
       }
     }
-    // B row block wid
+    // B row block vw(k)
     const bool bw = NBB == PNT / 64 || wid < NBB;  // (BK = 32: every wave issues one B row block)
-    const int br = wid * RPB + drow;
-    const int b_ch = dslot ^ swz<PBK>(br);
-    const bool b_ok = bw && n0 + br < N;
-    const unsigned b_base = (unsigned)(((long long)(b_ok ? n0 + br : 0) * P.ldb + b_ch * 8) * 2);
+    const bool loader = LW == PNT / 64 || wid < LW;
+    bool b_ok[8];
+    unsigned b_base[8];
+#pragma unroll
+    for (int k = 0; k < REP; ++k) {
+      const int br = vw(k) * RPB + drow;
+      const int b_ch = dslot ^ swz<PBK>(br);
+      b_ok[k] = bw && loader && n0 + br < N;
+      b_base[k] = (unsigned)(((long long)(b_ok[k] ? n0 + br : 0) * P.ldb + b_ch * 8) * 2);
+    }
     // x3d: four fp32 float4 slots per thread, slot i = row (tid + 512 i) / 8, k 4 ((tid + 512 i) % 8)
     constexpr int NSA = ASPLIT ? PBM / 64 : 1;
     const int aq = tid & 7;
@@ -267,18 +285,18 @@ gemm_x3p_kernel(const GemmArgs args) {
       // plane-0 byte offset of this lane's A piece and its out-of-range bit (kOOBp: padding taps, rows past M, k past
       // the end), combined per plane below without a branch (an exec-masked offset computation split the DMA issue
       // into basic blocks of its own, out of reach of the MFMA interleave)
-      unsigned aoff[2], abad[2];
+      unsigned aoff[16], abad[16];
 #pragma unroll
-      for (int i = 0; i < NAB; ++i) {
+      for (int x = 0; x < NAB * REP; ++x) {
         if (ASPLIT) break;
         if (AMODE == 0) {
-          aoff[i] = a_base[i] + (unsigned)k * 2;
-          abad[i] = a_ok[i] && kok ? 0u : kOOBp;
+          aoff[x] = a_base[x] + (unsigned)k * 2;
+          abad[x] = a_ok[x] && kok ? 0u : kOOBp;
         } else {
-          const int ih = a_ih0[i] + c_kh, iw = a_iw0[i] + c_kw;
-          const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
-          aoff[i] = ((a_base[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + c_sub * PBK + a_ch[i] * 8)) * 2u;
-          abad[i] = ok ? 0u : kOOBp;
+          const int ih = a_ih0[x] + c_kh, iw = a_iw0[x] + c_kw;
+          const bool ok = a_ok[x] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
+          aoff[x] = ((a_base[x] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + c_sub * PBK + a_ch[x] * 8)) * 2u;
+          abad[x] = ok ? 0u : kOOBp;
         }
       }
       if (AMODE == 2 && ++c_sub == SUB) {
@@ -292,20 +310,27 @@ gemm_x3p_kernel(const GemmArgs args) {
         }
       }
       unsigned char* base = lds + buf * PBUF;
+      if (loader) {
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
+        for (int kk = 0; kk < REP; ++kk) {
 #pragma unroll
-        for (int i = 0; i < (ASPLIT ? 0 : NAB); ++i)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              ra, (lds_ptr_t)(base + p * PBM * PROWB + (NAB * wid + i) * RPB * PROWB), 16,
-              PBK == 32 ? (aoff[i] + p * pA2) | abad[i] : (abad[i] ? kOOBp : aoff[i] + p * pA2), 0, 0, 0);
-      if (bw) {
-        const unsigned boff = b_base + (unsigned)k * 2, bbad = b_ok && kok ? 0u : kOOBp;
-        // (BK = 16, at its 128-register cap, keeps the select form: the branch-free one spilled it)
+          for (int p = 0; p < 3; ++p)
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * RPB * PROWB),
-                                                   16, PBK == 32 ? (boff + p * pB2) | bbad : (bbad ? kOOBp : boff + p * pB2), 0, 0, 0);
+            for (int i = 0; i < (ASPLIT ? 0 : NAB); ++i) {
+              const int x = kk * NAB + i;
+              __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                  ra, (lds_ptr_t)(base + p * PBM * PROWB + (NAB * vw(kk) + i) * RPB * PROWB), 16,
+                  PBK == 32 ? (aoff[x] + p * pA2) | abad[x] : (abad[x] ? kOOBp : aoff[x] + p * pA2), 0, 0, 0);
+            }
+          if (bw) {
+            const unsigned boff = b_base[kk] + (unsigned)k * 2, bbad = b_ok[kk] && kok ? 0u : kOOBp;
+            // (BK = 16, at its 128-register cap, keeps the select form: the branch-free one spilled it)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+              __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + vw(kk) * RPB * PROWB),
+                                                       16, PBK == 32 ? (boff + p * pB2) | bbad : (bbad ? kOOBp : boff + p * pB2), 0, 0, 0);
+          }
+        }
       }
     };
     // x3d: fp32 A registers of one k-tile -> (prologue) -> three planes
@@ -315,6 +340,12 @@ gemm_x3p_kernel(const GemmArgs args) {
 #pragma unroll
       for (int i = 0; i < NSA; ++i) {
         float4 v = ar[i];
+#if X3D_NOSPLIT  // timing-only builds: no prologue / split VALU, the raw bits stored (wrong results)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          *reinterpret_cast<uint2*>(base + p * PBM * PROWB + s_lds[i]) = make_uint2(__float_as_uint(v.x), __float_as_uint(v.z));
+        continue;
+#endif
         if (PRO) v = make_float4(fmaxf(fmaf(v.x, sc.x, sh.x), 0.f), fmaxf(fmaf(v.y, sc.y, sh.y), 0.f),
                                  fmaxf(fmaf(v.z, sc.z, sh.z), 0.f), fmaxf(fmaf(v.w, sc.w, sh.w), 0.f));
         if (!((msk >> i) & 1u)) v = make_float4(0.f, 0.f, 0.f, 0.f);  // padding taps: zeros AFTER the BN
@@ -429,7 +460,7 @@ gemm_x3p_kernel(const GemmArgs args) {
       const int k = k_lo + kt * PBK;
       unsigned char* base = lds + buf * PBUF;
       if (bw) {
-        const unsigned boff = b_base + (unsigned)k * 2, bbad = b_ok && k < k_hi ? 0u : kOOBp;
+        const unsigned boff = b_base[0] + (unsigned)k * 2, bbad = b_ok[0] && k < k_hi ? 0u : kOOBp;
 #pragma unroll
         for (int p = 0; p < 3; ++p)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * RPB * PROWB),
@@ -471,6 +502,12 @@ gemm_x3p_kernel(const GemmArgs args) {
     auto a_split = [&](int buf, int i) {  // slot i -> (prologue) -> three planes of buffer buf
       unsigned char* base = lds + buf * PBUF;
       float4 v = areg[i];
+#if X3D_NOSPLIT  // timing-only builds (above)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        *reinterpret_cast<uint2*>(base + p * PBM * PROWB + s_lds[i]) = make_uint2(__float_as_uint(v.x), __float_as_uint(v.z));
+      return;
+#endif
       if (PRO) v = make_float4(fmaxf(fmaf(v.x, a_sc.x, a_sh.x), 0.f), fmaxf(fmaf(v.y, a_sc.y, a_sh.y), 0.f),
                                fmaxf(fmaf(v.z, a_sc.z, a_sh.z), 0.f), fmaxf(fmaf(v.w, a_sc.w, a_sh.w), 0.f));
       const bool keep = (a_msk >> i) & 1u;  // padding taps / rows past M: zeros AFTER the BN
@@ -490,9 +527,6 @@ gemm_x3p_kernel(const GemmArgs args) {
 #ifndef X3P_PHASE
 #define X3P_PHASE 2
 #endif
-#ifndef X3D_VPM
-#define X3D_VPM 2  // x3d round-5 loop: VALU per MFMA in the interleave
-#endif
     // the six products of row block i of a k-tile, smallest terms first per accumulator
     auto mm6 = [&](int i, const bf16x8_p (&a)[3], const bf16x8_p (&b)[JN][3]) {
 #pragma unroll
@@ -508,141 +542,6 @@ gemm_x3p_kernel(const GemmArgs args) {
         acc4[i][j] = mf16(a[0], b[j][0], acc4[i][j]);
       }
     };
-#ifndef X3D_V2
-#define X3D_V2 0
-#endif
-    if constexpr (ASPLIT && M16 && X3D_V2 != 0) {
-      // x3d, round 5: one barrier per k-tile, before row block 3's MFMAs (the A fragments are read one row block
-      // ahead, so every read of tile kt is issued by then). Behind it buffer kt & 1 is free and tile kt + 2 is
-      // staged into it over a whole k-tile -- its B planes by LDS-DMA at once, its four A slots (loaded a k-tile
-      // earlier) split one per row block: slot 0 during block 3 of tile kt, slots 1-3 during blocks 0-2 of tile
-      // kt + 1 (which read the other buffer), each register reloaded at once with tile kt + 3's -- so the split
-      // VALU is spread over all 96 MFMAs of a k-tile and every DMA and load has a k-tile to land. The BN scale /
-      // shift of the tile being split and of the next one are two register sets.
-      const int c16 = lane >> 4, rl16 = lane & 15;
-      auto frag = [&](const unsigned char* plane, int r) {
-        return *reinterpret_cast<const bf16x8_p*>(plane + r * PROWB + ((c16 ^ swz<PBK>(r)) << 4));
-      };
-      auto ss_load = [&](int kt, float4& sc, float4& sh) {  // BN scale / shift of tile kt (at the walk's channel)
-        if (PRO) {  // always two loads (the barrier's vmcnt relies on it); past the end: out of range, zeros
-          const int k = k_lo + kt * PBK;
-          const unsigned ch = k < k_hi ? (unsigned)((AMODE == 2 ? c_ci : k) + aq * 4) * 4u : kOOBp;
-          sc = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsc_p, ch, 0, 0));
-          sh = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsh_p, ch, 0, 0));
-        }
-      };
-      auto walk = [&] {  // the conv walk advances one k-tile (32-deep: one (channel slice, tap) chunk)
-        if (AMODE == 2 && ++c_kw == cKW) {
-          c_kw = 0;
-          if (++c_kh == P.cKH) {
-            c_kh = 0;
-            c_ci += 32;
-          }
-        }
-      };
-      auto split = [&](int buf, int i, float4 sc, float4 sh) {  // slot i -> (prologue) -> three planes of buf
-        unsigned char* base = lds + buf * PBUF;
-        float4 v = areg[i];
-        if (PRO) v = make_float4(fmaxf(fmaf(v.x, sc.x, sh.x), 0.f), fmaxf(fmaf(v.y, sc.y, sh.y), 0.f),
-                                 fmaxf(fmaf(v.z, sc.z, sh.z), 0.f), fmaxf(fmaf(v.w, sc.w, sh.w), 0.f));
-        // padding taps / rows past M read zeros: with the prologue they must be zeros AFTER the BN (without it the
-        // zeros pass through the split as they are); unconditional, a uniform branch here would cut the block's
-        // MFMA interleave into separate scheduling regions
-        if (PRO) {
-          const bool keep = (a_msk >> i) & 1u;
-          v.x = keep ? v.x : 0.f;
-          v.y = keep ? v.y : 0.f;
-          v.z = keep ? v.z : 0.f;
-          v.w = keep ? v.w : 0.f;
-        }
-        unsigned lo[3], hi[3];
-        split3_pair(v.x, v.y, lo);
-        split3_pair(v.z, v.w, hi);
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          *reinterpret_cast<uint2*>(base + p * PBM * PROWB + s_lds[i]) = make_uint2(lo[p], hi[p]);
-      };
-      // one k-step. (sc0, sh0): the BN scale / shift of tile kt + 1, whose slots 1-3 are split in blocks 0-2, then
-      // reloaded with tile kt + 3's in block 3; (sc1, sh1): tile kt + 2's, used from block 3 on. The caller swaps
-      // the two sets every step (the loop is unrolled by two so that neither is ever copied: a loop-carried copy of
-      // a register just loaded made the compiler drain vmcnt at the back edge)
-      auto kstep = [&](int kt, float4& sc0, float4& sh0, float4& sc1, float4& sh1) {
-        const unsigned char* A_ = lds + (kt & 1) * PBUF;
-        const unsigned char* B_ = A_ + PA_BYTES;
-        bf16x8_p b[JN][3], a[3];
-#pragma unroll
-        for (int j = 0; j < JN; ++j)
-#pragma unroll
-          for (int p = 0; p < 3; ++p) b[j][p] = frag(B_ + p * PBN * PROWB, wn0 + 16 * j + rl16);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) a[p] = frag(A_ + p * PBM * PROWB, wm0 + rl16);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          bf16x8_p an[3];
-          if (i < 3) {
-#pragma unroll
-            for (int p = 0; p < 3; ++p) an[p] = frag(A_ + p * PBM * PROWB, wm0 + 16 * (i + 1) + rl16);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          if (i < 3) {
-            // slot i + 1 of tile kt + 1 into buffer (kt + 1) & 1, then its register takes tile kt + 2's
-            split((kt + 1) & 1, i + 1, sc0, sh0);
-            a_load(kt + 2, i + 1);
-            if (i == 2) walk();  // (the walk now stands at tile kt + 3)
-          } else {
-            // tile kt + 1's B planes landed (only the 4 A loads and 2 scale / shift loads issued after its DMA are
-            // younger), this wave's reads of tile kt and split stores of tile kt + 1 are done: after the barrier
-            // tile kt + 1 is complete and buffer kt & 1 free for tile kt + 2
-            if constexpr (PRO)
-              asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            else
-              asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            b_dma(kt + 2, kt & 1);
-            __builtin_amdgcn_sched_barrier(0);  // (the DMA stays older than every register load after it)
-            split(kt & 1, 0, sc1, sh1);
-            a_load(kt + 3, 0);
-            ss_load(kt + 3, sc0, sh0);
-          }
-          mm6(i, a, b);
-#pragma unroll
-          for (int r = 0; r < 6 * JN; ++r) {  // the slot's split VALU among the block's MFMAs
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, X3D_VPM, 0);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          if (i < 3) {
-#pragma unroll
-            for (int p = 0; p < 3; ++p) a[p] = an[p];
-          }
-        }
-      };
-      // prologue: tile 0 staged; tile 1's B DMA issued and its A loaded, slot 0 split ("block 3 of tile -1")
-      float4 scA = make_float4(1.f, 1.f, 1.f, 1.f), shA = make_float4(0.f, 0.f, 0.f, 0.f), scB = scA, shB = shA;
-      b_dma(0, 0);
-#pragma unroll
-      for (int i = 0; i < NSA; ++i) a_load(0, i);
-      ss_load(0, scA, shA);
-      walk();
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int i = 0; i < NSA; ++i) split(0, i, scA, shA);
-      b_dma(1, 1);
-#pragma unroll
-      for (int i = 0; i < NSA; ++i) a_load(1, i);
-      ss_load(1, scA, shA);
-      walk();
-      __syncthreads();  // tile 0 complete (its B DMA waited above, its split stores by the barrier's lgkmcnt)
-      split(1, 0, scA, shA);
-      a_load(2, 0);
-      ss_load(2, scB, shB);
-      for (int kt = 0; kt < nkt; kt += 2) {
-        kstep(kt, scA, shA, scB, shB);
-        if (kt + 1 < nkt) kstep(kt + 1, scB, shB, scA, shA);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the loads and DMA past the end drained)
-      __syncthreads();  // (the next tile's prologue rewrites buffers 0 and 1)
-      return;
-    }
     if (ASPLIT && M16 && X3D_PIPE && args.x3d_pipe) {
       // x3d, round 4: A two k-tiles deep in ONE register set. During tile kt's MFMAs each of the thread's four
       // float4 slots is split into the other buffer for tile kt + 1 and at once reloaded with tile kt + 2's
@@ -743,29 +642,23 @@ gemm_x3p_kernel(const GemmArgs args) {
           const int r = wn0 + 16 * j + rl;
           const int o = r * PROWB + ((c ^ swz<PBK>(r)) << 4);
 #pragma unroll
+#if X3P_SKIP & 2  // timing-only: no LDS reads
+          for (int p = 0; p < 3; ++p) b[j][p] = bf16x8_p{} + (__bf16)(float)(o - p);
+#else
           for (int p = 0; p < 3; ++p) b[j][p] = *reinterpret_cast<const bf16x8_p*>(B_ + p * PBN * PROWB + o);
+#endif
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = wm0 + 16 * i + rl;
           const int o = r * PROWB + ((c ^ swz<PBK>(r)) << 4);
 #pragma unroll
+#if X3P_SKIP & 2  // timing-only: no LDS reads
+          for (int p = 0; p < 3; ++p) a[i][p] = bf16x8_p{} + (__bf16)(float)(o + p);
+#else
           for (int p = 0; p < 3; ++p) a[i][p] = *reinterpret_cast<const bf16x8_p*>(A_ + p * PBM * PROWB + o);
+#endif
         }
-        auto mm = [&](int i) {  // the six products of row block i, smallest terms first per accumulator
-#pragma unroll
-          for (int j = 0; j < JN; ++j) {
-            acc4[i][j] = mf16(a[i][1], b[j][1], acc4[i][j]);
-            acc4[i][j] = mf16(a[i][0], b[j][2], acc4[i][j]);
-            acc4[i][j] = mf16(a[i][2], b[j][0], acc4[i][j]);
-          }
-#pragma unroll
-          for (int j = 0; j < JN; ++j) {
-            acc4[i][j] = mf16(a[i][0], b[j][1], acc4[i][j]);
-            acc4[i][j] = mf16(a[i][1], b[j][0], acc4[i][j]);
-            acc4[i][j] = mf16(a[i][0], b[j][0], acc4[i][j]);
-          }
-        };
         // X3P_PHASE = row blocks multiplied before the barrier (1-3)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -777,7 +670,7 @@ gemm_x3p_kernel(const GemmArgs args) {
             __builtin_amdgcn_sched_barrier(0);
             issue(kt + 2, kt & 1);  // (past the end: zeros, no memory traffic; keeps the DMA branch-free)
           }
-          mm(i);
+          mm6(i, a[i], b);
         }
 #pragma unroll
         for (int r = 0; r < 9; ++r) {  // the DMA pieces spread over the MFMAs after the barrier

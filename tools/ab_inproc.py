@@ -1,6 +1,7 @@
 """Same-process A/B of library builds on single conv GEMM launches: every build is loaded side by side
 (capmi._lib._load) and the builds take turns, `--rounds` times, on the same tensors, so clock and box drift
-fall on all arms alike. Prints the median us per launch of each build per case.
+fall on all arms alike. Prints the median us per launch of each build per case, and whether each build's output
+equals the first build's bit for bit.
 
 python tools/ab_inproc.py --libs base,ab/ph2.so --cases "l3c2:--x3p l3c3:--x3d,--dense" [--reps 20 --rounds 7]
 (base = the in-tree libcapmi.so; a case is a tools/gemm_one.py shape and its flags, commas for spaces)"""
@@ -33,6 +34,14 @@ def main():
         g = parser().parse_args(["--shape", shape] + [f for f in flags.split(",") if f])
         run, M, N, Kd = setup(g)
         times = {n: [] for n in names}
+        same = {}
+        for n in names:
+            _lib.lib = libs[n]
+            run.out.fill_(float("nan"))
+            run()
+            torch.cuda.synchronize()
+            same[n] = torch.equal(run.out, same[names[0]]) if n != names[0] else run.out.clone()
+        same[names[0]] = True
         for _ in range(a.rounds):
             for n in names:
                 _lib.lib = libs[n]
@@ -45,7 +54,7 @@ def main():
                 torch.cuda.synchronize()
                 times[n].append(s.elapsed_time(e) * 1e3 / a.reps)
         _lib.lib = base
-        print(f"| {case} | " + " | ".join(f"{st.median(times[n]):.1f}" for n in names) + " |", flush=True)
+        print(f"| {case} | " + " | ".join(f"{st.median(times[n]):.1f}{'' if same[n] else ' (DIFFERS)'}" for n in names) + " |", flush=True)
 
 
 if __name__ == "__main__":
