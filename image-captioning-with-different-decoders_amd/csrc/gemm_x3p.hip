@@ -155,54 +155,36 @@ gemm_x3p_kernel(const GemmArgs args) {
     const unsigned ss_bytes = PRO ? (unsigned)((AMODE == 2 ? cCin : P.K) * 4) : 0u;
     const auto rsc_p = rsrc_p(PRO ? (const void*)P.in_scale : P.B, ss_bytes);
     const auto rsh_p = rsrc_p(PRO ? (const void*)P.in_shift : P.B, ss_bytes);
-    // X3P_LOADERS (A/B, BK = 32 x3p only): only waves 0 .. X3P_LOADERS-1 issue the LDS-DMA pieces, each also those
-    // of waves wid + X3P_LOADERS, ... (0: every wave its own). Piece k of a loader wave stands for wave vw(k).
-#ifndef X3P_LOADERS
-#define X3P_LOADERS 0
-#endif
-    constexpr int LW = (X3P_LOADERS > 0 && PBK == 32 && !ASPLIT) ? X3P_LOADERS : PNT / 64;
-    constexpr int REP = PNT / 64 / LW;
-    auto vw = [&](int k) { return wid + k * LW; };
-    // this lane's A rows (row blocks NAB vw(k) + i) and B row (row block vw(k)) per piece set k
-    // (fixed array bounds >= NAB * REP: a template-dependent bound used in the nested lambdas loses the host
-    // launch stub)
-    unsigned a_base[16];  // dense: byte offset of (row, chunk) in plane 0; conv: pixel index of (n, 0, 0)
-    int a_ih0[16], a_iw0[16], a_ch[16];
-    bool a_ok[16];
-#pragma unroll
-    for (int k = 0; k < REP; ++k)
+    // this lane's two A rows (row blocks 2 wid, 2 wid + 1) and one B row (row block wid)
+    // (arrays sized 2 >= NAB: a dependent bound in the nested lambda loses the host launch stub)
+    unsigned a_base[2];  // dense: byte offset of (row, chunk) in plane 0; conv: pixel index of (n, 0, 0)
+    int a_ih0[2], a_iw0[2], a_ch[2];
+    bool a_ok[2];
 #pragma unroll
     for (int i = 0; i < NAB; ++i) {
-      const int x = k * NAB + i;
-      const int r = (NAB * vw(k) + i) * RPB + drow;
+      const int r = (NAB * wid + i) * RPB + drow;
       const int row = m0 + r;
-      a_ch[x] = dslot ^ swz<PBK>(r);
-      a_ok[x] = row < M;
+      a_ch[i] = dslot ^ swz<PBK>(r);
+      a_ok[i] = row < M;
       if (AMODE == 0) {
-        a_base[x] = (unsigned)(((long long)(a_ok[x] ? row : 0) * P.lda + a_ch[x] * 8) * 2);
-        a_ih0[x] = a_iw0[x] = 0;
+        a_base[i] = (unsigned)(((long long)(a_ok[i] ? row : 0) * P.lda + a_ch[i] * 8) * 2);
+        a_ih0[i] = a_iw0[i] = 0;
       } else {
         const int hw = P.cHo * P.cWo;
-        const int rr = a_ok[x] ? row : 0;
+        const int rr = a_ok[i] ? row : 0;
         const int n = rr / hw, rem = rr - n * hw;
         const int oh = rem / P.cWo, ow = rem - oh * P.cWo;
-        a_ih0[x] = oh * P.cStride - P.cPad;
-        a_iw0[x] = ow * P.cStride - P.cPad;
-        a_base[x] = (unsigned)(n * cH * cW);
+        a_ih0[i] = oh * P.cStride - P.cPad;
+        a_iw0[i] = ow * P.cStride - P.cPad;
+        a_base[i] = (unsigned)(n * cH * cW);
       }
     }
-    // B row block vw(k)
+    // B row block wid
     const bool bw = NBB == PNT / 64 || wid < NBB;  // (BK = 32: every wave issues one B row block)
-    const bool loader = LW == PNT / 64 || wid < LW;
-    bool b_ok[8];
-    unsigned b_base[8];
-#pragma unroll
-    for (int k = 0; k < REP; ++k) {
-      const int br = vw(k) * RPB + drow;
-      const int b_ch = dslot ^ swz<PBK>(br);
-      b_ok[k] = bw && loader && n0 + br < N;
-      b_base[k] = (unsigned)(((long long)(b_ok[k] ? n0 + br : 0) * P.ldb + b_ch * 8) * 2);
-    }
+    const int br = wid * RPB + drow;
+    const int b_ch = dslot ^ swz<PBK>(br);
+    const bool b_ok = bw && n0 + br < N;
+    const unsigned b_base = (unsigned)(((long long)(b_ok ? n0 + br : 0) * P.ldb + b_ch * 8) * 2);
     // x3d: four fp32 float4 slots per thread, slot i = row (tid + 512 i) / 8, k 4 ((tid + 512 i) % 8)
     constexpr int NSA = ASPLIT ? PBM / 64 : 1;
     const int aq = tid & 7;
@@ -285,18 +267,18 @@ gemm_x3p_kernel(const GemmArgs args) {
       // plane-0 byte offset of this lane's A piece and its out-of-range bit (kOOBp: padding taps, rows past M, k past
       // the end), combined per plane below without a branch (an exec-masked offset computation split the DMA issue
       // into basic blocks of its own, out of reach of the MFMA interleave)
-      unsigned aoff[16], abad[16];
+      unsigned aoff[2], abad[2];
 #pragma unroll
-      for (int x = 0; x < NAB * REP; ++x) {
+      for (int i = 0; i < NAB; ++i) {
         if (ASPLIT) break;
         if (AMODE == 0) {
-          aoff[x] = a_base[x] + (unsigned)k * 2;
-          abad[x] = a_ok[x] && kok ? 0u : kOOBp;
+          aoff[i] = a_base[i] + (unsigned)k * 2;
+          abad[i] = a_ok[i] && kok ? 0u : kOOBp;
         } else {
-          const int ih = a_ih0[x] + c_kh, iw = a_iw0[x] + c_kw;
-          const bool ok = a_ok[x] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
-          aoff[x] = ((a_base[x] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + c_sub * PBK + a_ch[x] * 8)) * 2u;
-          abad[x] = ok ? 0u : kOOBp;
+          const int ih = a_ih0[i] + c_kh, iw = a_iw0[i] + c_kw;
+          const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
+          aoff[i] = ((a_base[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + c_sub * PBK + a_ch[i] * 8)) * 2u;
+          abad[i] = ok ? 0u : kOOBp;
         }
       }
       if (AMODE == 2 && ++c_sub == SUB) {
@@ -310,27 +292,20 @@ gemm_x3p_kernel(const GemmArgs args) {
         }
       }
       unsigned char* base = lds + buf * PBUF;
-      if (loader) {
 #pragma unroll
-        for (int kk = 0; kk < REP; ++kk) {
+      for (int p = 0; p < 3; ++p)
 #pragma unroll
-          for (int p = 0; p < 3; ++p)
+        for (int i = 0; i < (ASPLIT ? 0 : NAB); ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              ra, (lds_ptr_t)(base + p * PBM * PROWB + (NAB * wid + i) * RPB * PROWB), 16,
+              PBK == 32 ? (aoff[i] + p * pA2) | abad[i] : (abad[i] ? kOOBp : aoff[i] + p * pA2), 0, 0, 0);
+      if (bw) {
+        const unsigned boff = b_base + (unsigned)k * 2, bbad = b_ok && kok ? 0u : kOOBp;
+        // (BK = 16, at its 128-register cap, keeps the select form: the branch-free one spilled it)
 #pragma unroll
-            for (int i = 0; i < (ASPLIT ? 0 : NAB); ++i) {
-              const int x = kk * NAB + i;
-              __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                  ra, (lds_ptr_t)(base + p * PBM * PROWB + (NAB * vw(kk) + i) * RPB * PROWB), 16,
-                  PBK == 32 ? (aoff[x] + p * pA2) | abad[x] : (abad[x] ? kOOBp : aoff[x] + p * pA2), 0, 0, 0);
-            }
-          if (bw) {
-            const unsigned boff = b_base[kk] + (unsigned)k * 2, bbad = b_ok[kk] && kok ? 0u : kOOBp;
-            // (BK = 16, at its 128-register cap, keeps the select form: the branch-free one spilled it)
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-              __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + vw(kk) * RPB * PROWB),
-                                                       16, PBK == 32 ? (boff + p * pB2) | bbad : (bbad ? kOOBp : boff + p * pB2), 0, 0, 0);
-          }
-        }
+        for (int p = 0; p < 3; ++p)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * RPB * PROWB),
+                                                   16, PBK == 32 ? (boff + p * pB2) | bbad : (bbad ? kOOBp : boff + p * pB2), 0, 0, 0);
       }
     };
     // x3d: fp32 A registers of one k-tile -> (prologue) -> three planes
@@ -460,7 +435,7 @@ gemm_x3p_kernel(const GemmArgs args) {
       const int k = k_lo + kt * PBK;
       unsigned char* base = lds + buf * PBUF;
       if (bw) {
-        const unsigned boff = b_base[0] + (unsigned)k * 2, bbad = b_ok[0] && k < k_hi ? 0u : kOOBp;
+        const unsigned boff = b_base + (unsigned)k * 2, bbad = b_ok && k < k_hi ? 0u : kOOBp;
 #pragma unroll
         for (int p = 0; p < 3; ++p)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(base + PA_BYTES + p * PBN * PROWB + wid * RPB * PROWB),
