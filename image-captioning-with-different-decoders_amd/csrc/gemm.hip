@@ -812,7 +812,12 @@ int gemm_bf16_io(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
     CAPMI_REQUIRE((long long)p.M * p.lda * 2 < (1LL << 31), CAPMI_ERANGE);
   }
   if (p.M == 0) return 0;
-  const int bm = 128, bn = (tile == CAPMI_TILE_128x64 || tile == CAPMI_TILE_64 || (tile == CAPMI_TILE_AUTO && p.N <= 64)) ? 64 : 128;
+  // AUTO on a short k (K <= 256: the bf16 config's 1x1 c3 convs and layer1's K = 64 convs): 128x64 tiles, one LDS
+  // stage, four workgroups per CU, data-parallel (round 5: l3 c3 20.0 -> 17.1 us, l2 c3 24.7 -> 18.4, l1 c3 33.3 ->
+  // 24.3; at K = 512 a tie and above it slower: the two-stage 128x128 form stays)
+  const bool st1 = tile == CAPMI_TILE_AUTO && p.K <= 256;
+  const int bm = 128,
+            bn = (st1 || tile == CAPMI_TILE_128x64 || tile == CAPMI_TILE_64 || (tile == CAPMI_TILE_AUTO && p.N <= 64)) ? 64 : 128;
   GemmArgs a;
   memset(&a, 0, sizeof(a));
   a.nprob = 1;
@@ -820,6 +825,7 @@ int gemm_bf16_io(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
   a.tiles_m[0] = (int)cdiv(p.M, bm);
   a.tiles_n[0] = (int)cdiv(p.N, bn);
   a.plain_epi = plain_epilogue(p, bn);  // (bf16 C: the fp32 bound on M * ldc is the stricter one)
+  if (p.ldc % 8 != 0 || !aligned16(p.C)) a.plain_epi = 0;  // (its 16-B row-chunk stores)
   const long long total = (long long)a.tiles_m[0] * a.tiles_n[0];
   a.tiles_begin[1] = (int)total;
   const int cus = cu_count();
@@ -834,7 +840,8 @@ int gemm_bf16_io(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
   }();
   const bool sk = bf16_sk && !sk_off() && workspace != nullptr && nkt >= 4 &&
                   (double)total / (double)(rounds * slots) < 0.9;
-  if (!sk) return gemm_bf16_launch(a, amode, bm, bn, (int)total, s);
+  if (st1) return gemm_bf16_launch(a, amode, bm, bn, (int)total, s, 1);
+  if (!sk) return gemm_bf16_launch(a, amode, bm, bn, (int)total, s, 2);
   CAPMI_REQUIRE(aligned16(workspace), CAPMI_EINVAL);
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
   a.sk_nkt = nkt;
@@ -843,7 +850,7 @@ int gemm_bf16_io(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
   a.sk_groups = sk_xcd_groups() && a.sk_workers % 8 == 0 && total >= 64 ? 8 : 1;
   a.sk_flags = static_cast<int*>(workspace);
   a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
-  return gemm_bf16_launch(a, amode, bm, bn, a.sk_workers, s);
+  return gemm_bf16_launch(a, amode, bm, bn, a.sk_workers, s, 2);
 }
 }  // namespace
 

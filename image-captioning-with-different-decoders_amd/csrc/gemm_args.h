@@ -120,7 +120,7 @@ inline int plain_epilogue(const capmi_gemm_problem& p, int bn) {
 int gemm_nt_launch(const GemmArgs& a, int amode, int bmode, int bm, int bn, int blocks, hipStream_t s,
                    int terms = 0, int nt = 256);
 // bf16-in/bf16-out conv GEMM (gemm_bf16.hip): BM = 128, BN in {128, 64}, amode 0 (dense) / 2 (conv)
-int gemm_bf16_launch(const GemmArgs& a, int amode, int bm, int bn, int blocks, hipStream_t s);
+int gemm_bf16_launch(const GemmArgs& a, int amode, int bm, int bn, int blocks, hipStream_t s, int stages);
 // fp32-accurate 3-way bf16 split GEMM (gemm_x3.hip): BM = 128, BN in {128, 64}, 512 threads,
 // amode 0 (dense) / 2 (conv, optional prologue)
 int gemm_x3_launch(const GemmArgs& a, int amode, int bn, int blocks, hipStream_t s);

@@ -15,7 +15,9 @@
 //   * LDS rows of 72 bf16 (144 B): the 16-lane groups of ds_read_b128 / 8-lane groups of
 //     ds_write_b128 hit 64 distinct banks; lane (r, h) reads k 16g+8h..+7 of row r, the operand
 //     layout of the 32x32x16 bf16 MFMA;
-//   * tiles 128x128 (wave 64x64: 4 MFMAs per 4 ds_read_b128) or 128x64.
+//   * tiles 128x128 (wave 64x64: 4 MFMAs per 4 ds_read_b128) or 128x64;
+//   * round 5: for K <= 256 a one-stage 128x64 form at four workgroups per CU (ST = 1 below), and the
+//     store-only epilogue leaves through LDS as 16-B row chunks.
 #include "gemm_args.h"
 
 namespace {
@@ -26,6 +28,9 @@ typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 constexpr unsigned kOOB = 0x80000000u;  // buffer offset past every operand: the load returns 0
 constexpr int kSc1h = 16;
+#ifndef BF16_SKIP  // timing-only builds (wrong results): 1 no C stores, 2 no MFMAs, 4 no operand loads
+#define BF16_SKIP 0
+#endif
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
@@ -43,14 +48,18 @@ __device__ __forceinline__ unsigned pack_bf(float lo, float hi) {
   return (unsigned)bf16_bits(lo) | ((unsigned)bf16_bits(hi) << 16);
 }
 
-template <int BM, int BN, int AMODE, bool SK>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+// ST = LDS stages: 2 (two register stages ahead, two workgroups per CU) or 1 (round 5, 128x64 data-parallel only:
+// one LDS stage, one register stage ahead, four workgroups per CU -- the short-k 1x1 convs, where a tile's few
+// k-tiles leave no steady state to pipeline and more resident tiles hide the load latency instead)
+template <int BM, int BN, int AMODE, bool SK, int ST>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST == 1 ? 4 : 2)))
 gemm_bf16_kernel(const GemmArgs args) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
   constexpr int NA = BM * BKH / 8 / 256, NB = BN * BKH / 8 / 256;
   static_assert(NA >= 1 && NB >= 1 && WM == 64, "tile");
-  __shared__ __attribute__((aligned(16))) __bf16 As[2][BM * SBH];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BN * SBH];
+  __shared__ __attribute__((aligned(16))) __bf16 lds_tile[ST * (BM + BN) * SBH];
+  __bf16* const As = lds_tile;                  // [ST][BM * SBH]
+  __bf16* const Bs = lds_tile + ST * BM * SBH;  // [ST][BN * SBH]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
@@ -59,25 +68,27 @@ gemm_bf16_kernel(const GemmArgs args) {
 
   f32x16 acc[TM][TN];
 
-  auto mainloop = [&](const capmi_gemm_problem& P, int m0, int n0, int k_lo, int k_hi) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    const int nkt = (k_hi - k_lo) / BKH;
-    if (nkt <= 0) return;
+  // operand walk of the current tile (set by begin_tile), the two register stages of the prefetch
+  const capmi_gemm_problem& P0 = args.p[0];
+  const unsigned a_bytes = AMODE == 2 ? (unsigned)((long long)P0.cN * P0.cH * P0.cW * P0.cCin * 2)
+                                      : (unsigned)((long long)P0.M * P0.lda * 2);
+  const auto ra = rsrc_of(P0.A, a_bytes);
+  const auto rb = rsrc_of(P0.B, (unsigned)((long long)P0.N * P0.ldb * 2));
+  unsigned a_off[NA];  // dense: byte offset of (row, kc); conv: element offset of the image
+  int a_ih0[NA], a_iw0[NA];
+  bool a_ok[NA];
+  unsigned b_off[NB];
+  int c_ci = 0, c_kh = 0, c_kw = 0;  // conv k walk, advanced BKH per k-tile
+  int t_lo = 0, t_hi = 0;             // k range of the current tile
+  struct Stage {
+    u32x4_t ra[NA], rb[NB];
+  };
+  Stage s0, s1;
+
+  auto begin_tile = [&](const capmi_gemm_problem& P, int m0, int n0, int k_lo, int k_hi) {
     const int M = P.M, N = P.N;
-    const int cH = P.cH, cW = P.cW, cCin = P.cCin, cKW = P.cKW;
-    const unsigned a_bytes = AMODE == 2 ? (unsigned)((long long)P.cN * cH * cW * cCin * 2)
-                                        : (unsigned)((long long)M * P.lda * 2);
-    const auto ra = rsrc_of(P.A, a_bytes);
-    const auto rb = rsrc_of(P.B, (unsigned)((long long)N * P.ldb * 2));
-    // per-slot row state
-    unsigned a_off[NA];  // dense: byte offset of (row, kc); conv: element offset of the image
-    int a_ih0[NA], a_iw0[NA];
-    bool a_ok[NA];
+    t_lo = k_lo;
+    t_hi = k_hi;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int row = m0 + ((tid + i * 256) >> 3);
@@ -92,88 +103,110 @@ gemm_bf16_kernel(const GemmArgs args) {
         const int oh = rem / P.cWo, ow = rem - oh * P.cWo;
         a_ih0[i] = oh * P.cStride - P.cPad;
         a_iw0[i] = ow * P.cStride - P.cPad;
-        a_off[i] = (unsigned)(n * cH * cW);  // pixel index of the image's (0, 0)
+        a_off[i] = (unsigned)(n * P.cH * P.cW);  // pixel index of the image's (0, 0)
       }
     }
-    unsigned b_off[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int n = n0 + ((tid + i * 256) >> 3);
       b_off[i] = n < N ? (unsigned)(((long long)n * P.ldb + kc) * 2) : kOOB;
     }
-    int c_ci = 0, c_kh = 0, c_kw = 0;  // conv k walk, advanced BKH per k-tile
     if (AMODE == 2) {
-      const int kpos = k_lo / cCin;
-      c_ci = k_lo - kpos * cCin;
-      c_kh = kpos / cKW;
-      c_kw = kpos - c_kh * cKW;
+      const int kpos = k_lo / P.cCin;
+      c_ci = k_lo - kpos * P.cCin;
+      c_kh = kpos / P.cKW;
+      c_kw = kpos - c_kh * P.cKW;
     }
-
-    struct Stage {
-      u32x4_t ra[NA], rb[NB];
-    };
-    auto load_tile = [&](Stage& st, int kt) {
-      const int k = k_lo + kt * BKH;
-      const bool kok = k < k_hi;
-      if (AMODE == 0) {
+  };
+  auto load_tile = [&](Stage& st, int kt) {
+    const int k = t_lo + kt * BKH;
+    const bool kok = k < t_hi;
+    if (AMODE == 0) {
 #pragma unroll
-        for (int i = 0; i < NA; ++i)
-          st.ra[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, kok ? a_off[i] + (unsigned)k * 2 : kOOB, 0, 0);
-      } else {
+      for (int i = 0; i < NA; ++i)
+        st.ra[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, kok && !(BF16_SKIP & 4) ? a_off[i] + (unsigned)k * 2 : kOOB, 0, 0);
+    } else {
+      const int cH = P0.cH, cW = P0.cW, cCin = P0.cCin;
 #pragma unroll
-        for (int i = 0; i < NA; ++i) {
-          const int ih = a_ih0[i] + c_kh, iw = a_iw0[i] + c_kw;
-          const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
-          const unsigned off = ((a_off[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + kc)) * 2u;
-          st.ra[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? off : kOOB, 0, 0);
-        }
-        c_ci += BKH;
-        if (c_ci >= cCin) {
-          c_ci = 0;
-          if (++c_kw == cKW) {
-            c_kw = 0;
-            ++c_kh;
-          }
+      for (int i = 0; i < NA; ++i) {
+        const int ih = a_ih0[i] + c_kh, iw = a_iw0[i] + c_kw;
+        const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
+        const unsigned off = ((a_off[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + kc)) * 2u;
+        st.ra[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, ok && !(BF16_SKIP & 4) ? off : kOOB, 0, 0);
+      }
+      c_ci += BKH;
+      if (c_ci >= cCin) {
+        c_ci = 0;
+        if (++c_kw == P0.cKW) {
+          c_kw = 0;
+          ++c_kh;
         }
       }
+    }
 #pragma unroll
-      for (int i = 0; i < NB; ++i)
-        st.rb[i] = __builtin_amdgcn_raw_buffer_load_b128(rb, kok ? b_off[i] + (unsigned)k * 2 : kOOB, 0, 0);
-    };
-    auto store_tile = [&](const Stage& st, int buf) {
-#pragma unroll
-      for (int i = 0; i < NA; ++i) *reinterpret_cast<u32x4_t*>(&As[buf][((tid + i * 256) >> 3) * SBH + kc]) = st.ra[i];
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-        *reinterpret_cast<u32x4_t*>(&Bs[buf][((tid + i * 256) >> 3) * SBH + kc]) = st.rb[i];
-    };
-    auto compute = [&](int buf) {
-      const __bf16* Ah = &As[buf][(wm0 + lr) * SBH + 8 * lh];
-      const __bf16* Bh = &Bs[buf][(wn0 + lr) * SBH + 8 * lh];
-#pragma unroll
-      for (int g = 0; g < BKH / 16; ++g) {
-        bf16x8_t a[TM], b[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const bf16x8_t*>(Ah + 32 * i * SBH + 16 * g);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const bf16x8_t*>(Bh + 32 * j * SBH + 16 * g);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-      }
-    };
-    auto kstep = [&](Stage& ld, const Stage& sv, int kt) {
-      load_tile(ld, kt + 2);
-      compute(kt & 1);
-      store_tile(sv, (kt + 1) & 1);
-      __syncthreads();
-    };
-    Stage s0, s1;
+    for (int i = 0; i < NB; ++i)
+      st.rb[i] = __builtin_amdgcn_raw_buffer_load_b128(rb, kok && !(BF16_SKIP & 4) ? b_off[i] + (unsigned)k * 2 : kOOB, 0, 0);
+  };
+  // the first k-tiles of a tile into the register stages
+  auto prefetch = [&](const capmi_gemm_problem& P, int m0, int n0, int k_lo, int k_hi) {
+    begin_tile(P, m0, n0, k_lo, k_hi);
     load_tile(s0, 0);
+    if (ST == 2) load_tile(s1, 1);
+  };
+  auto store_tile = [&](const Stage& st, int buf) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) *reinterpret_cast<u32x4_t*>(&As[buf * BM * SBH + ((tid + i * 256) >> 3) * SBH + kc]) = st.ra[i];
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      *reinterpret_cast<u32x4_t*>(&Bs[buf * BN * SBH + ((tid + i * 256) >> 3) * SBH + kc]) = st.rb[i];
+  };
+  auto compute = [&](int buf) {
+    const __bf16* Ah = &As[buf * BM * SBH + (wm0 + lr) * SBH + 8 * lh];
+    const __bf16* Bh = &Bs[buf * BN * SBH + (wn0 + lr) * SBH + 8 * lh];
+#pragma unroll
+    for (int g = 0; g < BKH / 16; ++g) {
+      bf16x8_t a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const bf16x8_t*>(Ah + 32 * i * SBH + 16 * g);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const bf16x8_t*>(Bh + 32 * j * SBH + 16 * g);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          if (BF16_SKIP & 2)
+            acc[i][j][0] += (float)a[i][0] * (float)b[j][1];
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  auto kstep = [&](Stage& ld, const Stage& sv, int kt) {
+    load_tile(ld, kt + 2);
+    compute(kt & 1);
+    store_tile(sv, (kt + 1) & 1);
+    __syncthreads();
+  };
+  // the k-loop of the prefetched tile (LDS free on entry: the previous k-loop ended on a barrier)
+  auto mainloop = [&]() {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int nkt = (t_hi - t_lo) / BKH;
+    if (nkt <= 0) return;
+    if (ST == 1) {  // one LDS stage, one register stage ahead
+      for (int kt = 0; kt < nkt; ++kt) {
+        store_tile(s0, 0);
+        __syncthreads();
+        load_tile(s0, kt + 1);
+        compute(0);
+        __syncthreads();
+      }
+      return;
+    }
     store_tile(s0, 0);
-    load_tile(s1, 1);
     __syncthreads();
     // back edge only from the second k-step (see gemm_nt.hip: keeps the prefetch two deep)
     int kt = 0;
@@ -192,10 +225,13 @@ gemm_bf16_kernel(const GemmArgs args) {
     const long long ldc = P.ldc;
     float csum[TN], csq[TN];
     if (args.plain_epi == 1 && m0 + BM <= M) {
-      // store-only form for a whole tile (round 3; host: plain_epilogue): one 32-bit lane offset, the row
-      // term of each register as a uniform soffset, no bounds checks or 64-bit addresses
-      const auto rc = rsrc_of(C, (unsigned)((long long)M * ldc * 2));
-      const unsigned lbase = (unsigned)((m0 + wm0 + 4 * lh) * ldc + n0 + wn0 + lr) * 2u;
+      // store-only form for a whole tile (round 3; host: plain_epilogue), through LDS since round 5: the rounded
+      // tile is written row-major into LDS (row stride BN + 8 bf16: the two 4-row halves of a ds_write_b16 land on
+      // disjoint banks), then leaves as 16-B row chunks, 4 rows x 256 B per store instruction instead of 2 x 64 B
+      // per 2-B store (l3 c2 32.3 -> 30.3 us, l3 c3 19.9 -> 19.5)
+      constexpr int ES = BN + 8;
+      __bf16* E = lds_tile;
+      static_assert(BM * ES <= ST * (BM + BN) * SBH, "staging tile fits the LDS tile");
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         csum[j] = 0.f;
@@ -205,13 +241,24 @@ gemm_bf16_kernel(const GemmArgs args) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const unsigned short h = bf16_bits(acc[i][j][r]);
-            const int rr = 32 * i + (r & 3) + 8 * (r >> 2);
-            __builtin_amdgcn_raw_buffer_store_b16(h, rc, lbase + 64u * j, (int)(rr * ldc * 2), 0);
+            const int rr = wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            reinterpret_cast<unsigned short*>(E)[rr * ES + wn0 + 32 * j + lr] = h;
             const float v = bf16_val(h);
             csum[j] += v;
             csq[j] = fmaf(v, v, csq[j]);
           }
       }
+      __syncthreads();
+      const auto rc = rsrc_of(C, (unsigned)((long long)M * ldc * 2));
+      constexpr int CPR = BN / 8;  // 16-B chunks per row
+#pragma unroll
+      for (int q = 0; q < BM * CPR / 256; ++q) {
+        const int e = q * 256 + tid, row = e / CPR, ch = e % CPR;
+        const u32x4_t v = *reinterpret_cast<const u32x4_t*>(E + row * ES + ch * 8);
+        if (!(BF16_SKIP & 1))
+          __builtin_amdgcn_raw_buffer_store_b128(v, rc, (unsigned)(((long long)(m0 + row) * ldc + n0 + ch * 8) * 2), 0, 0);
+      }
+      __syncthreads();  // (the next k-loop's first LDS stores overwrite the staging tile)
     } else
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -264,7 +311,8 @@ gemm_bf16_kernel(const GemmArgs args) {
     const capmi_gemm_problem& P = args.p[0];
     const int tiles_n = args.tiles_n[0];
     const int tn = bid % tiles_n, tm = bid / tiles_n;
-    mainloop(P, tm * BM, tn * BN, 0, P.K);
+    prefetch(P, tm * BM, tn * BN, 0, P.K);
+    mainloop();
     epilogue(P, tm, tn);
     return;
   }
@@ -283,7 +331,8 @@ gemm_bf16_kernel(const GemmArgs args) {
     const long long tb = t * nkt;
     const int ks = (int)(max(u0, tb) - tb), ke = (int)(min(u1, tb + nkt) - tb);
     const int tm = (int)(t / tiles_n), tn = (int)(t % tiles_n);
-    mainloop(P, tm * BM, tn * BN, ks * BKH, ke * BKH);
+    prefetch(P, tm * BM, tn * BN, ks * BKH, ke * BKH);
+    mainloop();
     if (ke < nkt) {
       const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + (long long)blockIdx.x * PART, 0,
                                                         PART * 4, 0x00020000);
@@ -327,21 +376,30 @@ gemm_bf16_kernel(const GemmArgs args) {
   }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int ST>
 void launch_bf16(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
   const dim3 g(blocks), b(256);
   const bool sk = a.sk_workers > 0;
   if (amode == 2) {
     if (sk)
-      CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 2, true>), g, b, 0, s, a);
+      CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 2, true, ST>), g, b, 0, s, a);
     else
-      CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 2, false>), g, b, 0, s, a);
+      CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 2, false, ST>), g, b, 0, s, a);
   } else {
     if (sk)
-      CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 0, true>), g, b, 0, s, a);
+      CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 0, true, ST>), g, b, 0, s, a);
     else
-      CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 0, false>), g, b, 0, s, a);
+      CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 0, false, ST>), g, b, 0, s, a);
   }
+}
+
+template <int BM, int BN>
+void launch_bf16_st1(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
+  const dim3 g(blocks), b(256);
+  if (amode == 2)
+    CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 2, false, 1>), g, b, 0, s, a);
+  else
+    CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 0, false, 1>), g, b, 0, s, a);
 }
 
 // ---- elementwise: the bf16 activations around the convs ---------------------------------------
@@ -448,11 +506,14 @@ unsigned grid_for(long long n) { return (unsigned)std::min<long long>(std::max<l
 
 }  // namespace
 
-int gemm_bf16_launch(const GemmArgs& a, int amode, int bm, int bn, int blocks, hipStream_t s) {
-  if (bm == 128 && bn == 128)
-    launch_bf16<128, 128>(a, amode, blocks, s);
+int gemm_bf16_launch(const GemmArgs& a, int amode, int bm, int bn, int blocks, hipStream_t s, int stages) {
+  if (stages == 1) {  // (data-parallel 128x64 only)
+    if (bm != 128 || bn != 64 || a.sk_workers > 0) return CAPMI_EINVAL;
+    launch_bf16_st1<128, 64>(a, amode, blocks, s);
+  } else if (bm == 128 && bn == 128)
+    launch_bf16<128, 128, 2>(a, amode, blocks, s);
   else if (bm == 128 && bn == 64)
-    launch_bf16<128, 64>(a, amode, blocks, s);
+    launch_bf16<128, 64, 2>(a, amode, blocks, s);
   else
     return CAPMI_EINVAL;
   CAPMI_LAUNCH_CHECK();

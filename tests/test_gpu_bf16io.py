@@ -76,7 +76,10 @@ def test_bf16io_conv(N, H, Cin, Cout, k, s, tile):
     assert torch.equal(out.view(torch.int16), out2.view(torch.int16))
 
 
-@pytest.mark.parametrize("M,N,Kd,tile", [(12544, 256, 1024, 3), (1000, 512, 256, 3), (300, 64, 128, 3)])
+# K <= 256 under AUTO: the one-stage 128x64 form (round 5) -- the l3 c3 shape, a partial last row tile, N not a
+# multiple of 64 (general epilogue), layer1's K = 64
+@pytest.mark.parametrize("M,N,Kd,tile", [(12544, 256, 1024, 3), (1000, 512, 256, 3), (300, 64, 128, 3),
+                                         (12544, 1024, 256, 3), (500, 200, 192, 3), (2000, 256, 64, 3)])
 def test_bf16io_dense(M, N, Kd, tile):
     from capmi import kernels as K
     from capmi._lib import CAPMI_A_KMAJOR

@@ -135,7 +135,7 @@ def setup(a):
     keep = (x, w, y, stats, sc, sh, prob, ws, locals().get("w3"), locals().get("xp"), locals().get("dy"),
             locals().get("dw"), locals().get("xb"), locals().get("wb"), locals().get("yb"))
     f = lambda: (run(), keep)[0]  # noqa: E731
-    f.out = locals()["dw"] if a.x3w else y  # what the launch writes (ab_inproc compares builds on it)
+    f.out = locals()["dw"] if a.x3w else locals()["yb"] if a.bf16io else y  # what the launch writes (ab_inproc compares builds on it)
     return f, M, co, Kd
 
 
