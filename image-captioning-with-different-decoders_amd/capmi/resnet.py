@@ -414,13 +414,15 @@ class EncoderRunner:
         launch = lambda: K.gemm_bf16(prob, mode, self._ws["sk"], K.TILE_AUTO)  # noqa: E731
         if self.conv_hook is not None:
             # the launch capmi_gemm_sk_ex makes for CAPMI_GEMM_BF16_IO (gemm.hip: gemm_bf16_io)
-            bn_ = 64 if co <= 64 else 128
+            # (round 5: K <= 256 takes the one-stage 128x64 form, data-parallel)
+            st1 = Kd <= 256
+            bn_ = 64 if co <= 64 or st1 else 128
             tiles = -(-rows // 128) * -(-co // bn_)
             slots = 2 * torch.cuda.get_device_properties(x.device).multi_processor_count
             rounds = -(-tiles // slots)
-            sk = (os.environ.get("CAPMI_BF16_SK", "0") == "1" and os.environ.get("CAPMI_SK_OFF", "0") != "1"
+            sk = (not st1 and os.environ.get("CAPMI_BF16_SK", "0") == "1" and os.environ.get("CAPMI_SK_OFF", "0") != "1"
                   and Kd // 64 >= 4 and tiles / (rounds * slots) < 0.9)  # (gemm.hip gemm_bf16_io)
-            key = f"gemm_bf16_kernel<128, {bn_}, {mode}, {'true' if sk else 'false'}>"
+            key = f"gemm_bf16_kernel<128, {bn_}, {mode}, {'true' if sk else 'false'}, {1 if st1 else 2}>"
             self.conv_hook(tag, 2.0 * rows * co * Kd, launch, key)
         else:
             launch()
