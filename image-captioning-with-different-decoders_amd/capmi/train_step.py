@@ -38,31 +38,6 @@ from .decoder_core import PNAMES
 from .resnet import feature_hw, pool_dup
 
 
-def _cu_masked_pair(dev, spec):
-    """CAPMI_PIPE_CUMASK = "<n>[:s]" (A/B): the decoder stream on n CUs, the encoder stream on the others, as two
-    CU-masked HIP streams (hipExtStreamCreateWithCUMask); s = strided (every (CUs / n)-th CU, spread over the
-    XCDs) instead of the top n. The encoder's stream-K grids must then be sized for its CUs (CAPMI_SK_CUS)."""
-    import ctypes
-    n, _, mode = spec.partition(":")
-    n = int(n)
-    cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    dec = set(range(0, cus, cus // n)) if mode == "s" else set(range(cus - n, cus))
-    hip = ctypes.CDLL("libamdhip64.so")
-
-    def make(bits):
-        words = [0] * ((cus + 31) // 32)
-        for b in bits:
-            words[b // 32] |= 1 << (b % 32)
-        arr = (ctypes.c_uint32 * len(words))(*words)
-        h = ctypes.c_void_p()
-        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(words)), arr)
-        if rc != 0:
-            raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
-        return torch.cuda.ExternalStream(h.value, device=dev)
-
-    return make(set(range(cus)) - dec), make(dec)
-
-
 class AttentionTrainStep:
     def __init__(self, encoder, decoder, optimizer, ctx=None, alpha_c=1.0, overlap=True, graph=False,
                  seed=None, pipeline=False, encoder_optimizer=None):
@@ -112,12 +87,8 @@ class AttentionTrainStep:
             self._pg_key = None
             lo, hi = torch.cuda.Stream.priority_range()
             pe, pd = {"swap": (hi, lo), "equal": (lo, lo)}.get(os.environ.get("CAPMI_PIPE_PRIO", ""), (lo, hi))
-            cum = os.environ.get("CAPMI_PIPE_CUMASK", "")
-            if cum:
-                self.s_enc, self.s_dec = _cu_masked_pair(dev, cum)
-            else:
-                self.s_enc = torch.cuda.Stream(device=dev, priority=pe)
-                self.s_dec = torch.cuda.Stream(device=dev, priority=pd)
+            self.s_enc = torch.cuda.Stream(device=dev, priority=pe)
+            self.s_dec = torch.cuda.Stream(device=dev, priority=pd)
             self._feats = [None, None]
             self._slot = 0
             self._pend = None
