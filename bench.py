@@ -159,10 +159,10 @@ def _traffic_file(config):
     """The committed PMC summary of ``config``'s own run (a kernel name can stand for different
     shapes in different configs, so each config reads only its own passes); the newest round's."""
     name = "pmc_traffic.json" if config == "attention" else f"pmc_traffic_{config}.json"
-    for rnd in ("r04", "r03", "r02", "r01"):
-        if os.path.exists(os.path.join(REPO, "profiles", f"{rnd}_{name}")):
-            return f"{rnd}_{name}"
-    return f"r04_{name}"
+    rounds = sorted((f.split("_", 1)[0] for f in os.listdir(os.path.join(REPO, "profiles"))
+                     if f.endswith("_" + name) and f[0] == "r" and f.split("_", 1)[0][1:].isdigit()),
+                    key=lambda r: int(r[1:]), reverse=True)
+    return f"{rounds[0]}_{name}" if rounds else f"r01_{name}"
 
 
 def _traffic(kernel, config="attention"):

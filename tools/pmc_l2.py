@@ -1,0 +1,37 @@
+"""L2 hit rate and memory-side reads per conv GEMM launch from the tools/r05_probe25.sh passes
+(gpurun_out/l2/<case>/.../*.db: TCC_HIT_sum, TCC_MISS_sum, TCC_EA0_RDREQ_sum). Memory-side read bytes =
+TCC_EA0_RDREQ x 64 B x 2 (MI355X_MICROARCH.md: on gfx950 each 128-B request of a wide read is tallied at 64 B)."""
+import glob
+import os
+import sqlite3
+import sys
+from collections import defaultdict
+
+
+def main(root="gpurun_out/l2"):
+    print(f"{'case':18s} {'kernel':48s} {'us':>6s} {'L2 hit':>7s} {'L2 req':>9s} {'mem-side read MB':>17s}")
+    for case in sorted(os.listdir(root)):
+        per = defaultdict(lambda: defaultdict(float))
+        ids = defaultdict(set)
+        dur = defaultdict(float)
+        for db in glob.glob(f"{root}/{case}/**/*.db", recursive=True):
+            c = sqlite3.connect(db)
+            for did, name, cn, v, d in c.execute(
+                    "select dispatch_id, kernel_name, counter_name, value, duration from counters_collection"):
+                if "gemm" not in name:
+                    continue
+                k = name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+                per[k][cn] += v
+                if did not in ids[k]:
+                    ids[k].add(did)
+                    dur[k] += d
+        for k, p in per.items():
+            n = len(ids[k])
+            hit, miss = p.get("TCC_HIT_sum", 0) / n, p.get("TCC_MISS_sum", 0) / n
+            rd = p.get("TCC_EA0_RDREQ_sum", 0) / n * 128 / 1e6
+            print(f"{case:18s} {k[:48]:48s} {dur[k] / n / 1e3:6.1f} {100 * hit / max(hit + miss, 1):6.1f}% "
+                  f"{hit + miss:9.3g} {rd:17.1f}")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
