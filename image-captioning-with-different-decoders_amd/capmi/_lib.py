@@ -23,7 +23,7 @@ CAPMI_B_NMAJOR_W, CAPMI_B_KROWS, CAPMI_B_CONV_NHWC = 0, 1, 2
 CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO, CAPMI_TILE_128_W8 = 0, 1, 2, 3, 4
 CAPMI_MAX_GROUP = 4
 CAPMI_COLSUM_GROUPS = 64
-ABI_VERSION = 23
+ABI_VERSION = 24
 CAPMI_BNB_RELU_Y, CAPMI_BNB_RELU_OUT = 0, 1
 CAPMI_BNB_MAX_SLABS = 256
 CAPMI_GEMM_BF16 = 1
@@ -51,6 +51,12 @@ class GemmProblem(ctypes.Structure):
         ("cKW", c_int), ("cStride", c_int), ("cPad", c_int), ("cHo", c_int), ("cWo", c_int),
         ("in_scale", c_vp), ("in_shift", c_vp),
     ]
+
+
+class Wx3Job(ctypes.Structure):
+    """Mirror of ``capmi_wx3_job`` (include/capmi.h)."""
+    _fields_ = [("w", c_vp), ("out", c_vp), ("mode", c_int), ("cout", c_int), ("cin", c_int), ("kh", c_int),
+                ("kw", c_int), ("ph", c_int), ("pw", c_int), ("pad_", c_int)]
 
 
 class DstepSeg(ctypes.Structure):
@@ -95,6 +101,7 @@ _SIGS = {
     "capmi_conv_weight_pack_dgrad": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_conv_weight_pack_dgrad_s2": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_conv_weight_pack_dgrad_x3": [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp],
+    "capmi_weight_x3_batch": [c_vp, c_int, c_vp],
     "capmi_conv_weight_unpack": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_zero_upsample2_nhwc": [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_bn_bwd_reduce": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_ll, c_int,

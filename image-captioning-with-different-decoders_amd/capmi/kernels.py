@@ -452,6 +452,33 @@ def conv_weight_pack_dgrad_s2(w, ph, pw, out):
     call("capmi_conv_weight_pack_dgrad_s2", ptr(w), co, ci, int(ph), int(pw), ptr(out), stream())
 
 
+WX3_FWD, WX3_FWD_X3P, WX3_DGRAD, WX3_DGRAD_T = 0, 1, 2, 3
+
+
+def wx3_jobs(specs, device):
+    """Device array of capmi_wx3_job descriptors from (w, out, mode, ph, pw) tuples (w: the nn.Conv2d weight,
+    out: its [3][R][Kc] bf16 planes); the tensors must outlive every launch of the array."""
+    from ._lib import Wx3Job
+    arr = (Wx3Job * len(specs))()
+    for i, (w, out, mode, ph, pw) in enumerate(specs):
+        co, ci, kh, kw = w.shape
+        assert w.is_contiguous() and w.dtype == torch.float32 and out.dtype == torch.bfloat16
+        T = (ph + 1) * (pw + 1) if mode == WX3_DGRAD and ph >= 0 else kh * kw
+        assert out.numel() >= 3 * co * ci * T
+        assert mode != WX3_DGRAD_T or kh * kw == 1
+        assert mode != WX3_FWD_X3P or ci % 32 == 0
+        assert mode != WX3_DGRAD or (co % 32 == 0 and (ph < 0 or (kh == 3 and kw == 3)))
+        arr[i] = Wx3Job(w.data_ptr(), out.data_ptr(), mode, co, ci, kh, kw, ph, pw, 0)
+    raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+    return raw.to(device)
+
+
+def weight_x3_batch(jobs, njobs):
+    """capmi_weight_x3_batch: the three-plane splits of every job in ``jobs`` (wx3_jobs) in one launch."""
+    _cuda(jobs, dtype=torch.uint8)
+    call("capmi_weight_x3_batch", ptr(jobs), int(njobs), stream())
+
+
 def conv_weight_pack_dgrad_x3(w, out, ph=-1, pw=-1):
     """The dgrad weight pack (ph < 0: conv_weight_pack_dgrad; else the sub-pixel class (ph, pw) of
     conv_weight_pack_dgrad_s2) in the x3p conv k order, split into out bf16 [3][Cin][T * Cout]

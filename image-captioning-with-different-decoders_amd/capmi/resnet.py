@@ -605,6 +605,10 @@ _FT_DGRAD1_X3 = os.environ.get("CAPMI_FT_DGRAD1_X3", "1") != "0"
 # x3 mode: the weight gradients on the x3w kernel (round 4: both fp32 operands split in-kernel, transposed
 # LDS reads, k-split slabs; CAPMI_FT_WGRAD_X3W=0: the split-staging nts kernel)
 _FT_WGRAD_X3W = os.environ.get("CAPMI_FT_WGRAD_X3W", "1") != "0"
+# round 5: every trainable conv's three-plane weights (forward B planes, data-gradient planes) refreshed by ONE
+# capmi_weight_x3_batch launch per step, from the second step on (the first records what the step uses);
+# CAPMI_FT_WPREP_BATCH=0: the per-conv packs and splits (A/B)
+_FT_WPREP_BATCH = os.environ.get("CAPMI_FT_WPREP_BATCH", "1") != "0"
 
 
 class FineTuneRunner:
@@ -626,6 +630,11 @@ class FineTuneRunner:
         self.saved = _Pool()
         self.grad = _Pool()
         self.state = None
+        # batched weight preparation (_FT_WPREP_BATCH): per (weight, ph, pw) the data-gradient planes, the job
+        # specs recorded on the first step, their device array once built
+        self._dgrad_x3 = {}
+        self._wx3_specs = []
+        self._wx3 = None
 
     # ------------------------------------------------------------------ forward
     def _bn_save(self, ws, bn, rows):
@@ -647,9 +656,12 @@ class FineTuneRunner:
         N, _, H, W = imgs.shape
         dev = imgs.device
         ws = r._workspace(N, H, W, dev)
-        # the optimizer updates trainable weights in place (same storage, same _version):
-        # drop their packed copies so this forward re-packs them
-        for li in range(self.first, 5):
+        # the optimizer updates trainable weights in place (same storage, same _version): refresh every
+        # trainable conv's planes in one launch (the cache entries keep their buffers), or drop the packed copies
+        # so this forward re-packs them
+        if self._wx3 is not None:
+            K.weight_x3_batch(self._wx3, len(self._wx3_specs))
+        for li in range(self.first, 5) if self._wx3 is None else ():
             for blk in getattr(net, f"layer{li}"):
                 r.packed.cache.pop(id(blk.conv2), None)
                 convs = [blk.conv1, blk.conv2, blk.conv3] + ([blk.downsample[0]] if blk.downsample is not None else [])
@@ -790,32 +802,52 @@ class FineTuneRunner:
             word = gp("w_dgrad_ord", max(wmax, w1max), dev)
             w3 = gp("w_dgrad_x3", 3 * max(wmax, w1max), dev, dtype=torch.bfloat16)
 
-        def run_dgrad(tag, flops, prob, w, kh=1, kw=1, cin=None, conv_w=None, ph=-1, pw=-1):
+        def run_dgrad(tag, flops, prob, w, kh=1, kw=1, cin=None, conv_w=None, ph=-1, pw=-1, w1=None):
             """Data gradient with B = the packed dgrad weight w ([N][K]); A = dY (3x3 / sub-pixel:
             through the implicit im2col, kh x kw taps of cin channels). x3 mode: x3d on w re-ordered
             to the x3p k order and split (CAPMI_FT_DGRAD_X3D / CAPMI_FT_DGRAD1_X3D for the 1x1s); for
-            a 3x3 conv_w (the nn.Conv2d weight) is packed, ordered and split in one pass instead."""
+            a 3x3 conv_w (the nn.Conv2d weight) is packed, ordered and split in one pass instead. w1: a 1x1
+            conv's weight, packed transposed into w here. With the batched weight preparation the split planes
+            of conv_w / w1 are the ones the forward's capmi_weight_x3_batch launch refreshed (the first step
+            computes them per conv into their own buffer and records the job)."""
             n, kd = prob.N, prob.K
             conv = kh * kw > 1 or cin is not None
             amode = AC if conv else AK
             use = (x3d if conv else x3d1) and kd % 32 == 0 and (not conv or cin % 32 == 0)
-            if conv_w is not None and not (use and _FT_PACK_X3):  # the fp32 pack
-                if ph < 0:
-                    K.conv_weight_pack_dgrad(conv_w, w[:n * kd])
-                else:
-                    K.conv_weight_pack_dgrad_s2(conv_w, ph, pw, w[:n * kd])
-                conv_w = None
-            if not use:
-                return run(tag, flops, prob, amode, BW)
-            if conv_w is not None:
-                K.conv_weight_pack_dgrad_x3(conv_w, w3[:3 * n * kd], ph, pw)
+            batch = _FT_WPREP_BATCH and use and ((conv_w is not None and _FT_PACK_X3) or w1 is not None)
+            key = ((conv_w if conv_w is not None else w1).data_ptr(), ph, pw) if batch else None
+            planes = self._dgrad_x3.get(key) if batch else None
+            if planes is not None and self._wx3 is not None:
+                prob.B = planes.data_ptr()  # refreshed this step by the forward's batched launch
+                conv_w = w1 = None
             else:
-                src = w[:n * kd].view(n, kd)
-                if kh * kw > 1:
-                    word[:n * kd].view(n, kd).copy_(K.conv_weight_order_x3p(src, kh, kw, cin))
-                    src = word[:n * kd]
-                K.split3_bf16(src, w3[:3 * n * kd])
-            prob.B = w3.data_ptr()
+                if w1 is not None:
+                    K.conv_weight_pack_dgrad(w1, w[:n * kd])
+                if conv_w is not None and not (use and _FT_PACK_X3):  # the fp32 pack
+                    if ph < 0:
+                        K.conv_weight_pack_dgrad(conv_w, w[:n * kd])
+                    else:
+                        K.conv_weight_pack_dgrad_s2(conv_w, ph, pw, w[:n * kd])
+                    conv_w = None
+                if not use:
+                    return run(tag, flops, prob, amode, BW)
+                dst = w3
+                if batch:  # first step: this conv's own planes, recorded as a job of the batched launch
+                    dst = self._dgrad_x3.get(key)
+                    if dst is None:
+                        dst = torch.empty(3 * n * kd, device=dev, dtype=torch.bfloat16)
+                        self._dgrad_x3[key] = dst
+                        src = conv_w if conv_w is not None else w1
+                        self._wx3_specs.append((src, dst, K.WX3_DGRAD if conv_w is not None else K.WX3_DGRAD_T, ph, pw))
+                if conv_w is not None:
+                    K.conv_weight_pack_dgrad_x3(conv_w, dst[:3 * n * kd], ph, pw)
+                else:
+                    src = w[:n * kd].view(n, kd)
+                    if kh * kw > 1:
+                        word[:n * kd].view(n, kd).copy_(K.conv_weight_order_x3p(src, kh, kw, cin))
+                        src = word[:n * kd]
+                    K.split3_bf16(src, dst[:3 * n * kd])
+                prob.B = dst.data_ptr()
             if not conv and _FT_DGRAD1_X3 and kd >= 4 * n and prob.c_r1 <= 0:
                 # long-k 1x1 data gradients (conv3's: K = 4 N) on gemm_x3 (the same split planes; 1x1: plain k
                 # order), as the forward's long-k plain c1 convs (DESIGN 4.8)
@@ -866,9 +898,8 @@ class FineTuneRunner:
                 run(tag + ".conv3.dgrad", 2.0 * r3 * Cout * wd,
                     K.problem(r3, wd, Cout, dy3, Cout, c3.weight.detach(), wd, da2, wd), AK, BKR)
             else:
-                K.conv_weight_pack_dgrad(c3.weight.detach(), wt[:Cout * wd])
                 run_dgrad(tag + ".conv3.dgrad", 2.0 * r3 * Cout * wd,
-                          K.problem(r3, wd, Cout, dy3, Cout, wt, Cout, da2, wd), wt)
+                          K.problem(r3, wd, Cout, dy3, Cout, wt, Cout, da2, wd), wt, w1=c3.weight.detach())
             # ---- bn2 + relu
             bn2 = blk.bn2
             K.bn_bwd_reduce(K.BNB_RELU_Y, da2, b["y2"], None, s2, b2, bn2.weight, m2[0], m2[1], bn2.eps, r3, wd,
@@ -918,9 +949,9 @@ class FineTuneRunner:
                         K.problem(r1, Cin, wd, da1, wd, c1.weight.detach(), Cin, dx, Cin,
                                   beta=1.0 if ds is None else 0.0), AK, BKR)
                 else:
-                    K.conv_weight_pack_dgrad(c1.weight.detach(), wt[:wd * Cin])
                     run_dgrad(tag + ".conv1.dgrad", 2.0 * r1 * wd * Cin,
-                              K.problem(r1, Cin, wd, da1, wd, wt, wd, dx, Cin, beta=1.0 if ds is None else 0.0), wt)
+                              K.problem(r1, Cin, wd, da1, wd, wt, wd, dx, Cin, beta=1.0 if ds is None else 0.0), wt,
+                              w1=c1.weight.detach())
             # ---- downsample (1x1, stride s) on x
             if ds is not None:
                 cd = ds[0]
@@ -936,11 +967,30 @@ class FineTuneRunner:
                             K.problem(r3, Cin, Cout, dyd, Cout, cd.weight.detach(), Cin, dx, s * Cin, beta=1.0, **rm),
                             AK, BKR)
                     else:
-                        K.conv_weight_pack_dgrad(cd.weight.detach(), wt[:Cout * Cin])
                         run_dgrad(tag + ".downsample.dgrad", 2.0 * r3 * Cout * Cin,
-                                  K.problem(r3, Cin, Cout, dyd, Cout, wt, Cout, dx, s * Cin, beta=1.0, **rm), wt)
+                                  K.problem(r3, Cin, Cout, dyd, Cout, wt, Cout, dx, s * Cin, beta=1.0, **rm), wt,
+                                  w1=cd.weight.detach())
             cur ^= 1
         self.state = None
+        if _FT_WPREP_BATCH and self._wx3 is None and self.r.x3:
+            self._build_wx3(stt)
+
+    def _build_wx3(self, stt):
+        """After the first step: the batched weight preparation's job array -- the forward's three-plane
+        weights of every trainable conv (the cache entries this step created, refreshed in place from now on)
+        and the data-gradient planes run_dgrad recorded."""
+        specs = list(self._wx3_specs)
+        for b in stt["blocks"]:
+            blk = b["blk"]
+            convs = [blk.conv1, blk.conv2, blk.conv3] + ([blk.downsample[0]] if blk.downsample is not None else [])
+            for c in convs:
+                for tag, mode in (("x3", K.WX3_FWD), ("x3p", K.WX3_FWD_X3P)):
+                    ent = self.r.packed.cache.get((tag, id(c)))
+                    if ent is not None:
+                        specs.append((c.weight.detach(), ent[2], mode, -1, -1))
+        if specs:
+            self._wx3_specs = specs
+            self._wx3 = K.wx3_jobs(specs, stt["device"])
 
 
 def trainable_encoder_params(net, first_layer=2):

@@ -123,6 +123,76 @@ extern "C" int capmi_conv_weight_pack_dgrad_x3(const float* w, int Cout, int Cin
   return 0;
 }
 
+// Round 5: every trainable conv's three-plane weight operands of a fine-tune step in ONE launch (the forward's
+// B planes in the plain [Cout][KH][KW][Cin] or the x3p k order, the data gradients' transposed / flipped planes),
+// instead of 2-3 latency-bound launches per conv (split3_bf16 + packs: ~250 launches per step). Block row y =
+// job y (read once, uniform); the element map of each mode restates the per-conv kernels above exactly, and the
+// split is split3_bf16's (RNE at each step), so the planes are bit-identical to the per-conv path.
+__device__ __forceinline__ void wx3_store(__bf16* out, long long n, long long e, float x) {
+  const __bf16 h0 = (__bf16)x;
+  const float r1 = x - (float)h0;
+  const __bf16 h1 = (__bf16)r1;
+  out[e] = h0;
+  out[n + e] = h1;
+  out[2 * n + e] = (__bf16)(r1 - (float)h1);
+}
+
+__global__ void __launch_bounds__(256) weight_x3_batch_kernel(const capmi_wx3_job* __restrict__ jobs) {
+  const capmi_wx3_job j = jobs[blockIdx.y];
+  const int KH = j.kh, KW = j.kw;
+  const int T = j.mode == CAPMI_WX3_DGRAD && j.ph >= 0 ? (j.ph + 1) * (j.pw + 1) : KH * KW;
+  const int TW = j.mode == CAPMI_WX3_DGRAD && j.ph >= 0 ? j.pw + 1 : KW;
+  const bool dg = j.mode == CAPMI_WX3_DGRAD || j.mode == CAPMI_WX3_DGRAD_T;
+  const long long R = dg ? j.cin : j.cout;                   // rows of the B operand
+  const long long Kc = (long long)T * (dg ? j.cout : j.cin);  // its k extent
+  const long long n = R * Kc;
+  const float* __restrict__ w = j.w;
+  __bf16* __restrict__ out = static_cast<__bf16*>(j.out);
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    const long long r = e / Kc;
+    const int k = (int)(e - r * Kc);
+    int co, ci, kh, kw;
+    if (j.mode == CAPMI_WX3_FWD) {  // [Cout][KH][KW][Cin] (capmi_conv_weight_pack_pad, Cin >= 4)
+      co = (int)r;
+      const int tap = k / j.cin;
+      ci = k - tap * j.cin;
+      kh = tap / KW;
+      kw = tap - kh * KW;
+    } else if (j.mode == CAPMI_WX3_FWD_X3P) {  // (ci / 32, kh, kw, ci % 32): conv_weight_order_x3p
+      co = (int)r;
+      const int slice = k / (T * 32), rem = k - slice * T * 32, tap = rem >> 5;
+      ci = slice * 32 + (rem & 31);
+      kh = tap / KW;
+      kw = tap - kh * KW;
+    } else if (j.mode == CAPMI_WX3_DGRAD) {  // conv_weight_pack_dgrad_x3_kernel's map
+      ci = (int)r;
+      const int slice = k / (T * 32), rem = k - slice * T * 32, tap = rem >> 5;
+      co = slice * 32 + (rem & 31);
+      const int th = tap / TW, tw = tap - th * TW;
+      if (j.ph < 0) {
+        kh = KH - 1 - th;
+        kw = KW - 1 - tw;
+      } else {
+        kh = j.ph ? 2 - 2 * th : 1;
+        kw = j.pw ? 2 - 2 * tw : 1;
+      }
+    } else {  // CAPMI_WX3_DGRAD_T: 1x1, out[ci][co] = w[co][ci] (capmi_conv_weight_pack_dgrad at 1x1)
+      ci = (int)r;
+      co = k;
+      kh = kw = 0;
+    }
+    wx3_store(out, n, e, w[(((long long)co * j.cin + ci) * KH + kh) * KW + kw]);
+  }
+}
+
+extern "C" int capmi_weight_x3_batch(const capmi_wx3_job* jobs, int njobs, void* stream) {
+  CAPMI_REQUIRE(njobs >= 0 && njobs <= 65535 && (njobs == 0 || jobs), CAPMI_EINVAL);
+  if (njobs == 0) return 0;
+  hipLaunchKernelGGL(weight_x3_batch_kernel, dim3(64, njobs), dim3(256), 0, as_stream(stream), jobs);
+  CAPMI_LAUNCH_CHECK();
+  return 0;
+}
+
 // out[co][ci][kh][kw] (= nn.Conv2d weight layout) from the GEMM layout g[co][kh][kw][ci]
 __global__ void conv_weight_unpack_kernel(const float* __restrict__ g, int Cout, int Cin, int KH, int KW,
                                           float* __restrict__ out) {

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 23
+#define CAPMI_ABI_VERSION 24
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -282,6 +282,27 @@ int capmi_conv_weight_pack_dgrad_s2(const float* w, int Cout, int Cin, int ph, i
  * (KH = KW = 3). Cout % 32 == 0. */
 int capmi_conv_weight_pack_dgrad_x3(const float* w, int Cout, int Cin, int KH, int KW, int ph, int pw, void* out,
                                     void* stream);
+/* Many conv weights' three-plane bf16 operands in one launch (ABI 24, the fine-tune step's weight
+ * preparation). jobs: DEVICE array of njobs descriptors (read by the kernel, so it may be built once and
+ * re-launched every step, e.g. from a captured graph); w = the nn.Conv2d weight [Cout][Cin][KH][KW] fp32, out =
+ * three planes [3][R][Kc] bf16, the exact RNE split of capmi_split3_bf16, bit-identical to:
+ *   CAPMI_WX3_FWD      R = Cout, Kc = KH*KW*Cin: split3 of capmi_conv_weight_pack_pad (Cin >= 4, unpadded)
+ *   CAPMI_WX3_FWD_X3P  the same in the x3p conv k order (ci/32, kh, kw, ci%32); Cin % 32 == 0
+ *   CAPMI_WX3_DGRAD    capmi_conv_weight_pack_dgrad_x3 with (ph, pw) (ph < 0: the flipped KHxKW kernel)
+ *   CAPMI_WX3_DGRAD_T  KH = KW = 1: split3 of capmi_conv_weight_pack_dgrad (out[ci][co] = w[co][ci]) */
+#define CAPMI_WX3_FWD 0
+#define CAPMI_WX3_FWD_X3P 1
+#define CAPMI_WX3_DGRAD 2
+#define CAPMI_WX3_DGRAD_T 3
+typedef struct {
+  const float* w;
+  void* out;
+  int mode;
+  int cout, cin, kh, kw;
+  int ph, pw;
+  int pad_;
+} capmi_wx3_job;
+int capmi_weight_x3_batch(const capmi_wx3_job* jobs, int njobs, void* stream);
 /* [Cout][KH][KW][Cin] (GEMM layout of a weight gradient) -> [Cout][Cin][KH][KW] (nn.Conv2d layout) */
 int capmi_conv_weight_unpack(const float* packed, int Cout, int Cin, int KH, int KW, float* out, void* stream);
 /* out (N,H,W,C) = dy (N,Ho,Wo,C) at even (h, w), zero elsewhere (stride-2 conv data gradient) */
