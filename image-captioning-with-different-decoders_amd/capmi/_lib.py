@@ -35,7 +35,6 @@ CAPMI_GEMM_X3D = 32
 CAPMI_GEMM_X3S = 64
 CAPMI_GEMM_X3W = 128
 CAPMI_GEMM_X3C = 256
-CAPMI_GEMM_X3W_DEFER = 512
 
 
 class GemmProblem(ctypes.Structure):
@@ -58,12 +57,6 @@ class Wx3Job(ctypes.Structure):
     """Mirror of ``capmi_wx3_job`` (include/capmi.h)."""
     _fields_ = [("w", c_vp), ("out", c_vp), ("mode", c_int), ("cout", c_int), ("cin", c_int), ("kh", c_int),
                 ("kw", c_int), ("ph", c_int), ("pw", c_int), ("pad_", c_int)]
-
-
-class SkrJob(ctypes.Structure):
-    """Mirror of ``capmi_skr_job`` (include/capmi.h)."""
-    _fields_ = [("in_", c_vp), ("out", c_vp), ("slab", c_ll), ("ld_in", c_ll), ("ld_out", c_ll), ("S", c_int),
-                ("rows", c_int), ("cols", c_int), ("kh", c_int), ("kw", c_int), ("cin", c_int)]
 
 
 class DstepSeg(ctypes.Structure):
@@ -109,7 +102,6 @@ _SIGS = {
     "capmi_conv_weight_pack_dgrad_s2": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_conv_weight_pack_dgrad_x3": [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_weight_x3_batch": [c_vp, c_int, c_vp],
-    "capmi_splitk_reduce_batch": [c_vp, c_int, c_vp],
     "capmi_conv_weight_unpack": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_zero_upsample2_nhwc": [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_bn_bwd_reduce": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_ll, c_int,

@@ -9,7 +9,7 @@ import weakref
 import torch
 
 from ._lib import DstepEpi, DstepSeg
-from ._lib import (CAPMI_A_CONV_NHWC, CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_GEMM_BF16_IO, CAPMI_GEMM_X3, CAPMI_GEMM_X3P, CAPMI_GEMM_X3W_DEFER,
+from ._lib import (CAPMI_A_CONV_NHWC, CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_GEMM_BF16_IO, CAPMI_GEMM_X3, CAPMI_GEMM_X3P,
                    CAPMI_GEMM_SPLIT3, CAPMI_GEMM_X3C, CAPMI_GEMM_X3D, CAPMI_GEMM_X3S, CAPMI_GEMM_X3W,
                    CAPMI_COLSUM_GROUPS, CAPMI_TILE_128, CAPMI_TILE_64,
                    CAPMI_TILE_128x64, CAPMI_TILE_AUTO, GemmProblem, call, lib)
@@ -219,44 +219,13 @@ def gemm_x3c_kernel_name(prob):
     return f"gemm_x3c_kernel<{'true' if prob.in_scale else 'false'}>"
 
 
-def gemm_x3w(prob, bmode, workspace, defer=False):
+def gemm_x3w(prob, bmode, workspace):
     """CAPMI_GEMM_X3W: the conv weight gradient dW = dY^T . B (A = dY fp32 k rows, CAPMI_A_MMAJOR; B fp32 k
     rows, CAPMI_B_KROWS, or the NHWC conv input's im2col, CAPMI_B_CONV_NHWC, with the optional BN prologue);
-    k-split partial slabs in the stream-K workspace. defer (CAPMI_GEMM_X3W_DEFER): the slabs stay there for
-    the caller to sum (x3w_slabs, splitk_reduce_batch)."""
+    k-split partial slabs in the stream-K workspace."""
     _cuda(workspace, dtype=torch.int32)
-    call("capmi_gemm_sk_ex", ctypes.byref(prob), CAPMI_A_MMAJOR, bmode, CAPMI_TILE_AUTO,
-         CAPMI_GEMM_X3W_DEFER if defer else CAPMI_GEMM_X3W, ptr(workspace), workspace.numel() * 4, stream())
-
-
-def x3w_slabs(prob, bmode):
-    """(S, slab floats, ld) of a CAPMI_GEMM_X3W_DEFER launch: S k-split slabs of M x ld floats after the
-    workspace's flag bytes (S == 1: the launch writes C itself)."""
-    S = gemm_sk_plan(prob, CAPMI_A_MMAJOR, CAPMI_TILE_AUTO, bmode, flags=CAPMI_GEMM_X3W)[3]
-    ld = -(-prob.N // 128) * 128
-    return S, prob.M * ld, ld
-
-
-def skr_jobs(specs, device):
-    """Device array of capmi_skr_job descriptors from (in, S, slab, ld_in, out, rows, cols, ld_out, unpack)
-    tuples; unpack = (KH, KW, Cin) writes the nn.Conv2d layout (or None)."""
-    from ._lib import SkrJob
-    arr = (SkrJob * len(specs))()
-    for i, (src, S, slab, ld_in, out, rows, cols, ld_out, unpack) in enumerate(specs):
-        kh, kw, cin = unpack if unpack is not None else (1, 1, 0)
-        assert src.numel() * src.element_size() >= 4 * ((S - 1) * slab + (rows - 1) * ld_in + cols)
-        if not isinstance(out, int):  # (an int: a raw fp32 pointer the caller vouches for, e.g. a problem's C)
-            assert out.numel() >= rows * cols and out.dtype == torch.float32 and out.is_contiguous()
-            out = out.data_ptr()
-        assert unpack is None or kh * kw * cin == cols
-        arr[i] = SkrJob(src.data_ptr(), out, slab, ld_in, ld_out, S, rows, cols, kh, kw, cin)
-    return torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(device)
-
-
-def splitk_reduce_batch(jobs, njobs):
-    """capmi_splitk_reduce_batch: every job's slab sum (skr_jobs) in one launch."""
-    _cuda(jobs, dtype=torch.uint8)
-    call("capmi_splitk_reduce_batch", ptr(jobs), int(njobs), stream())
+    call("capmi_gemm_sk_ex", ctypes.byref(prob), CAPMI_A_MMAJOR, bmode, CAPMI_TILE_AUTO, CAPMI_GEMM_X3W,
+         ptr(workspace), workspace.numel() * 4, stream())
 
 
 def gemm_x3w_kernel_name(prob, bmode):

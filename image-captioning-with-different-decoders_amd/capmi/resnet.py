@@ -609,10 +609,6 @@ _FT_WGRAD_X3W = os.environ.get("CAPMI_FT_WGRAD_X3W", "1") != "0"
 # capmi_weight_x3_batch launch per step, from the second step on (the first records what the step uses);
 # CAPMI_FT_WPREP_BATCH=0: the per-conv packs and splits (A/B)
 _FT_WPREP_BATCH = os.environ.get("CAPMI_FT_WPREP_BATCH", "1") != "0"
-# round 5: the x3w weight gradients leave their k-split slabs in per-conv buffers (CAPMI_GEMM_X3W_DEFER) and one
-# capmi_splitk_reduce_batch launch at the end of the backward sums them all, straight into the nn.Conv2d layout
-# (instead of one reduce per gradient plus an unpack per 3x3); CAPMI_FT_WGRAD_DEFER=0: per gradient (A/B)
-_FT_WGRAD_DEFER = os.environ.get("CAPMI_FT_WGRAD_DEFER", "1") != "0"
 
 
 class FineTuneRunner:
@@ -639,11 +635,6 @@ class FineTuneRunner:
         self._dgrad_x3 = {}
         self._wx3_specs = []
         self._wx3 = None
-        # deferred weight-gradient sums (_FT_WGRAD_DEFER): per-gradient slab buffers, the job list of the last
-        # backward and its device array
-        self._wg_ws = {}
-        self._skr_key = None
-        self._skr = None
 
     # ------------------------------------------------------------------ forward
     def _bn_save(self, ws, bn, rows):
@@ -791,32 +782,14 @@ class FineTuneRunner:
         def G(p):
             return grads.get(id(p))
 
-        skr = []  # deferred weight-gradient sums of this backward
-
-        def run(tag, flops, prob, amode, bmode, tile=K.TILE_AUTO, unpack=None):
-            """One backward GEMM. Returns True when it is an x3w weight gradient whose sum is deferred to the
-            batched reduce at the end (then written to ``unpack[0]`` in the nn.Conv2d layout when ``unpack`` =
-            (out, KH, KW, Cin) is given, else to prob.C)."""
+        def run(tag, flops, prob, amode, bmode, tile=K.TILE_AUTO):
             if amode == AMM and self.r.x3 and _FT_WGRAD_X3W and K.gemm_x3w_ok(prob, bmode):
-                ws, defer = self.r._ws["sk"], False
-                if _FT_WGRAD_DEFER and prob.alpha == 1.0 and prob.beta == 0.0:
-                    S, slab, ld = K.x3w_slabs(prob, bmode)
-                    if S > 1:
-                        nflag = int(K.lib.capmi_gemm_workspace_flag_bytes()) // 4
-                        ws = self._wg_ws.get(tag)
-                        if ws is None or ws.numel() < nflag + S * slab:
-                            ws = torch.zeros(nflag + S * slab, device=dev, dtype=torch.int32)
-                            self._wg_ws[tag] = ws
-                        out, ld_out, unp = (unpack[0], 0, unpack[1:]) if unpack is not None else \
-                            (int(prob.C), prob.ldc, None)
-                        skr.append((ws[nflag:], S, slab, ld, out, prob.M, prob.N, ld_out, unp))
-                        defer = True
-                launch = lambda: K.gemm_x3w(prob, bmode, ws, defer=defer)  # noqa: E731
+                launch = lambda: K.gemm_x3w(prob, bmode, self.r._ws["sk"])  # noqa: E731
                 if hook is None:
                     launch()
                 else:
                     hook(tag, flops, launch, K.gemm_x3w_kernel_name(prob, bmode))
-                return defer
+                return
             if hook is None:
                 self._gemm(prob, amode, bmode, tile)
             else:
@@ -936,10 +909,10 @@ class FineTuneRunner:
             c2 = blk.conv2
             geo2 = dict(N=N, H=H, W=W, Cin=wd, KH=3, KW=3, stride=s, pad=1, Ho=H2, Wo=W2)
             if G(c2.weight) is not None:
-                if not run(tag + ".conv2.wgrad", 2.0 * r3 * wd * 9 * wd,
-                           K.problem(wd, 9 * wd, r3, da2, wd, b["y1"], 0, dwp, 9 * wd, conv=geo2, in_scale=s1,
-                                     in_shift=b1), AMM, BCONV, unpack=(G(c2.weight), 3, 3, wd)):
-                    K.conv_weight_unpack(dwp, tuple(c2.weight.shape), G(c2.weight))
+                run(tag + ".conv2.wgrad", 2.0 * r3 * wd * 9 * wd,
+                    K.problem(wd, 9 * wd, r3, da2, wd, b["y1"], 0, dwp, 9 * wd, conv=geo2, in_scale=s1,
+                              in_shift=b1), AMM, BCONV)
+                K.conv_weight_unpack(dwp, tuple(c2.weight.shape), G(c2.weight))
             da1 = dy3[:r1 * wd]  # dy3 is consumed
             if s == 1:
                 geod = dict(N=N, H=H, W=W, Cin=wd, KH=3, KW=3, stride=1, pad=1, Ho=H, Wo=W)
@@ -998,11 +971,6 @@ class FineTuneRunner:
                                   K.problem(r3, Cin, Cout, dyd, Cout, wt, Cout, dx, s * Cin, beta=1.0, **rm), wt,
                                   w1=cd.weight.detach())
             cur ^= 1
-        if skr:  # the deferred weight-gradient sums, one launch (the job array rebuilt only when a pointer moved)
-            key = tuple((sp[0].data_ptr(), sp[1], sp[4] if isinstance(sp[4], int) else sp[4].data_ptr()) for sp in skr)
-            if key != self._skr_key:
-                self._skr_key, self._skr = key, K.skr_jobs(skr, dev)
-            K.splitk_reduce_batch(self._skr, len(skr))
         self.state = None
         if _FT_WPREP_BATCH and self._wx3 is None and self.r.x3:
             self._build_wx3(stt)

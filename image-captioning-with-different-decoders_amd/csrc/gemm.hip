@@ -723,7 +723,7 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
     if (generic) *generic = 32;
     return 0;
   }
-  if (flags == CAPMI_GEMM_X3W || flags == CAPMI_GEMM_X3W_DEFER) {
+  if (flags == CAPMI_GEMM_X3W) {
     GemmArgs a;
     int S = 1;
     long long tiles = 0;
@@ -1123,8 +1123,7 @@ int x3w_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long ws_
   return 0;
 }
 
-int gemm_x3w(const capmi_gemm_problem* prob, int amode, int bmode, void* workspace, long long ws_bytes, hipStream_t s,
-             bool defer = false) {
+int gemm_x3w(const capmi_gemm_problem* prob, int amode, int bmode, void* workspace, long long ws_bytes, hipStream_t s) {
   const int cus = cu_count();
   const long long part_floats =
       workspace != nullptr && ws_bytes > sk_flag_bytes(cus) ? (ws_bytes - sk_flag_bytes(cus)) / 4 : 0;
@@ -1136,7 +1135,7 @@ int gemm_x3w(const capmi_gemm_problem* prob, int amode, int bmode, void* workspa
   CAPMI_REQUIRE(workspace == nullptr || aligned16(workspace), CAPMI_EINVAL);
   if (S > 1) a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
   int e = gemm_x3w_launch(a, bmode, (int)(tiles * S), s);
-  if (e || S == 1 || defer) return e;  // (defer: the caller sums the slabs, CAPMI_GEMM_X3W_DEFER)
+  if (e || S == 1) return e;
   const int ldp = a.tiles_n[0] * 128;
   return capmi_splitk_reduce(a.sk_part, S, (long long)prob->M * ldp, prob->M, prob->N, ldp, nullptr, prob->C,
                              prob->ldc, s);
@@ -1249,7 +1248,6 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   if (flags == CAPMI_GEMM_X3D) return gemm_x3d(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3S) return gemm_x3s(prob, amode, bmode, as_stream(stream));
   if (flags == CAPMI_GEMM_X3W) return gemm_x3w(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
-  if (flags == CAPMI_GEMM_X3W_DEFER) return gemm_x3w(prob, amode, bmode, workspace, ws_bytes, as_stream(stream), true);
   if (flags == CAPMI_GEMM_X3C) return gemm_x3c(prob, amode, bmode, as_stream(stream));
   int terms = flag_terms(flags);
   CAPMI_REQUIRE(terms >= 0, CAPMI_EINVAL);
@@ -1313,33 +1311,6 @@ extern "C" int capmi_splitk_reduce(const float* in, int S, long long slab, int r
   const unsigned blocks = (unsigned)std::min<long long>(cdiv(n, 256), 4096);
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), in, S,
                      slab, rows, cols, ld_in, bias, out, ld_out);
-  CAPMI_LAUNCH_CHECK();
-  return 0;
-}
-
-// Round 5: the deferred slab sums of many weight gradients in one launch (block row y = job y), each in
-// splitk_reduce_kernel's order (bit-identical), optionally written straight into the nn.Conv2d layout:
-// column c = (kh, kw, ci) of row co goes to out[co][ci][kh][kw] (capmi_conv_weight_unpack's map).
-__global__ void __launch_bounds__(256) splitk_reduce_batch_kernel(const capmi_skr_job* __restrict__ jobs) {
-  const capmi_skr_job j = jobs[blockIdx.y];
-  const long long n = (long long)j.rows * j.cols;
-  const bool unpack = j.kh * j.kw > 1;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    const int r = (int)(i / j.cols), c = (int)(i - (long long)r * j.cols);
-    const float v = slab_sum(j.in + r * j.ld_in + c, j.S, j.slab, 0.f);
-    if (unpack) {
-      const int tap = c / j.cin, ci = c - tap * j.cin, kh = tap / j.kw, kw = tap - kh * j.kw;
-      j.out[(((long long)r * j.cin + ci) * j.kh + kh) * j.kw + kw] = v;
-    } else {
-      j.out[r * j.ld_out + c] = v;
-    }
-  }
-}
-
-extern "C" int capmi_splitk_reduce_batch(const capmi_skr_job* jobs, int njobs, void* stream) {
-  CAPMI_REQUIRE(njobs >= 0 && njobs <= 65535 && (njobs == 0 || jobs), CAPMI_EINVAL);
-  if (njobs == 0) return 0;
-  hipLaunchKernelGGL(splitk_reduce_batch_kernel, dim3(64, njobs), dim3(256), 0, as_stream(stream), jobs);
   CAPMI_LAUNCH_CHECK();
   return 0;
 }

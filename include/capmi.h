@@ -156,12 +156,6 @@ int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int t
  * capmi_gemm_sk's) and are summed in a fixed order (capmi_splitk_reduce); capmi_gemm_sk_plan reports the
  * split count in `generic`. */
 #define CAPMI_GEMM_X3W 128
-/* CAPMI_GEMM_X3W_DEFER (alone, ABI 24): as CAPMI_GEMM_X3W, but when the plan splits the pixel range (S =
- * capmi_gemm_sk_plan's `generic` > 1) the S partial slabs stay in the workspace, after
- * capmi_gemm_workspace_flag_bytes(), and C is not written: slab s holds rows [M] x ldp floats at s * M * ldp
- * (ldp = N rounded up to 128), for the caller to sum later (capmi_splitk_reduce, capmi_splitk_reduce_batch).
- * With S == 1 it writes C as CAPMI_GEMM_X3W does. The fine-tune step sums all its weight gradients in one launch. */
-#define CAPMI_GEMM_X3W_DEFER 512
 /* CAPMI_GEMM_X3C (alone, ABI 23): DIRECT 3x3 convolution in the CAPMI_GEMM_X3 arithmetic for short-channel
  * layers (layer1's 3x3): CAPMI_A_CONV_NHWC with KH = KW = 3, stride 1, pad 1, Cin % 32 == 0, W <= 64, the
  * optional BN-apply + ReLU prologue; N == 64; B = the weight's three bf16 planes in CAPMI_GEMM_X3P's packed k
@@ -198,18 +192,6 @@ int capmi_gemm_sk_plan(const capmi_gemm_problem* problem, int amode, int bmode, 
 /* sum of S partial slabs: out[r][c] = sum_s in[s*slab + r*ld_in + c] (+ bias[c]); rows x cols */
 int capmi_splitk_reduce(const float* in, int S, long long slab, int rows, int cols, long long ld_in,
                         const float* bias, float* out, long long ld_out, void* stream);
-/* Many slab sums in one launch (ABI 24): jobs = DEVICE array of njobs descriptors, each summed as
- * capmi_splitk_reduce does (same order: bit-identical); kh * kw > 1 writes column c = (kh, kw, ci) of row r
- * to out[r][cin][kh][kw] (the nn.Conv2d layout of a weight gradient, capmi_conv_weight_unpack's map) instead
- * of out[r * ld_out + c]. */
-typedef struct {
-  const float* in;
-  float* out;
-  long long slab, ld_in, ld_out;
-  int S, rows, cols;
-  int kh, kw, cin;
-} capmi_skr_job;
-int capmi_splitk_reduce_batch(const capmi_skr_job* jobs, int njobs, void* stream);
 /* column sums of a rows x cols row-major matrix (bias gradients): out[c] = scale * sum_r in[r*ld + c].
  * work must hold CAPMI_COLSUM_GROUPS * cols floats. accumulate != 0 adds into out. */
 #define CAPMI_COLSUM_GROUPS 64
