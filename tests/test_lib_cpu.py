@@ -212,3 +212,30 @@ def test_vocabulary_layout():
     v = synthetic_vocab(8100)
     assert len(v) == 8100 and v(PAD_TOKEN) == 0 and v(START_TOKEN) == 8097 and v(END_TOKEN) == 8098
     assert v(UNK_TOKEN) == 8099 and v("never-seen") == 8099
+
+
+def test_struct_layout_matches_c_compiler(tmp_path):
+    """Every ctypes mirror (_lib.py) has the C compiler's size and field offsets for its struct in capmi.h
+    (gcc on a probe that prints offsetof of each mirrored field; a field name missing in C fails the build)."""
+    import shutil
+    import subprocess
+    from capmi._lib import DstepEpi, DstepSeg, GemmProblem, Wx3Job
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    mirrors = [(GemmProblem, "capmi_gemm_problem"), (Wx3Job, "capmi_wx3_job"), (DstepSeg, "capmi_dstep_seg"),
+               (DstepEpi, "capmi_dstep_epi")]
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "capmi.h"', "int main(void) {"]
+    want = []
+    for cls, cname in mirrors:
+        lines.append(f'  printf("%zu\\n", sizeof({cname}));')
+        want.append(ctypes.sizeof(cls))
+        for f in cls._fields_:
+            lines.append(f'  printf("%zu\\n", offsetof({cname}, {f[0]}));')
+            want.append(getattr(cls, f[0]).offset)
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert got == want
