@@ -101,7 +101,7 @@ _SIGS = {
     "capmi_conv_weight_pack_dgrad": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_conv_weight_pack_dgrad_s2": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_conv_weight_pack_dgrad_x3": [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp],
-    "capmi_weight_x3_batch": [c_vp, c_int, c_vp],
+    "capmi_weight_x3_batch": [c_vp, c_int, c_ll, c_vp],
     "capmi_conv_weight_unpack": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_zero_upsample2_nhwc": [c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp],
     "capmi_bn_bwd_reduce": [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_float, c_ll, c_int,

@@ -460,6 +460,7 @@ def wx3_jobs(specs, device):
     out: its [3][R][Kc] bf16 planes); the tensors must outlive every launch of the array."""
     from ._lib import Wx3Job
     arr = (Wx3Job * len(specs))()
+    big = 0
     for i, (w, out, mode, ph, pw) in enumerate(specs):
         co, ci, kh, kw = w.shape
         assert w.is_contiguous() and w.dtype == torch.float32 and out.dtype == torch.bfloat16
@@ -469,14 +470,18 @@ def wx3_jobs(specs, device):
         assert mode != WX3_FWD_X3P or ci % 32 == 0
         assert mode != WX3_DGRAD or (co % 32 == 0 and (ph < 0 or (kh == 3 and kw == 3)))
         arr[i] = Wx3Job(w.data_ptr(), out.data_ptr(), mode, co, ci, kh, kw, ph, pw, 0)
+        big = max(big, co * ci * T)
+        assert big < 2 ** 31  # (the kernel indexes a job's elements in 32 bits)
     raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
-    return raw.to(device)
+    return raw.to(device), big
 
 
 def weight_x3_batch(jobs, njobs):
-    """capmi_weight_x3_batch: the three-plane splits of every job in ``jobs`` (wx3_jobs) in one launch."""
-    _cuda(jobs, dtype=torch.uint8)
-    call("capmi_weight_x3_batch", ptr(jobs), int(njobs), stream())
+    """capmi_weight_x3_batch: the three-plane splits of every job in ``jobs`` = wx3_jobs(...) (the device
+    array and its largest job's element count) in one launch."""
+    arr, big = jobs
+    _cuda(arr, dtype=torch.uint8)
+    call("capmi_weight_x3_batch", ptr(arr), int(njobs), int(big), stream())
 
 
 def conv_weight_pack_dgrad_x3(w, out, ph=-1, pw=-1):

@@ -143,14 +143,14 @@ __global__ void __launch_bounds__(256) weight_x3_batch_kernel(const capmi_wx3_jo
   const int T = j.mode == CAPMI_WX3_DGRAD && j.ph >= 0 ? (j.ph + 1) * (j.pw + 1) : KH * KW;
   const int TW = j.mode == CAPMI_WX3_DGRAD && j.ph >= 0 ? j.pw + 1 : KW;
   const bool dg = j.mode == CAPMI_WX3_DGRAD || j.mode == CAPMI_WX3_DGRAD_T;
-  const long long R = dg ? j.cin : j.cout;                   // rows of the B operand
-  const long long Kc = (long long)T * (dg ? j.cout : j.cin);  // its k extent
-  const long long n = R * Kc;
+  const int R = dg ? j.cin : j.cout;  // rows of the B operand
+  const int Kc = T * (dg ? j.cout : j.cin);  // its k extent
+  const int n = R * Kc;                      // (< 2^31: the host checks)
   const float* __restrict__ w = j.w;
   __bf16* __restrict__ out = static_cast<__bf16*>(j.out);
-  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
-    const long long r = e / Kc;
-    const int k = (int)(e - r * Kc);
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {  // 32-bit index math
+    const int r = e / Kc;
+    const int k = e - r * Kc;
     int co, ci, kh, kw;
     if (j.mode == CAPMI_WX3_FWD) {  // [Cout][KH][KW][Cin] (capmi_conv_weight_pack_pad, Cin >= 4)
       co = (int)r;
@@ -185,10 +185,14 @@ __global__ void __launch_bounds__(256) weight_x3_batch_kernel(const capmi_wx3_jo
   }
 }
 
-extern "C" int capmi_weight_x3_batch(const capmi_wx3_job* jobs, int njobs, void* stream) {
-  CAPMI_REQUIRE(njobs >= 0 && njobs <= 65535 && (njobs == 0 || jobs), CAPMI_EINVAL);
-  if (njobs == 0) return 0;
-  hipLaunchKernelGGL(weight_x3_batch_kernel, dim3(64, njobs), dim3(256), 0, as_stream(stream), jobs);
+extern "C" int capmi_weight_x3_batch(const capmi_wx3_job* jobs, int njobs, long long max_elems, void* stream) {
+  CAPMI_REQUIRE(njobs >= 0 && njobs <= 65535 && (njobs == 0 || jobs) && max_elems >= 0, CAPMI_EINVAL);
+  CAPMI_REQUIRE(max_elems < (1LL << 31), CAPMI_ERANGE);
+  if (njobs == 0 || max_elems == 0) return 0;
+  // a grid row per job, sized so the largest job's threads take about 8 elements each (a fixed 64 blocks per
+  // row left the 2.4M-element layer4 jobs at ~144 serial elements per thread); rows of smaller jobs end early
+  const unsigned bx = (unsigned)std::min<long long>(std::max<long long>(cdiv(max_elems, 256 * 8), 1), 4096);
+  hipLaunchKernelGGL(weight_x3_batch_kernel, dim3(bx, njobs), dim3(256), 0, as_stream(stream), jobs);
   CAPMI_LAUNCH_CHECK();
   return 0;
 }

@@ -284,7 +284,8 @@ int capmi_conv_weight_pack_dgrad_x3(const float* w, int Cout, int Cin, int KH, i
                                     void* stream);
 /* Many conv weights' three-plane bf16 operands in one launch (ABI 24, the fine-tune step's weight
  * preparation). jobs: DEVICE array of njobs descriptors (read by the kernel, so it may be built once and
- * re-launched every step, e.g. from a captured graph); w = the nn.Conv2d weight [Cout][Cin][KH][KW] fp32, out =
+ * re-launched every step, e.g. from a captured graph), max_elems = the largest job's R * Kc (< 2^31; sizes
+ * the grid); w = the nn.Conv2d weight [Cout][Cin][KH][KW] fp32, out =
  * three planes [3][R][Kc] bf16, the exact RNE split of capmi_split3_bf16, bit-identical to:
  *   CAPMI_WX3_FWD      R = Cout, Kc = KH*KW*Cin: split3 of capmi_conv_weight_pack_pad (Cin >= 4, unpadded)
  *   CAPMI_WX3_FWD_X3P  the same in the x3p conv k order (ci/32, kh, kw, ci%32); Cin % 32 == 0
@@ -302,7 +303,7 @@ typedef struct {
   int ph, pw;
   int pad_;
 } capmi_wx3_job;
-int capmi_weight_x3_batch(const capmi_wx3_job* jobs, int njobs, void* stream);
+int capmi_weight_x3_batch(const capmi_wx3_job* jobs, int njobs, long long max_elems, void* stream);
 /* [Cout][KH][KW][Cin] (GEMM layout of a weight gradient) -> [Cout][Cin][KH][KW] (nn.Conv2d layout) */
 int capmi_conv_weight_unpack(const float* packed, int Cout, int Cin, int KH, int KW, float* out, void* stream);
 /* out (N,H,W,C) = dy (N,Ho,Wo,C) at even (h, w), zero elsewhere (stride-2 conv data gradient) */
