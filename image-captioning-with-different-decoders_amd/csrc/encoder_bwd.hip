@@ -139,6 +139,29 @@ __device__ __forceinline__ void wx3_store(__bf16* out, long long n, long long e,
 
 __global__ void __launch_bounds__(256) weight_x3_batch_kernel(const capmi_wx3_job* __restrict__ jobs) {
   const capmi_wx3_job j = jobs[blockIdx.y];
+  if (j.mode == CAPMI_WX3_DGRAD_T) {  // 1x1 transpose through LDS: 64 x 64 tiles, both sides row-contiguous
+    __shared__ float tile[64][65];
+    const int co_n = j.cout, ci_n = j.cin, tco = (co_n + 63) / 64, tci = (ci_n + 63) / 64;
+    const long long n = (long long)co_n * ci_n;
+    __bf16* __restrict__ out = static_cast<__bf16*>(j.out);
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int t = blockIdx.x; t < tco * tci; t += gridDim.x) {
+      const int co0 = (t / tci) * 64, ci0 = (t % tci) * 64;
+      __syncthreads();  // (the previous tile's reads are done)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {  // rows co0 + ty + 4 i, columns ci0 + tx: coalesced along ci
+        const int co = co0 + ty + 4 * i, ci = ci0 + tx;
+        tile[ty + 4 * i][tx] = co < co_n && ci < ci_n ? j.w[(long long)co * ci_n + ci] : 0.f;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {  // out[ci][co]: coalesced along co
+        const int ci = ci0 + ty + 4 * i, co = co0 + tx;
+        if (ci < ci_n && co < co_n) wx3_store(out, n, (long long)ci * co_n + co, tile[tx][ty + 4 * i]);
+      }
+    }
+    return;
+  }
   const int KH = j.kh, KW = j.kw;
   const int T = j.mode == CAPMI_WX3_DGRAD && j.ph >= 0 ? (j.ph + 1) * (j.pw + 1) : KH * KW;
   const int TW = j.mode == CAPMI_WX3_DGRAD && j.ph >= 0 ? j.pw + 1 : KW;
