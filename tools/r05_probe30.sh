@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5, probe 30: the batched weight preparation (grid rows sized by the largest job, 32-bit index math, 1x1 transposes through LDS): its tests, the
+# round 5, probe 30: the batched weight preparation (grid rows sized by the largest job, 32-bit index math, 1x1 and 3x3-dgrad jobs through LDS tiles): its tests, the
 # fine-tune tests, config 4 with it and with the per-conv path (CAPMI_FT_WPREP_BATCH=0), alternating, and a trace
 T="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
 B="python bench.py --config glove_finetune --steps 20 --warmup 3 --no-cpu-baseline --no-roofline"
