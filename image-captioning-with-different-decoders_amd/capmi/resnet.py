@@ -416,7 +416,9 @@ class EncoderRunner:
             # the launch capmi_gemm_sk_ex makes for CAPMI_GEMM_BF16_IO (gemm.hip: gemm_bf16_io)
             # (round 5: K <= 256 takes the one-stage 128x64 form, data-parallel)
             st1 = Kd <= 256
-            bn_ = 64 if co <= 64 or st1 else 128
+            cus = torch.cuda.get_device_properties(x.device).multi_processor_count
+            narrow = 2 * -(-rows // 128) * -(-co // 128) <= cus  # (gemm.hip: 128x64 on grids under half the CUs)
+            bn_ = 64 if co <= 64 or st1 or narrow else 128
             tiles = -(-rows // 128) * -(-co // bn_)
             slots = 2 * torch.cuda.get_device_properties(x.device).multi_processor_count
             rounds = -(-tiles // slots)

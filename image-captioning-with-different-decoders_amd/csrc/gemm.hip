@@ -816,8 +816,13 @@ int gemm_bf16_io(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
   // stage, four workgroups per CU, data-parallel (round 5: l3 c3 20.0 -> 17.1 us, l2 c3 24.7 -> 18.4, l1 c3 33.3 ->
   // 24.3; at K = 512 a tie and above it slower: the two-stage 128x128 form stays)
   const bool st1 = tile == CAPMI_TILE_AUTO && p.K <= 256;
+  // AUTO on a grid of 128x128 tiles that fills at most half the CUs (layer4's 3136-row convs: 100 tiles):
+  // 128x64 tiles, twice the workgroups (round 5: l4 3x3 53.2 -> 40.8 us, l4 c1 25.8 -> 18.9; the 400-tile
+  // layer4 c3 / downsample and layer3's 196-tile grids stay at 128x128, where 128x64 measured slower)
+  const bool narrow = tile == CAPMI_TILE_AUTO && 2 * cdiv(p.M, 128) * cdiv(p.N, 128) <= cu_count();
   const int bm = 128,
-            bn = (st1 || tile == CAPMI_TILE_128x64 || tile == CAPMI_TILE_64 || (tile == CAPMI_TILE_AUTO && p.N <= 64)) ? 64 : 128;
+            bn = (st1 || narrow || tile == CAPMI_TILE_128x64 || tile == CAPMI_TILE_64 ||
+                  (tile == CAPMI_TILE_AUTO && p.N <= 64)) ? 64 : 128;
   GemmArgs a;
   memset(&a, 0, sizeof(a));
   a.nprob = 1;
