@@ -60,26 +60,42 @@ class Adam:
     def grad_buffers(self):
         return [f[2] for f in self.flats]
 
-    def grad_buckets(self, first):
-        """Split the flat gradient buffers into two lists of contiguous views: the span covering the
-        parameters in ``first`` (a set of Parameter objects; 256-B aligned slots, so the span also
-        holds their zero padding) and the rest. Data-parallel steps all-reduce ``first`` as soon as
-        those gradients are final, the rest after the backward."""
-        head, rest = [], []
+    def grad_spans(self, groups):
+        """Split the flat gradient buffers into contiguous views, one list per group of ``groups``
+        (sets of Parameter objects, each group's parameters adjacent in the layout; 256-B aligned
+        slots, so a span also holds its parameters' zero padding), and a last list with the rest.
+        Data-parallel steps all-reduce a group's span as soon as its gradients are final (the fc
+        bucket beside the decoder's BPTT; layer4 / layer3 / layer2 of a fine-tuned encoder as its
+        backward leaves each stage), the rest after the backward."""
+        out = [[] for _ in range(len(groups) + 1)]
         for dt, pf, gf, m, v, layout in self.flats:
-            idx = [i for i, (p, off, k) in enumerate(layout) if any(p is q for q in first)]
-            if not idx:
-                rest.append(gf)
-                continue
-            lo = layout[idx[0]][1]
-            hi = layout[idx[-1] + 1][1] if idx[-1] + 1 < len(layout) else gf.numel()
-            if idx != list(range(idx[0], idx[-1] + 1)):
-                raise ValueError("grad_buckets: the parameters of the first bucket are not contiguous")
-            head.append(gf[lo:hi])
-            if lo > 0:
-                rest.append(gf[:lo])
-            if hi < gf.numel():
-                rest.append(gf[hi:])
+            cuts = []
+            for gi, grp in enumerate(groups):
+                ids = {id(q) for q in grp}
+                idx = [i for i, (p, off, k) in enumerate(layout) if id(p) in ids]
+                if not idx:
+                    continue
+                if idx != list(range(idx[0], idx[-1] + 1)):
+                    raise ValueError(f"grad_spans: the parameters of group {gi} are not contiguous")
+                lo = layout[idx[0]][1]
+                hi = layout[idx[-1] + 1][1] if idx[-1] + 1 < len(layout) else gf.numel()
+                cuts.append((lo, hi, gi))
+            cuts.sort()
+            pos = 0
+            for lo, hi, gi in cuts:
+                if lo < pos:
+                    raise ValueError("grad_spans: groups overlap")
+                if lo > pos:
+                    out[-1].append(gf[pos:lo])
+                out[gi].append(gf[lo:hi])
+                pos = hi
+            if pos < gf.numel():
+                out[-1].append(gf[pos:])
+        return out
+
+    def grad_buckets(self, first):
+        """(span of the parameters in ``first``, the rest): grad_spans with one group."""
+        head, rest = self.grad_spans([first])
         return head, rest
 
     def zero_grad(self, set_to_none=False):

@@ -219,7 +219,6 @@ class EncoderRunner:
         Ho, Wo = (H + 2 * pd - kh) // st + 1, (W + 2 * pd - kw) // st + 1
         rows = N * Ho * Wo
         Kd = ci * kh * kw
-        w = self.packed.get(conv)
         geo = dict(N=N, H=H, W=W, Cin=ci, KH=kh, KW=kw, stride=st, pad=pd, Ho=Ho, Wo=Wo)
         stats = ws_stats = self._ws["stats"] if train else None
         kw_ = dict(stats=ws_stats)
@@ -278,7 +277,10 @@ class EncoderRunner:
             else:
                 launch()
             return Ho, Wo, rows
+        # the fp32 packed weight is fetched (and packed when stale) only by the routes that read it: the x3 routes
+        # read their split planes, built from it only when those are rebuilt
         if nchw:
+            w = self.packed.get(conv)
             # conv1: the NCHW images are re-laid out once as NHWC with 4 channels (one float4 per
             # pixel); the implicit GEMM then runs over k = (kh, kw, c4), the 4th channel zero
             img4 = self._ws["img4"]
@@ -291,6 +293,7 @@ class EncoderRunner:
             # short-k convs (layer1's K = 64): both operands split in-kernel on the 256-thread kernel
             # (CAPMI_GEMM_SPLIT3, two workgroups per CU overlap one's epilogue with the other's loads)
             sc, sh = in_ss if in_ss is not None else (None, None)
+            w = self.packed.get(conv)
             if kh == 1 and st == 1 and in_ss is None:
                 prob, mode = K.problem(rows, co, Kd, x, ci, w, Kd, out, co, **kw_), CAPMI_A_KMAJOR
             else:
@@ -333,14 +336,12 @@ class EncoderRunner:
                 launch()
             return Ho, Wo, rows
         elif kh == 1 and st == 1 and in_ss is None:
-            if x3 and Kd % 32 == 0:
-                w = self._packed_x3(conv)
+            w = self._packed_x3(conv) if x3 and Kd % 32 == 0 else self.packed.get(conv)
             prob = K.problem(rows, co, Kd, x, ci, w, Kd, out, co, **kw_)
             mode = CAPMI_A_KMAJOR
         else:
             sc, sh = in_ss if in_ss is not None else (None, None)
-            if x3 and Kd % 32 == 0 and ci % 32 == 0:
-                w = self._packed_x3(conv)
+            w = self._packed_x3(conv) if x3 and Kd % 32 == 0 and ci % 32 == 0 else self.packed.get(conv)
             prob = K.problem(rows, co, Kd, x, 0, w, Kd, out, co, conv=geo, in_scale=sc, in_shift=sh, **kw_)
             mode = CAPMI_A_CONV_NHWC
         if w.dtype == torch.bfloat16:  # the three-plane split weight: fp32-accurate x3 GEMM
@@ -364,9 +365,10 @@ class EncoderRunner:
 
     def _packed_x3(self, conv, tap_inner=False):
         """[3][Cout][K] bf16 split of the packed fp32 weight (B operand of gemm_x3; with ``tap_inner``
-        in gemm_x3p's conv k order), refreshed when the weight tensor changes (FineTuneRunner drops
-        the trainable convs' entries every step: the fused Adam writes the weights in place without
-        bumping their version)."""
+        in gemm_x3p's conv k order), refreshed when the weight tensor changes. The fused Adam writes the
+        weights in place without bumping their version, so FineTuneRunner.forward refreshes the trainable
+        convs' entries itself: the ones its batched job array covers in that launch, every other one (and
+        the fp32 pack they are made from) dropped, to be rebuilt here from the current weights."""
         w = conv.weight
         key = ("x3p" if tap_inner else "x3", id(conv))
         ent = self.packed.cache.get(key)
@@ -637,6 +639,8 @@ class FineTuneRunner:
         self._dgrad_x3 = {}
         self._wx3_specs = []
         self._wx3 = None
+        self._wx3_n = 0  # jobs in the device array (fixed when it is built)
+        self._wx3_fwd = {}  # cache key -> the forward planes buffer the array refreshes
 
     # ------------------------------------------------------------------ forward
     def _bn_save(self, ws, bn, rows):
@@ -661,15 +665,22 @@ class FineTuneRunner:
         # the optimizer updates trainable weights in place (same storage, same _version): refresh every
         # trainable conv's planes in one launch (the cache entries keep their buffers), or drop the packed copies
         # so this forward re-packs them
+        # Entries the job array does not refresh are dropped every step, whichever route created them: the fp32
+        # [Cout][KH][KW][Cin] pack of every trainable 3x3 (the source a rebuilt split is made from) and any split
+        # entry created after the array was built (a batch or image size that routes a conv differently, e.g. a
+        # ragged last batch, or a weight whose storage moved) -- those are rebuilt from the current weights
+        # whenever a forward uses them.
         if self._wx3 is not None:
-            K.weight_x3_batch(self._wx3, len(self._wx3_specs))
-        for li in range(self.first, 5) if self._wx3 is None else ():
+            K.weight_x3_batch(self._wx3, self._wx3_n)
+        for li in range(self.first, 5):
             for blk in getattr(net, f"layer{li}"):
                 r.packed.cache.pop(id(blk.conv2), None)
                 convs = [blk.conv1, blk.conv2, blk.conv3] + ([blk.downsample[0]] if blk.downsample is not None else [])
                 for c in convs:
-                    r.packed.cache.pop(("x3", id(c)), None)
-                    r.packed.cache.pop(("x3p", id(c)), None)
+                    for key in (("x3", id(c)), ("x3p", id(c))):
+                        ent = r.packed.cache.get(key)
+                        if ent is not None and self._wx3_fwd.get(key) is not ent[2]:
+                            del r.packed.cache[key]
         H1, W1, rows = r._conv("conv1", imgs, net.conv1, ws["y1"], N, H, W, True, nchw=True)
         s, b = r._bn(ws, net.bn1, rows, True)
         Hp, Wp = (H1 + 2 - 3) // 2 + 1, (W1 + 2 - 3) // 2 + 1
@@ -713,7 +724,7 @@ class FineTuneRunner:
                     K.bn_add_relu(y3, s3, b3, x, o, r3, Cout)
                 bns += [blk.bn1, blk.bn2, blk.bn3]
                 if trainable:
-                    blocks.append(dict(blk=blk, tag=tag, x=x, Cin=Cx, H=H, W=W, H2=H2, W2=W2, wd=wd, Cout=Cout,
+                    blocks.append(dict(blk=blk, tag=tag, li=li, x=x, Cin=Cx, H=H, W=W, H2=H2, W2=W2, wd=wd, Cout=Cout,
                                        stride=st, y1=y1, y2=y2, y3=y3, yd=yd, out=o,
                                        ss=[(s1, b1, m1), (s2, b2, m2), (s3, b3, m3), (sd, bd, md)]))
                     x = o
@@ -752,10 +763,14 @@ class FineTuneRunner:
         K.gemm_sk(prob, amode, self.r._ws["sk"], tile, bmode, flags=self._flags(prob, amode, bmode))
 
     @torch.no_grad()
-    def backward(self, dfeat, grads, hook=None):
+    def backward(self, dfeat, grads, hook=None, on_layer=None):
         """dfeat: (N, OH, OW, 2048) gradient of the features. grads: dict id(param) -> tensor
         receiving d(loss)/d(param) (conv weights in nn.Conv2d layout, BN weight/bias); missing
-        entries are skipped. ``hook(tag, flops, launch, key)`` optionally wraps every conv GEMM."""
+        entries are skipped. ``hook(tag, flops, launch, key)`` optionally wraps every conv GEMM.
+        ``on_layer(li)`` is called (in stream order) as soon as stage li's gradients are final --
+        after its first block, before the next stage's backward is launched: layer4, layer3,
+        layer2 -- so a data-parallel step can all-reduce each stage's bucket beside the rest of
+        the backward (nothing launched after the call reads or writes stage li's gradients)."""
         stt = self.state
         if stt is None:
             raise RuntimeError("FineTuneRunner.backward without a saved forward")
@@ -819,6 +834,9 @@ class FineTuneRunner:
             batch = _FT_WPREP_BATCH and use and ((conv_w is not None and _FT_PACK_X3) or w1 is not None)
             key = ((conv_w if conv_w is not None else w1).data_ptr(), ph, pw) if batch else None
             planes = self._dgrad_x3.get(key) if batch else None
+            # jobs are recorded only before the array is built; a key it does not cover (a weight whose storage
+            # moved) takes the per-conv path into the shared scratch planes from then on
+            record = batch and self._wx3 is None
             if planes is not None and self._wx3 is not None:
                 prob.B = planes.data_ptr()  # refreshed this step by the forward's batched launch
                 conv_w = w1 = None
@@ -834,7 +852,7 @@ class FineTuneRunner:
                 if not use:
                     return run(tag, flops, prob, amode, BW)
                 dst = w3
-                if batch:  # first step: this conv's own planes, recorded as a job of the batched launch
+                if record:  # first step: this conv's own planes, recorded as a job of the batched launch
                     dst = self._dgrad_x3.get(key)
                     if dst is None:
                         dst = torch.empty(3 * n * kd, device=dev, dtype=torch.bfloat16)
@@ -973,6 +991,8 @@ class FineTuneRunner:
                                   K.problem(r3, Cin, Cout, dyd, Cout, wt, Cout, dx, s * Cin, beta=1.0, **rm), wt,
                                   w1=cd.weight.detach())
             cur ^= 1
+            if on_layer is not None and (bi == 0 or blocks[bi - 1]["li"] != b["li"]):
+                on_layer(b["li"])
         self.state = None
         if _FT_WPREP_BATCH and self._wx3 is None and self.r.x3:
             self._build_wx3(stt)
@@ -982,6 +1002,7 @@ class FineTuneRunner:
         weights of every trainable conv (the cache entries this step created, refreshed in place from now on)
         and the data-gradient planes run_dgrad recorded."""
         specs = list(self._wx3_specs)
+        fwd = {}
         for b in stt["blocks"]:
             blk = b["blk"]
             convs = [blk.conv1, blk.conv2, blk.conv3] + ([blk.downsample[0]] if blk.downsample is not None else [])
@@ -990,8 +1011,11 @@ class FineTuneRunner:
                     ent = self.r.packed.cache.get((tag, id(c)))
                     if ent is not None:
                         specs.append((c.weight.detach(), ent[2], mode, -1, -1))
+                        fwd[(tag, id(c))] = ent[2]
         if specs:
             self._wx3_specs = specs
+            self._wx3_fwd = fwd
+            self._wx3_n = len(specs)
             self._wx3 = K.wx3_jobs(specs, stt["device"])
 
 

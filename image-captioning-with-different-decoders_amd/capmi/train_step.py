@@ -26,6 +26,14 @@ With more than one rank (eager mode) the all-reduce of step k is issued asynchro
 its clamp+Adam update is applied at the start of step k+1's decoder, after step k+1's
 encoder forward has been launched: the encoder does not read the decoder's weights, so the
 collective overlaps the ResNet forward. ``flush()`` completes the last pending update.
+
+Encoder fine-tune (config 4) with more than one rank, eager and graph alike: the decoder's
+gradient bucket is all-reduced as soon as the decoder backward ends, beside the encoder
+backward; the encoder's layer4, layer3 and layer2 buckets each as the backward leaves that
+stage (FineTuneRunner.backward's ``on_layer``); clamp + Adam once all are in
+(models/attention.py:417-430). In graph mode the step is captured as segments cut at exactly
+those points and the collectives are issued between the segments' replays. ``schedule`` lists
+what the last call issued, in order ("seg0", "ar:dec", "seg1", "ar:layer4", ...).
 """
 import os
 
@@ -50,6 +58,9 @@ class AttentionTrainStep:
             pipeline = False  # the encoder of batch k needs the update of batch k-1
             self._denc = None
             self.enc_params = [q for grp in encoder_optimizer.param_groups for q in grp["params"]]
+            # per-stage gradient buckets of the encoder (contiguous spans of its flat buffer): layer4, layer3,
+            # layer2 (children 7, 6, 5 of resnet, models/encoder.py:112-121), and whatever else is trainable
+            self._enc_buckets = self._stage_buckets(encoder, encoder_optimizer)
         dev = next(decoder.parameters()).device
         self.ctx = ctx or cdist.DistCtx(device=dev)
         self.alpha_c = alpha_c
@@ -70,10 +81,20 @@ class AttentionTrainStep:
         self.seed_dev = torch.full((1,), s, dtype=torch.int64, device=dev)
         self._graph = None
         self._static = None
+        # per-shape graph cache: key (image shape, caption shape, lengths) -> captured graphs and the
+        # workspaces they hold raw pointers into (pinned: the per-shape workspace caches keep only the
+        # latest shape). Once CAPMI_GRAPH_CACHE keys are held, a new key runs eagerly (no eviction, so a
+        # stream of one-off caption lengths cannot make every call a capture).
+        self._gcache = {}
+        self.graph_cache_size = int(os.environ.get("CAPMI_GRAPH_CACHE", "8"))
+        self.counts = {"replay": 0, "eager": 0, "capture": 0}
         # optional callable(label) run before each graph capture (bench: graph-node timing), and
         # the labels of the graphs the last call replayed ("enc0"/"dec1"..., or "step")
         self.capture_hook = None
         self.replayed = []
+        self.schedule = []  # graph segments replayed and collectives issued by the last call, in order
+        self._segs = None  # data-parallel graph mode: (graphs, the bucket label ending each)
+        self._capturing = False  # inside _capture (warm-ups and capture: no collectives, no update)
         # pipelined mode: the frozen encoder of batch k runs on its own stream while the decoder
         # step of batch k-1 runs (the encoder reads no decoder state); see _pipe_call
         self.pipeline = pipeline
@@ -84,7 +105,6 @@ class AttentionTrainStep:
             self.pipe_graph = graph
             self.graph_mode = False
             self._pg = None
-            self._pg_key = None
             lo, hi = torch.cuda.Stream.priority_range()
             pe, pd = {"swap": (hi, lo), "equal": (lo, lo)}.get(os.environ.get("CAPMI_PIPE_PRIO", ""), (lo, hi))
             self.s_enc = torch.cuda.Stream(device=dev, priority=pe)
@@ -96,6 +116,57 @@ class AttentionTrainStep:
 
     def _grads(self):
         return {n: self.params[n].grad for n in self.need}
+
+    @staticmethod
+    def _stage_buckets(encoder, opt):
+        """{"layer4": views, "layer3": ..., "layer2": ..., "rest": ...} over the encoder optimizer's flat
+        gradient buffer (Adam.grad_spans); stages with no trainable parameter map to []."""
+        seq = getattr(encoder, "resnet", None)
+        owned = {id(q) for grp in opt.param_groups for q in grp["params"]}
+        groups, names = [], []
+        if seq is not None and len(seq) >= 8:
+            for li in (4, 3, 2):
+                ps = [q for q in seq[li + 3].parameters() if id(q) in owned]
+                if ps:
+                    groups.append(set(ps))
+                    names.append(f"layer{li}")
+        spans = opt.grad_spans(groups)
+        out = {f"layer{li}": [] for li in (2, 3, 4)}
+        out.update(dict(zip(names, spans[:-1])))
+        out["rest"] = spans[-1]
+        return out
+
+    def _bucket(self, label):
+        if label == "dec":
+            return self.opt.grad_buffers()
+        if label == "fc":
+            return self._b_fc
+        if label == "dec_rest":
+            return self._b_rest
+        return self._enc_buckets[label]
+
+    def _pins(self):
+        """References to every per-shape workspace a capture's kernels address (encoder runner, fine-tune
+        pools, decoder core and fused-loss buffers): held by the cache entry, so a later shape replacing
+        them in those caches does not free memory a cached graph still replays into."""
+        pins = [dict(DF.CORE._ws), dict(vars(DF._FS))]
+        r = getattr(self.encoder, "_runner", None)
+        if r is not None:
+            pins.append(r._ws)
+        ft = getattr(self.encoder, "_ft_runner", None)
+        if ft is not None:
+            pins += [dict(ft.saved.bufs), dict(ft.grad.bufs)]
+        if getattr(self, "_denc", None) is not None:
+            pins.append(self._denc)
+        return pins
+
+    def _cache_room(self, key):
+        return key in self._gcache or len(self._gcache) < self.graph_cache_size
+
+    def _issue(self, label, works):
+        """All-reduce (mean, async) the bucket ``label`` on the collective stream, behind the work queued so far."""
+        works.extend(cdist.allreduce_mean_(self._bucket(label), self.ctx, async_op=True))
+        self.schedule.append(f"ar:{label}")
 
     def _feat_layout(self, imgs):
         """(feature buffer shape, dup) for a batch: the layer4 map when the encoder's pool only
@@ -150,9 +221,16 @@ class AttentionTrainStep:
             self._step_all()
 
     # ---------------------------------------------------------------- eager
-    def _body_ft(self, imgs, captions, caption_lengths, with_update):
+    def _body_ft(self, imgs, captions, caption_lengths, with_update, cut=None):
         """Fine-tune step: encoder forward keeping layer2-4 activations, decoder fwd/bwd also
-        producing d(features), encoder backward into the encoder optimizer's gradients."""
+        producing d(features), encoder backward into the encoder optimizer's gradients.
+
+        Data parallel: each bucket is handed over where its gradients become final -- the decoder's
+        after the decoder backward (it overlaps the encoder backward), layer4 / layer3 / layer2 as
+        the encoder backward leaves each stage (they overlap the lower stages' backward). Eager
+        (``cut`` None): the all-reduces are issued right there and the update follows once all
+        are in. Graph capture: ``cut(label)`` ends the segment being captured there; _replay
+        issues the bucket's all-reduce between that segment's replay and the next one's."""
         K.counter_add(self.seed_dev, 1)
         self._apply_pending()
         _, dup = self._feat_layout(imgs)
@@ -162,23 +240,37 @@ class AttentionTrainStep:
         loss, _, _ = DF.fused_loss_and_grads(self.decoder, feats, captions, caption_lengths,
                                              self.alpha_c, self._grads(), need=self.need,
                                              seed_dev=self.seed_dev, denc=self._denc, dup=dup)
+        dp = self.ctx.distributed
         works = []
-        if self.ctx.distributed and not self.graph_mode:
-            # the decoder's gradients are final: their all-reduce overlaps the encoder backward
-            works = cdist.allreduce_mean_(self.opt.grad_buffers(), self.ctx, async_op=True)
-        self.encoder.ft_backward(self._denc, {id(q): q.grad for q in self.enc_params})
-        if self.ctx.distributed and not self.graph_mode:
-            works += cdist.allreduce_mean_(self.enc_opt.grad_buffers(), self.ctx, async_op=True)
+        hand = None
+        if dp and cut is not None:
+            # the lowest trainable stage finishes with the backward itself: its bucket is issued after the
+            # last segment (a cut there would leave an empty graph)
+            last = f"layer{self.encoder._ft().first}"
+
+            def hand(label):
+                if label != last:
+                    cut(label)
+        elif dp and not self._capturing:
+            def hand(label):
+                self._issue(label, works)
+        if hand is not None:
+            hand("dec")  # the decoder's gradients are final
+        self.encoder.ft_backward(self._denc, {id(q): q.grad for q in self.enc_params},
+                                 on_layer=None if hand is None else (lambda li: hand(f"layer{li}")))
+        if dp and cut is None and not self._capturing:
+            self._issue("rest", works)
             for w in works:
                 w.wait()
             self._step_all()
+            self.schedule.append("update")
         elif with_update:
             self._step_all()
         return loss
 
-    def _body(self, imgs, captions, caption_lengths, with_update):
+    def _body(self, imgs, captions, caption_lengths, with_update, cut=None):
         if self.fine_tune:
-            return self._body_ft(imgs, captions, caption_lengths, with_update)
+            return self._body_ft(imgs, captions, caption_lengths, with_update, cut=cut)
         K.counter_add(self.seed_dev, 1)
         shape, dup = self._feat_layout(imgs)
         if hasattr(self.encoder, "forward_into"):
@@ -189,7 +281,8 @@ class AttentionTrainStep:
         self._apply_pending()
         loss, _, _ = DF.fused_loss_and_grads(self.decoder, feats, captions, caption_lengths,
                                              self.alpha_c, self._grads(), need=self.need,
-                                             seed_dev=self.seed_dev, dup=dup)
+                                             seed_dev=self.seed_dev, dup=dup,
+                                             on_fc_grads=None if cut is None else (lambda: cut("fc")))
         if with_update:
             self.opt.step()
         return loss
@@ -238,22 +331,21 @@ class AttentionTrainStep:
         workspace is allocated outside the graphs' pools; each graph keeps its own pool (the two
         streams' graphs run concurrently)."""
         dev = imgs.device
-        N = imgs.shape[0]
         upd = not self.ctx.distributed
         snap = self._snapshot()
         shape, dup = self._feat_layout(imgs)
-        self._feats = [torch.empty(shape, device=dev, dtype=torch.float32) for _ in range(2)]
+        feats = [torch.empty(shape, device=dev, dtype=torch.float32) for _ in range(2)]
         pg = []
         for slot in range(2):
             pg.append({"imgs": imgs.detach().clone(), "caps": captions.detach().clone(),
-                       "lens": list(caption_lengths)})
+                       "lens": list(caption_lengths), "slot": slot})
         torch.cuda.synchronize()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
-                self._encode_into(pg[0]["imgs"], self._feats[0], dup)
-                self._dec_body(self._feats[0], pg[0]["caps"], pg[0]["lens"], with_update=False, dup=dup)
+                self._encode_into(pg[0]["imgs"], feats[0], dup)
+                self._dec_body(feats[0], pg[0]["caps"], pg[0]["lens"], with_update=False, dup=dup)
         torch.cuda.current_stream().wait_stream(s)
         self._restore(snap)
         for slot in range(2):
@@ -262,25 +354,53 @@ class AttentionTrainStep:
             if self.capture_hook is not None:
                 self.capture_hook(f"enc{slot}")
             with torch.cuda.graph(g):
-                self._encode_into(st["imgs"], self._feats[slot], dup)
+                self._encode_into(st["imgs"], feats[slot], dup)
             st["g_enc"] = g
-            st["feats"] = self._feats[slot]  # the graphs hold raw pointers: keep the buffer alive
+            st["feats"] = feats[slot]  # the graphs hold raw pointers: keep the buffer alive
             if self.capture_hook is not None:
                 self.capture_hook(f"dec{slot}")
             if upd:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    st["loss"] = self._dec_body(self._feats[slot], st["caps"], st["lens"], with_update=True,
+                    st["loss"] = self._dec_body(feats[slot], st["caps"], st["lens"], with_update=True,
                                                 dup=dup)
                 st["g_dec"] = g
             else:
                 # data parallel: two graphs cut where the fc gradients are final, so their all-reduce
                 # is issued between the replays and runs beside the backward-through-time graph
                 st["loss"], st["g_dec"], st["g_dec2"] = self._capture_split(
-                    lambda cut: self._dec_body(self._feats[slot], st["caps"], st["lens"], with_update=False, on_fc=cut,
+                    lambda cut: self._dec_body(feats[slot], st["caps"], st["lens"], with_update=False, on_fc=cut,
                                                dup=dup))
         torch.cuda.synchronize()
-        self._pg, self._pg_key = pg, key
+        pg[0]["pins"] = self._pins()
+        self.counts["capture"] += 1
+        return pg
+
+    @staticmethod
+    def _capture_segments(body):
+        """Capture ``body(cut)`` into a chain of HIP graphs sharing one memory pool: every
+        ``cut(label)`` ends the graph being captured and starts the next. Returns (body's result,
+        [graphs], [the label of the cut that ended each graph; None for the last])."""
+        graphs, labels = [torch.cuda.CUDAGraph()], []
+        pool = torch.cuda.graph_pool_handle()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        cs = torch.cuda.Stream()
+        cs.wait_stream(torch.cuda.current_stream())
+
+        def cut(label):
+            graphs[-1].capture_end()
+            labels.append(label)
+            graphs.append(torch.cuda.CUDAGraph())
+            graphs[-1].capture_begin(pool=pool)
+
+        with torch.cuda.stream(cs):
+            graphs[0].capture_begin(pool=pool)
+            out = body(cut)
+            graphs[-1].capture_end()
+            labels.append(None)
+        torch.cuda.current_stream().wait_stream(cs)
+        return out, graphs, labels
 
     @staticmethod
     def _capture_split(body):
@@ -317,14 +437,20 @@ class AttentionTrainStep:
 
     def _pg_call(self, imgs, captions, caption_lengths):
         key = (tuple(imgs.shape), tuple(captions.shape), tuple(caption_lengths))
-        if self._pg_key != key:
+        pg = self._gcache.get(key)
+        early = None
+        if pg is None:
+            if not self._cache_room(key):
+                return self._pipe_call(imgs, captions, caption_lengths)  # cache full: this key runs eagerly
             if self._pend is not None:
-                self.flush()
-            self._pg_capture(imgs, captions, caption_lengths, key)
+                early = self.flush()  # the pending batch's loss: returned by this call, as the pipeline would
+            pg = self._pg_capture(imgs, captions, caption_lengths, key)
+            self._gcache[key] = pg
+        self._pg = pg
         cur = torch.cuda.current_stream()
         slot = self._slot
         self._slot ^= 1
-        st = self._pg[slot]
+        st = pg[slot]
         # the slot's static inputs and features were last read by the decoder of the previous call
         self.s_enc.wait_stream(cur)
         if self._ev_dec is not None:
@@ -340,8 +466,11 @@ class AttentionTrainStep:
             ev_enc = torch.cuda.Event()
             ev_enc.record(self.s_enc)
         self.replayed = [f"enc{slot}"]
+        self.counts["replay"] += 1
         loss = self._pipe_decoder()
-        self._pend = ("graph", slot, captions, caption_lengths, ev_enc, None)
+        if early is not None:
+            loss = early
+        self._pend = ("graph", st, captions, caption_lengths, ev_enc, None)
         return loss
 
     def _pipe_decoder(self):
@@ -350,14 +479,13 @@ class AttentionTrainStep:
         # dispatch on how the pending batch's encoder was launched (a ragged batch runs eagerly
         # between graph-replayed ones)
         if self._pend[0] == "graph":
-            _, pslot, _, _, ev, _ = self._pend
+            _, st, _, _, ev, _ = self._pend
             self._pend = None
             self.s_dec.wait_event(ev)
             self.s_dec.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self.s_dec):
-                st = self._pg[pslot]
                 st["g_dec"].replay()
-                self.replayed.append(f"dec{pslot}")
+                self.replayed.append(f"dec{st['slot']}")
                 if self.ctx.distributed:
                     fc_works = cdist.allreduce_mean_(self._b_fc, self.ctx, async_op=True)
                     st["g_dec2"].replay()
@@ -368,6 +496,8 @@ class AttentionTrainStep:
             return loss
         _, pslot, caps, lens, ev, dup = self._pend
         self._pend = None
+        self.counts["eager"] += 1
+        self._feats[pslot].record_stream(self.s_dec)  # a later shape may replace the slot's buffer
         self.s_dec.wait_event(ev)
         self.s_dec.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.s_dec):
@@ -385,6 +515,7 @@ class AttentionTrainStep:
         return loss
 
     def __call__(self, imgs, captions, caption_lengths):
+        self.schedule = []
         if self.pipeline:
             if self.pipe_graph and len(set(caption_lengths)) == 1:
                 return self._pg_call(imgs, captions, caption_lengths)
@@ -394,6 +525,7 @@ class AttentionTrainStep:
         return self._eager(imgs, captions, caption_lengths)
 
     def _eager(self, imgs, captions, caption_lengths):
+        self.counts["eager"] += 1
         if not self.ctx.distributed or self.fine_tune:  # fine-tune: DP exchange inside _body_ft
             return self._body(imgs, captions, caption_lengths, with_update=True)
         loss = self._body(imgs, captions, caption_lengths, with_update=False)
@@ -422,18 +554,43 @@ class AttentionTrainStep:
             # copy of the per-step batch sizes: run them eagerly
             return self._eager(imgs, captions, caption_lengths)
         key = (tuple(imgs.shape), tuple(captions.shape), tuple(caption_lengths))
-        if self._graph is None or self._static["key"] != key:
+        ent = self._gcache.get(key)
+        if ent is None:
+            if not self._cache_room(key):
+                return self._eager(imgs, captions, caption_lengths)  # cache full: this key runs eagerly
             self._capture(imgs, captions, caption_lengths, key)
+            ent = self._gcache[key] = (self._graph, self._static, self._segs)
+        self._graph, self._static, self._segs = ent
+        self.counts["replay"] += 1
         st = self._static
         if imgs.data_ptr() != st["imgs"].data_ptr():
             st["imgs"].copy_(imgs, non_blocking=True)
         if captions.data_ptr() != st["caps"].data_ptr():
             st["caps"].copy_(captions, non_blocking=True)
-        self._graph.replay()
-        self.replayed = ["step"]
-        if self.ctx.distributed:
-            cdist.allreduce_mean_(self._grad_buffers(), self.ctx)
-            self._step_all()
+        self.schedule = []
+        if self._segs is None:
+            self._graph.replay()
+            self.replayed = ["step"]
+            self.schedule.append("step")
+            return st["loss"]
+        # data parallel: the segments, each bucket's all-reduce issued as soon as the segment that
+        # finalises it has been queued (it then runs beside the next segment's replay)
+        graphs, labels = self._segs
+        works = []
+        self.replayed = []
+        for i, (g, label) in enumerate(zip(graphs, labels)):
+            g.replay()
+            self.replayed.append(f"seg{i}")
+            self.schedule.append(f"seg{i}")
+            if label is not None:
+                self._issue(label, works)
+        tail = [f"layer{self.encoder._ft().first}", "rest"] if self.fine_tune else ["dec_rest"]
+        for label in tail:
+            self._issue(label, works)
+        for w in works:
+            w.wait()
+        self._step_all()
+        self.schedule.append("update")
         return st["loss"]
 
     def _capture(self, imgs, captions, caption_lengths, key, warmup=2):
@@ -447,14 +604,31 @@ class AttentionTrainStep:
         snap = self._snapshot()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(warmup):
-                self._body(st["imgs"], st["caps"], st["lens"], with_update=False)
-        torch.cuda.current_stream().wait_stream(s)
-        self._restore(snap)
-        g = torch.cuda.CUDAGraph()
+        self._capturing = True
+        try:
+            with torch.cuda.stream(s):
+                for _ in range(warmup):
+                    self._body(st["imgs"], st["caps"], st["lens"], with_update=False)
+            torch.cuda.current_stream().wait_stream(s)
+            self._restore(snap)
+            self._capture_graphs(st, upd)
+        finally:
+            self._capturing = False
+
+    def _capture_graphs(self, st, upd):
         if self.capture_hook is not None:
             self.capture_hook("step")
-        with torch.cuda.graph(g):
-            st["loss"] = self._body(st["imgs"], st["caps"], st["lens"], with_update=upd)
+        if upd:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                st["loss"] = self._body(st["imgs"], st["caps"], st["lens"], with_update=True)
+            self._segs = None
+        else:
+            # data parallel: segments cut where buckets become final (fc / decoder, layer4, layer3, layer2)
+            st["loss"], graphs, labels = self._capture_segments(
+                lambda cut: self._body(st["imgs"], st["caps"], st["lens"], with_update=False, cut=cut))
+            g = graphs[0]
+            self._segs = (graphs, labels)
+        st["pins"] = self._pins()
+        self.counts["capture"] += 1
         self._graph, self._static = g, st

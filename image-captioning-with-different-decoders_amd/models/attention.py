@@ -7,6 +7,7 @@ Same classes, constructor arguments, sub-module attributes and state-dict keys
 compute runs on libcapmi's HIP kernels (capmi.decoder_core): forward,
 backward-through-time, fused CE + regulariser and the clamp+Adam update.
 """
+import os
 import time
 
 import torch
@@ -234,9 +235,15 @@ def train(device, args):
     # pipelined: the frozen encoder of batch k overlaps the decoder step of batch k-1
     # (bit-identical results; losses arrive one batch late and are logged in order).
     # Fine-tuning runs the sequential step (the encoder needs the previous update).
+    # On HIP graphs (the launch mode bench.py measures): each (batch, caption length) shape is
+    # captured once and replayed; ragged batches, and new shapes once CAPMI_GRAPH_CACHE shapes are
+    # held, run eagerly. CAPMI_TRAIN_GRAPH=0: every step eager.
+    on_gpu = device.type == "cuda"
     step = AttentionTrainStep(encoder, decoder, decoder_optimizer, ctx, alpha_c=args.alpha_c,
-                              pipeline=device.type == "cuda" and encoder_optimizer is None,
+                              pipeline=on_gpu and encoder_optimizer is None,
+                              graph=on_gpu and os.environ.get("CAPMI_TRAIN_GRAPH", "1") != "0",
                               encoder_optimizer=encoder_optimizer)
+    train.last_step = step  # (tests: which launch mode ran)
 
     decoder.train()
     encoder.train()

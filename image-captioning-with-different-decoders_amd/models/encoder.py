@@ -198,10 +198,11 @@ class EncoderAttention(nn.Module):
         return self._ft().forward(_ResNetView(self.resnet), imgs.contiguous(),
                                   self._out_hw() if pooled else None, out=out)
 
-    def ft_backward(self, dfeat, grads, hook=None):
+    def ft_backward(self, dfeat, grads, hook=None, on_layer=None):
         """d(loss)/d(features) (B,14,14,2048) -> parameter gradients of layer2-4 written into
-        ``grads`` (dict id(param) -> tensor)."""
-        self._ft().backward(dfeat, grads, hook=hook)
+        ``grads`` (dict id(param) -> tensor). ``on_layer(li)``: called as stage li's gradients
+        become final (layer4, layer3, layer2; capmi.resnet.FineTuneRunner.backward)."""
+        self._ft().backward(dfeat, grads, hook=hook, on_layer=on_layer)
 
     def forward_into(self, imgs, out, pooled=True):
         """forward() writing the (B,14,14,2048) features into a caller-owned buffer (the

@@ -6,8 +6,9 @@ driver's), i.e. capmi.train_step's DP logic with real HIP kernels:
     default; the all-reduce + update run after the decoder graph's replay): after the step the gradient buffer of
     every rank equals the mean of the per-shard gradients, computed in the same process by the
     non-DP fused path on each shard; parameters are identical on both ranks;
-  * encoder fine-tune (config 4): the same for the decoder AND the encoder gradient buffers
-    (decoder all-reduce issued before the encoder backward, encoder all-reduce after it).
+  * encoder fine-tune (config 4), eager and on HIP graph segments: the same for the decoder AND
+    the encoder gradient buffers (the decoder bucket all-reduced beside the encoder backward, the
+    layer4 / layer3 / layer2 buckets each as the backward leaves that stage).
 
 Equality is to fp32 summation order (rtol 1e-6 relative to max|g|): the only difference is
 (g0 + g1) / 2 vs the gloo SUM-then-scale."""
@@ -122,10 +123,14 @@ def _worker(rank, world, port, fine_tune, q, graph=False, backend="gloo"):
             want_e = sum(ref_e) / world
             err_e = float((got_e - want_e).abs().max() / want_e.abs().max())
         p = torch.cat([q.detach().reshape(-1) for q in dec.parameters()]).cpu()
-        q.put((rank, err_d, err_e, p))
+        if fine_tune:
+            p = torch.cat([p, torch.cat([q.detach().reshape(-1) for q in enc.parameters()]).cpu()])
+        import hashlib
+        digest = hashlib.sha256(p.numpy().tobytes()).hexdigest()  # (a 170 MB tensor does not cross the queue)
+        q.put((rank, err_d, err_e, digest, list(step.schedule)))
     except Exception as e:  # noqa: BLE001
         import traceback
-        q.put((rank, "error", traceback.format_exc(), None))
+        q.put((rank, "error", traceback.format_exc(), None, None))
         raise e
     finally:
         import torch.distributed as dist
@@ -133,7 +138,7 @@ def _worker(rank, world, port, fine_tune, q, graph=False, backend="gloo"):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fine_tune,graph", [(False, False), (False, True), (True, False)])
+@pytest.mark.parametrize("fine_tune,graph", [(False, False), (False, True), (True, False), (True, True)])
 def test_dp_two_ranks_one_gpu(fine_tune, graph):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -152,16 +157,26 @@ def test_dp_two_ranks_one_gpu(fine_tune, graph):
     for r in (0, 1):
         assert res[r][1] < 1e-6, ("decoder grads", res[r][1])
         assert res[r][2] < 1e-6, ("encoder grads", res[r][2])
-    assert torch.equal(res[0][3], res[1][3])  # identical parameters after the update
+    assert res[0][3] == res[1][3]  # identical parameters after the update (sha256 of every parameter)
 
 
-@pytest.mark.parametrize("fine_tune,graph", [(False, False), (False, True), (True, False)])
+# what a fine-tune step issues, in order: the graph segments (cut where a bucket becomes final) with each
+# bucket's all-reduce issued between the segment that finalises it and the next one's replay; eager: the
+# same collectives in the same order, issued from inside the backward
+_FT_GRAPH_SCHEDULE = ["seg0", "ar:dec", "seg1", "ar:layer4", "seg2", "ar:layer3", "seg3", "ar:layer2", "ar:rest",
+                      "update"]
+_FT_EAGER_SCHEDULE = ["ar:dec", "ar:layer4", "ar:layer3", "ar:layer2", "ar:rest", "update"]
+
+
+@pytest.mark.parametrize("fine_tune,graph", [(False, False), (False, True), (True, False), (True, True)])
 def test_dp_rccl_one_rank(fine_tune, graph):
     """The RCCL ("nccl" backend) branch of capmi.dist -- init_process_group(device_id=...), the
     async ReduceOp.AVG all-reduce of the flat buffers (the fc bucket beside the BPTT loop, the rest
-    after; in fine-tune the decoder's beside the encoder backward) -- at world size 1
-    (CAPMI_DIST_FORCE=1; RCCL refuses two ranks on one GPU). AVG over one rank is the identity, so
-    the gradient buffers must equal the non-DP ones bit for bit."""
+    after; in fine-tune the decoder's beside the encoder backward and the encoder's per stage) -- at
+    world size 1 (CAPMI_DIST_FORCE=1; RCCL refuses two ranks on one GPU). AVG over one rank is the
+    identity, so the gradient buffers must equal the non-DP ones bit for bit -- for the segmented
+    fine-tune graph too, i.e. cutting the step into segments changes nothing -- and the fine-tune step
+    must issue its collectives between the segments that finalise their buckets."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_worker, args=(0, 1, _free_port(), fine_tune, q, graph, "nccl"))
@@ -171,6 +186,8 @@ def test_dp_rccl_one_rank(fine_tune, graph):
     assert r[1] != "error", r[2]
     assert r[1] == 0.0, ("decoder grads", r[1])
     assert r[2] == 0.0, ("encoder grads", r[2])
+    if fine_tune:
+        assert r[4] == (_FT_GRAPH_SCHEDULE if graph else _FT_EAGER_SCHEDULE), r[4]
 
 
 @pytest.mark.parametrize("captured", [False, True])
@@ -226,3 +243,58 @@ def test_fc_bucket_cut_is_race_free(captured):
         assert bool((h == sentinel).all()), "the backward after the cut touched the fc bucket"
     for r, w in zip(rest, want):
         assert torch.equal(r, w)
+
+
+@pytest.mark.parametrize("captured", [False, True])
+def test_encoder_stage_buckets_cut_is_race_free(captured):
+    """The fine-tune step all-reduces each encoder stage's gradient bucket (layer4, then layer3, then layer2)
+    while the backward of the lower stages continues (eager: FineTuneRunner.backward's on_layer callback;
+    graph mode: segments cut there). Race-free only if nothing launched after a stage's callback reads or
+    writes that stage's bucket. Proof on one GPU: at each callback the stage's span is first copied, then
+    overwritten whole (padding included) with a sentinel. Every copy must equal the reference gradients bit
+    for bit (a lower stage that read a higher stage's bucket would see the sentinel), and after the whole
+    backward (eager, or the remaining segments' replays) every sentinel must be intact."""
+    from capmi.train_step import AttentionTrainStep
+    from helpers import t
+    import gen
+    enc, dec, dopt, eopt = _setup(True)
+    buckets = AttentionTrainStep._stage_buckets(enc, eopt)
+    assert all(buckets[f"layer{li}"] for li in (2, 3, 4))
+    imgs = t(gen.images(13, 2, 64, 64), "cuda")
+    feats = enc.ft_forward(imgs)
+    dfeat = torch.rand(feats.shape, device="cuda", generator=torch.Generator(device="cuda").manual_seed(4)) - 0.5
+    grads = {id(q): q.grad for q in enc.parameters() if q.requires_grad}
+    sentinel = 4321.0
+    enc.ft_backward(dfeat, grads)  # (also records the weight-prep jobs: later passes allocate nothing new)
+    torch.cuda.synchronize()
+    want = {li: [v.clone() for v in buckets[f"layer{li}"]] for li in (2, 3, 4)}
+    snap, order = {}, []
+
+    def hand_over(li):
+        order.append(li)
+        snap[li] = [v.clone() for v in buckets[f"layer{li}"]]
+        for v in buckets[f"layer{li}"]:
+            v.fill_(sentinel)
+
+    for g_ in eopt.grad_buffers():
+        g_.zero_()
+    if not captured:
+        enc.ft_forward(imgs)
+        enc.ft_backward(dfeat, grads, on_layer=hand_over)
+    else:
+        def body(cut):
+            enc.ft_forward(imgs)
+            enc.ft_backward(dfeat, grads, on_layer=lambda li: cut(li) if li != 2 else None)
+        _, graphs, labels = AttentionTrainStep._capture_segments(body)
+        assert labels == [4, 3, None], labels
+        for g_ in eopt.grad_buffers():
+            g_.zero_()
+        for g, lab in zip(graphs, labels):
+            g.replay()
+            hand_over(lab if lab is not None else 2)
+    torch.cuda.synchronize()
+    assert order == [4, 3, 2], order
+    for li in (2, 3, 4):
+        for v, c, w in zip(buckets[f"layer{li}"], snap[li], want[li]):
+            assert torch.equal(c, w), f"layer{li}'s gradients differ once the higher stages' buckets are handed over"
+            assert bool((v == sentinel).all()), f"the backward after layer{li}'s callback touched its bucket"

@@ -187,3 +187,72 @@ def test_pipelined_inputs_freed_and_reallocated():
         np.testing.assert_array_equal(np.array(lp), np.array(le), err_msg=mode)
         for n in pe:
             assert torch.equal(pe[n], pp[n]), (mode, n)
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_graph_cache_over_mixed_shapes_equals_eager(pipeline):
+    """Per-shape graph cache: batches of three shapes (image side 64 / 96, caption length 7 / 9) in an
+    interleaved order are each captured once and replayed from then on -- every replay running on the
+    workspaces its own capture pinned, although later shapes replace the workspace caches -- and a cache of
+    two shapes runs the third shape eagerly. Losses, decoder parameters and BN running statistics equal the
+    eager sequential step's bit for bit."""
+    B, V = 4, 50
+    shapes = [(64, 7), (96, 7), (64, 9), (64, 7), (96, 7), (64, 9), (96, 7), (64, 7)]
+    batches = [(t(gen.images(80 + i, B, s, s), DEV), t(gen.captions(80 + i, B, L, V), DEV), L)
+               for i, (s, L) in enumerate(shapes)]
+    res = {}
+    for mode in ("eager", "graph", "graph_cap2"):
+        enc, dec, opt, Step = _setup(0.5)
+        step = Step(enc, dec, opt, alpha_c=1.0, graph=(mode != "eager"), seed=9, pipeline=pipeline and mode != "eager")
+        if mode == "graph_cap2":
+            step.graph_cache_size = 2
+        out = []
+        for im, cp, L in batches:
+            x = step(im, cp, [L] * B)
+            out.append(x.clone() if not step.pipeline else x)
+        last = step.flush()
+        torch.cuda.synchronize()
+        losses = [float(x) for x in out if x is not None] + ([float(last)] if last is not None else [])
+        res[mode] = (losses, {n: q.detach().clone() for n, q in dec.named_parameters()},
+                     {k: v.clone() for k, v in enc.state_dict().items() if "running" in k or "num_batches" in k},
+                     dict(step.counts))
+    le, pe, re_, _ = res["eager"]
+    assert len(le) == len(batches)
+    for mode, (cap, rep) in (("graph", (3, 8)), ("graph_cap2", (2, 6))):
+        lg, pg, rg, cnt = res[mode]
+        assert cnt["capture"] == cap and cnt["replay"] == rep, (mode, cnt)
+        np.testing.assert_array_equal(np.array(lg), np.array(le), err_msg=mode)
+        for n in pe:
+            assert torch.equal(pe[n], pg[n]), (mode, n)
+        for k in re_:
+            assert torch.equal(re_[k], rg[k]), (mode, k)
+
+
+def test_train_loop_replays_graphs_and_equals_eager(tmp_path, monkeypatch):
+    """models.attention.train() runs the launch mode bench.py measures (pipelined HIP-graph
+    replay). Over a synthetic fixed-length dataset it captures once and replays every later batch, and its
+    logged losses equal those of CAPMI_TRAIN_GRAPH=0 (eager pipelined launches) bit for bit."""
+    import types
+    import checkpoint as C
+    from models import attention as A
+    monkeypatch.setattr(C, "CHECKPOINTS_DIR", str(tmp_path / "ck"))
+    losses, counts = {}, {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CAPMI_TRAIN_GRAPH", mode)
+        torch.manual_seed(0)
+        args = types.SimpleNamespace(
+            model_name=f"syn{mode}", model="attention", attention_dim=32, decoder_dim=32, decoder_dropout=0.5,
+            embed_size=16, epochs=1, batch_size=4, workers=0, encoder_lr=1e-4, decoder_lr=1e-4, grad_clip=5.0,
+            alpha_c=1.0, fine_tune_encoder=False, fine_tune_embedding=False, checkpoint=None, print_freq=2,
+            use_glove=False, max_caption_length=-1, use_bert=False, synthetic=True, synthetic_size=20,
+            synthetic_len=9, vocab_size=50, trusted_checkpoint=False)
+        A.train(torch.device(DEV), args)
+        ck = torch.load(tmp_path / "ck" / f"syn{mode}_0.pth.tar", weights_only=True)
+        losses[mode] = ck["metrics"]["epoch_losses"][0]
+        step = A.train.last_step
+        counts[mode] = dict(step.counts)
+        assert step.pipeline and step.pipe_graph == (mode == "1")
+    assert len(losses["1"]) == 5 and all(np.isfinite(losses["1"]))
+    assert counts["1"]["capture"] == 1 and counts["1"]["replay"] == 5 and counts["1"]["eager"] == 0, counts
+    assert counts["0"]["replay"] == 0, counts
+    np.testing.assert_array_equal(np.array(losses["1"]), np.array(losses["0"]))

@@ -239,3 +239,41 @@ def test_struct_layout_matches_c_compiler(tmp_path):
     subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
     assert got == want
+
+
+def test_grad_spans_cover_the_flat_buffer():
+    """Adam.grad_spans (the DP buckets: fc beside the BPTT loop; an encoder's layer4 / layer3 / layer2 as its
+    backward leaves each stage): one contiguous view per group, each holding exactly its parameters' slots and
+    padding, the groups disjoint, and the groups plus the rest tiling the flat gradient buffer in order."""
+    import torch
+    from capmi.optim import Adam
+    from capmi.train_step import AttentionTrainStep
+    torch.manual_seed(0)
+    seq = torch.nn.Sequential(*[torch.nn.Linear(3 + i, 5) for i in range(8)])
+    for i in range(5):
+        for q in seq[i].parameters():
+            q.requires_grad = False
+    opt = Adam([q for q in seq.parameters() if q.requires_grad], lr=1e-3)
+    gf = opt.grad_buffers()[0]
+    spans = opt.grad_spans([set(seq[7].parameters()), set(seq[5].parameters())])
+    assert len(spans) == 3 and all(len(s) == 1 for s in spans[:2])
+    for grp, (view,) in zip((seq[7], seq[5]), spans[:2]):
+        for q in grp.parameters():
+            assert q.grad.data_ptr() >= view.data_ptr()
+            assert q.grad.data_ptr() + q.numel() * 4 <= view.data_ptr() + view.numel() * 4
+    pieces = sorted([v for s in spans for v in s], key=lambda v: v.data_ptr())
+    pos = gf.data_ptr()
+    for v in pieces:
+        assert v.data_ptr() == pos
+        pos += v.numel() * 4
+    assert pos == gf.data_ptr() + gf.numel() * 4
+    head, rest = opt.grad_buckets(set(seq[6].parameters()))
+    assert len(head) == 1 and len(rest) == 2
+    # the train step's per-stage encoder buckets: children 5, 6, 7 = layer2, layer3, layer4
+    enc = type("E", (), {"resnet": seq})()
+    b = AttentionTrainStep._stage_buckets(enc, opt)
+    assert [v.data_ptr() for v in b["layer4"]] == [spans[0][0].data_ptr()]
+    assert [v.data_ptr() for v in b["layer2"]] == [spans[1][0].data_ptr()]
+    assert b["rest"] == []
+    with pytest.raises(ValueError):
+        opt.grad_spans([set(seq[5].parameters()) | set(seq[7].parameters())])  # not contiguous
