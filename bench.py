@@ -134,14 +134,22 @@ class ConvTimer:
     def __init__(self):
         self.events = []  # (kernel key, flops, start event, end event)
         self.enabled = False
+        self.checked = 0
+        self.mismatch = set()  # (priced key, launched instantiation) pairs that differ
 
     def __call__(self, tag, flops, launch, key):
         if not self.enabled or torch.cuda.is_current_stream_capturing():
             launch()
             return
-        from capmi.kernels import TimingEvent, timed_launch
+        from capmi.kernels import TimingEvent, last_launch_name, timed_launch
         s, e = TimingEvent(), TimingEvent()
         timed_launch(launch, s, e)
+        # the name this launch is priced under (the planner's plan query) against the instantiation the launcher
+        # actually ran (capmi_last_launch_name): roofline.kernel / traffic attribution cannot drift from the planner
+        self.checked += 1
+        got = last_launch_name()
+        if got != key:
+            self.mismatch.add((key, got))
         self.events.append((key, flops, s, e))
 
     def result(self):
@@ -503,6 +511,8 @@ def main():
                                 "conv_ms_per_step": round(fam_ms / args.steps, 3),
                                 "conv_gflop_per_image": round(per_img / 1e9, 3)},
                 "timing": timing,
+                "kernel_names": {"launches_checked": timer.checked,
+                                 "priced_vs_launched_mismatches": sorted(f"{a} != {b}" for a, b in timer.mismatch)},
                 # which pass gives achieved / frac: the serialized one (encoder and decoder on one
                 # stream, as the rocprofv3 kernel trace runs the bench) unless the steps themselves were eager;
                 # in_pipeline below is the same kernel with the decoder stream beside it
@@ -554,6 +564,9 @@ def main():
             "loss_last_step": round(loss_v, 5),
             "launch": ("pipelined_2stream_eager" if args.eager else "pipelined_2stream_hip_graphs") if pipe
             else ("eager" if args.eager else "hip_graph"),
+            # models.attention.train() builds the same step: pipelined (frozen encoder) or sequential (fine-tune),
+            # replaying per-shape HIP graphs (CAPMI_TRAIN_GRAPH=0: eager)
+            "launch_is_train_default": not args.eager and pipe == (not ft),
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -23,7 +23,7 @@ CAPMI_B_NMAJOR_W, CAPMI_B_KROWS, CAPMI_B_CONV_NHWC = 0, 1, 2
 CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO, CAPMI_TILE_128_W8 = 0, 1, 2, 3, 4
 CAPMI_MAX_GROUP = 4
 CAPMI_COLSUM_GROUPS = 64
-ABI_VERSION = 24
+ABI_VERSION = 25
 CAPMI_BNB_RELU_Y, CAPMI_BNB_RELU_OUT = 0, 1
 CAPMI_BNB_MAX_SLABS = 256
 CAPMI_GEMM_BF16 = 1
@@ -87,6 +87,7 @@ _SIGS = {
     "capmi_gemm_ex": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_int, c_int, c_vp],
     "capmi_gemm_sk_ex": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_int, c_vp, c_ll, c_vp],
     "capmi_gemm_sk_plan": [ctypes.POINTER(GemmProblem), c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "capmi_last_launch_name": [ctypes.c_char_p, c_int],
     "capmi_splitk_reduce": [c_vp, c_int, c_ll, c_int, c_int, c_ll, c_vp, c_vp, c_ll, c_vp],
     "capmi_colsum": [c_vp, c_int, c_int, c_ll, c_float, c_vp, c_vp, c_int, c_vp],
     "capmi_conv_weight_pack": [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp],

@@ -277,6 +277,22 @@ def gemm_x3_kernel_name(prob, amode, tile=CAPMI_TILE_AUTO):
     return f"gemm_x3_kernel<{v[1].value}, {amode}, {b(bool(prob.in_scale))}, {b(v[2].value)}>"
 
 
+def gemm_bf16_kernel_name(prob, amode, tile=CAPMI_TILE_AUTO):
+    """The instantiation gemm_bf16(prob, amode, workspace, tile) launches (capmi_gemm_sk_plan with
+    CAPMI_GEMM_BF16_IO: the launcher's own plan, gemm.hip bf16_io_plan)."""
+    v = [ctypes.c_int(0) for _ in range(5)]
+    call("capmi_gemm_sk_plan", ctypes.byref(prob), amode, CAPMI_B_NMAJOR_W, tile, CAPMI_GEMM_BF16_IO,
+         *[ctypes.byref(x) for x in v])
+    return f"gemm_bf16_kernel<128, {v[1].value}, {amode}, {'true' if v[2].value else 'false'}, {v[3].value}>"
+
+
+def last_launch_name():
+    """The demangled instantiation of the last GEMM kernel launched on this thread (capmi_last_launch_name)."""
+    buf = ctypes.create_string_buffer(512)
+    call("capmi_last_launch_name", buf, 512)
+    return buf.value.decode()
+
+
 def gemm_sk_plan(prob, amode, tile=CAPMI_TILE_AUTO, bmode=CAPMI_B_NMAJOR_W, bf16=False, threads=False,
                  flags=None):
     """(bm, bn, stream_k, generic[, threads]) of the launch gemm_sk would make for ``prob``."""

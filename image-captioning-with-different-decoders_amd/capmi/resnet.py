@@ -415,18 +415,7 @@ class EncoderRunner:
             prob, mode = K.problem_bf16(rows, co, Kd, x, 0, w, Kd, out, co, stats=stats, conv=geo), AC
         launch = lambda: K.gemm_bf16(prob, mode, self._ws["sk"], K.TILE_AUTO)  # noqa: E731
         if self.conv_hook is not None:
-            # the launch capmi_gemm_sk_ex makes for CAPMI_GEMM_BF16_IO (gemm.hip: gemm_bf16_io)
-            # (round 5: K <= 256 takes the one-stage 128x64 form, data-parallel)
-            st1 = Kd <= 256
-            cus = torch.cuda.get_device_properties(x.device).multi_processor_count
-            narrow = 2 * -(-rows // 128) * -(-co // 128) <= cus  # (gemm.hip: 128x64 on grids under half the CUs)
-            bn_ = 64 if co <= 64 or st1 or narrow else 128
-            tiles = -(-rows // 128) * -(-co // bn_)
-            slots = 2 * torch.cuda.get_device_properties(x.device).multi_processor_count
-            rounds = -(-tiles // slots)
-            sk = (not st1 and os.environ.get("CAPMI_BF16_SK", "0") == "1" and os.environ.get("CAPMI_SK_OFF", "0") != "1"
-                  and Kd // 64 >= 4 and tiles / (rounds * slots) < 0.9)  # (gemm.hip gemm_bf16_io)
-            key = f"gemm_bf16_kernel<128, {bn_}, {mode}, {'true' if sk else 'false'}, {1 if st1 else 2}>"
+            key = K.gemm_bf16_kernel_name(prob, mode)  # the launcher's own plan (gemm.hip bf16_io_plan)
             self.conv_hook(tag, 2.0 * rows * co * Kd, launch, key)
         else:
             launch()

@@ -27,8 +27,12 @@ struct CapmiArmedEvents {
   hipEvent_t start, stop;
 };
 extern thread_local CapmiArmedEvents g_capmi_armed;
+// the last kernel CAPMI_KLAUNCH launched on this host thread (capmi_last_launch_name: the instantiation a plan
+// query names must be the one launched -- tests/test_gpu_plan_names.py)
+extern thread_local const void* g_capmi_last_kernel;
 #define CAPMI_KLAUNCH(kernel, grid, block, shmem, stream, ...)                                          \
   do {                                                                                                 \
+    g_capmi_last_kernel = reinterpret_cast<const void*>(kernel);                                       \
     if (g_capmi_armed.start != nullptr) {                                                              \
       const CapmiArmedEvents ev__ = g_capmi_armed;                                                     \
       g_capmi_armed = CapmiArmedEvents{nullptr, nullptr};                                              \

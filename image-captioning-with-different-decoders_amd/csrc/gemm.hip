@@ -692,6 +692,38 @@ int x3s_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long& ld
 int x3c_plan(const capmi_gemm_problem* prob, int amode, int bmode, int& tiles);
 int x3w_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long ws_floats, GemmArgs& a, int& S,
              long long& tiles);
+// CAPMI_GEMM_BF16_IO's launch plan (shared by the launcher and capmi_gemm_sk_plan): the column tile bn (BM = 128),
+// the LDS stages (1: the one-stage short-k form, 2) and stream-K
+struct Bf16Plan {
+  int bn, stages;
+  bool sk;
+  long long total;
+};
+Bf16Plan bf16_io_plan(const capmi_gemm_problem& p, int tile, bool have_ws) {
+  // AUTO on a short k (K <= 256: the bf16 config's 1x1 c3 convs and layer1's K = 64 convs): 128x64 tiles, one LDS
+  // stage, four workgroups per CU, data-parallel (round 5: l3 c3 20.0 -> 17.1 us, l2 c3 24.7 -> 18.4, l1 c3 33.3 ->
+  // 24.3; at K = 512 a tie and above it slower: the two-stage 128x128 form stays)
+  const bool st1 = tile == CAPMI_TILE_AUTO && p.K <= 256;
+  // AUTO on a grid of 128x128 tiles that fills at most half the CUs (layer4's 3136-row convs: 100 tiles):
+  // 128x64 tiles, twice the workgroups (round 5: l4 3x3 53.2 -> 40.8 us, l4 c1 25.8 -> 18.9; the 400-tile
+  // layer4 c3 / downsample and layer3's 196-tile grids stay at 128x128, where 128x64 measured slower)
+  const bool narrow = tile == CAPMI_TILE_AUTO && 2 * cdiv(p.M, 128) * cdiv(p.N, 128) <= cu_count();
+  Bf16Plan r;
+  r.bn = (st1 || narrow || tile == CAPMI_TILE_128x64 || tile == CAPMI_TILE_64 || (tile == CAPMI_TILE_AUTO && p.N <= 64))
+             ? 64 : 128;
+  r.total = cdiv(p.M, 128) * cdiv(p.N, r.bn);
+  const long long slots = (long long)sk_cus() * 2;
+  const long long rounds = (r.total + slots - 1) / slots;
+  // (round 3) stream-K for the bf16 convs only on CAPMI_BF16_SK=1: data-parallel grids measured faster in the
+  // pipelined bf16 step (config 5; DESIGN 4.11c)
+  static const bool bf16_sk = [] {
+    const char* e = getenv("CAPMI_BF16_SK");
+    return e && e[0] == '1';
+  }();
+  r.sk = !st1 && bf16_sk && !sk_off() && have_ws && p.K / 64 >= 4 && (double)r.total / (double)(rounds * slots) < 0.9;
+  r.stages = st1 ? 1 : 2;
+  return r;
+}
 }  // namespace
 
 extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int bmode, int tile, int flags,
@@ -773,6 +805,18 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
     if (generic) *generic = 0;
     return 0;
   }
+  if (flags == CAPMI_GEMM_BF16_IO) {  // (the launcher's own plan; stream-K assumes a workspace is passed)
+    CAPMI_REQUIRE(prob != nullptr && bmode == CAPMI_B_NMAJOR_W &&
+                      (amode == CAPMI_A_KMAJOR || amode == CAPMI_A_CONV_NHWC) && prob->K > 0 && prob->K % 64 == 0,
+                  CAPMI_EINVAL);
+    const Bf16Plan pl = bf16_io_plan(*prob, tile, true);
+    if (threads) *threads = 256;
+    if (bm) *bm = 128;
+    if (bn) *bn = pl.bn;
+    if (stream_k) *stream_k = pl.sk ? 1 : 0;
+    if (generic) *generic = pl.stages;  // CAPMI_GEMM_BF16_IO: the LDS stages (1: the one-stage short-k form)
+    return 0;
+  }
   int terms = flag_terms(flags);
   CAPMI_REQUIRE(terms >= 0 && terms_mode_ok(terms, amode, bmode), CAPMI_EINVAL);
   int rc = sk_decide(prob, amode, bmode, tile, terms, g, sk);
@@ -812,17 +856,8 @@ int gemm_bf16_io(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
     CAPMI_REQUIRE((long long)p.M * p.lda * 2 < (1LL << 31), CAPMI_ERANGE);
   }
   if (p.M == 0) return 0;
-  // AUTO on a short k (K <= 256: the bf16 config's 1x1 c3 convs and layer1's K = 64 convs): 128x64 tiles, one LDS
-  // stage, four workgroups per CU, data-parallel (round 5: l3 c3 20.0 -> 17.1 us, l2 c3 24.7 -> 18.4, l1 c3 33.3 ->
-  // 24.3; at K = 512 a tie and above it slower: the two-stage 128x128 form stays)
-  const bool st1 = tile == CAPMI_TILE_AUTO && p.K <= 256;
-  // AUTO on a grid of 128x128 tiles that fills at most half the CUs (layer4's 3136-row convs: 100 tiles):
-  // 128x64 tiles, twice the workgroups (round 5: l4 3x3 53.2 -> 40.8 us, l4 c1 25.8 -> 18.9; the 400-tile
-  // layer4 c3 / downsample and layer3's 196-tile grids stay at 128x128, where 128x64 measured slower)
-  const bool narrow = tile == CAPMI_TILE_AUTO && 2 * cdiv(p.M, 128) * cdiv(p.N, 128) <= cu_count();
-  const int bm = 128,
-            bn = (st1 || narrow || tile == CAPMI_TILE_128x64 || tile == CAPMI_TILE_64 ||
-                  (tile == CAPMI_TILE_AUTO && p.N <= 64)) ? 64 : 128;
+  const Bf16Plan pl = bf16_io_plan(p, tile, workspace != nullptr);
+  const int bm = 128, bn = pl.bn;
   GemmArgs a;
   memset(&a, 0, sizeof(a));
   a.nprob = 1;
@@ -831,22 +866,12 @@ int gemm_bf16_io(const capmi_gemm_problem* prob, int amode, int bmode, int tile,
   a.tiles_n[0] = (int)cdiv(p.N, bn);
   a.plain_epi = plain_epilogue(p, bn);  // (bf16 C: the fp32 bound on M * ldc is the stricter one)
   if (p.ldc % 8 != 0 || !aligned16(p.C)) a.plain_epi = 0;  // (its 16-B row-chunk stores)
-  const long long total = (long long)a.tiles_m[0] * a.tiles_n[0];
+  const long long total = pl.total;
   a.tiles_begin[1] = (int)total;
   const int cus = cu_count();
   const long long slots = (long long)sk_cus() * 2;
   const int nkt = p.K / 64;
-  const long long rounds = (total + slots - 1) / slots;
-  // (round 3) stream-K for the bf16 convs only on CAPMI_BF16_SK=1: data-parallel grids measured faster in the
-  // pipelined bf16 step (config 5; DESIGN 4.11c)
-  static const bool bf16_sk = [] {
-    const char* e = getenv("CAPMI_BF16_SK");
-    return e && e[0] == '1';
-  }();
-  const bool sk = bf16_sk && !sk_off() && workspace != nullptr && nkt >= 4 &&
-                  (double)total / (double)(rounds * slots) < 0.9;
-  if (st1) return gemm_bf16_launch(a, amode, bm, bn, (int)total, s, 1);
-  if (!sk) return gemm_bf16_launch(a, amode, bm, bn, (int)total, s, 2);
+  if (!pl.sk) return gemm_bf16_launch(a, amode, bm, bn, (int)total, s, pl.stages);
   CAPMI_REQUIRE(aligned16(workspace), CAPMI_EINVAL);
   CAPMI_REQUIRE(ws_bytes >= capmi_gemm_workspace_bytes(), CAPMI_ERANGE);
   a.sk_nkt = nkt;

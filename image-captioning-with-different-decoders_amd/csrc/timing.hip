@@ -1,12 +1,58 @@
 // Kernel timing inside HIP graphs (bench.py's roofline): timing events whose records become
 // graph nodes when the stream is being captured (hipEventRecordExternal), so the duration of a
 // single kernel can be read after each replay of a captured step. Host-side only; no kernels.
+#include <cxxabi.h>
+#include <dlfcn.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <string>
+
 #include "common.h"
 
 // 0: hipEventRecordWithFlags(External) first; 1: it was refused once, go straight to the node
 static int g_record_mode = 0;
 
 thread_local CapmiArmedEvents g_capmi_armed = {nullptr, nullptr};
+thread_local const void* g_capmi_last_kernel = nullptr;
+
+// the demangled instantiation of the last GEMM kernel this host thread launched through CAPMI_KLAUNCH, as
+// rocprofv3 prints it without the return type and parameter list ("gemm_bf16_kernel<128, 64, 2, false, 2>")
+extern "C" int capmi_last_launch_name(char* out, int n) {
+  CAPMI_REQUIRE(out != nullptr && n > 0, CAPMI_EINVAL);
+  out[0] = 0;
+  CAPMI_REQUIRE(g_capmi_last_kernel != nullptr, CAPMI_EINVAL);
+  // the kernel's host stub is a weak, default-visibility symbol named as the kernel: dladdr names it without the
+  // runtime; the HIP runtime's own registry is the fallback
+  const char* raw = nullptr;
+  Dl_info info;
+  if (dladdr(g_capmi_last_kernel, &info) != 0 && info.dli_sname != nullptr && info.dli_saddr == g_capmi_last_kernel)
+    raw = info.dli_sname;
+  hipFunction_t fn = nullptr;
+  if ((raw == nullptr || raw[0] == 0) && hipGetFuncBySymbol(&fn, g_capmi_last_kernel) == hipSuccess && fn != nullptr)
+    raw = hipKernelNameRef(fn);
+  if (raw == nullptr || raw[0] == 0) raw = hipKernelNameRefByPtr(g_capmi_last_kernel, nullptr);
+  CAPMI_REQUIRE(raw != nullptr && raw[0] != 0, CAPMI_EINVAL);
+  int st = -1;
+  char* dem = (raw[0] == '_' && raw[1] == 'Z') ? abi::__cxa_demangle(raw, nullptr, nullptr, &st) : nullptr;
+  std::string name = (dem && st == 0) ? std::string(dem) : std::string(raw);
+  free(dem);
+  if (name.compare(0, 5, "void ") == 0) name = name.substr(5);
+  static const std::string anon = "(anonymous namespace)::";
+  if (name.compare(0, anon.size(), anon) == 0) name = name.substr(anon.size());
+  // drop the parameter list: the '(' that closes the template argument list's nesting level 0
+  int depth = 0;
+  for (size_t i = 0; i < name.size(); ++i) {
+    if (name[i] == '<') ++depth;
+    else if (name[i] == '>') --depth;
+    else if (name[i] == '(' && depth == 0) {
+      name.resize(i);
+      break;
+    }
+  }
+  snprintf(out, (size_t)n, "%s", name.c_str());
+  return 0;
+}
 
 // the next GEMM launch of this host thread records its dispatch start / end into (start, stop)
 // (CAPMI_KLAUNCH, common.h); eager launches only (a stream under capture refuses it)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 24
+#define CAPMI_ABI_VERSION 25
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -188,6 +188,11 @@ int capmi_gemm_sk_ex(const capmi_gemm_problem* problem, int amode, int bmode, in
  * time. Any out pointer may be NULL. */
 int capmi_gemm_sk_plan(const capmi_gemm_problem* problem, int amode, int bmode, int tile, int flags, int* bm,
                        int* bn, int* stream_k, int* generic, int* threads);
+/* (ABI 25) for CAPMI_GEMM_BF16_IO the plan is the launcher's own (generic = the LDS stages, 1 or 2; stream_k as
+ * if a workspace were passed). The name of the last GEMM kernel instantiation this host thread launched (demangled,
+ * without return type and parameters, as rocprofv3 lists it) into out[n]: what a plan query's name must equal.
+ * Needs the HIP runtime's code-object registry (a GPU process). */
+int capmi_last_launch_name(char* out, int n);
 
 /* sum of S partial slabs: out[r][c] = sum_s in[s*slab + r*ld_in + c] (+ bias[c]); rows x cols */
 int capmi_splitk_reduce(const float* in, int S, long long slab, int rows, int cols, long long ld_in,

@@ -158,6 +158,30 @@ def test_gemm_sk_plan_on_host():
     assert x3c_plan(64, 1, 32)[0] == 1001  # eight 1-row images per tile: 24 padded rows x 34 > 640 positions
     assert x3c_plan(4, 56, 56, Cin=48)[0] == 1001  # Cin % 32 != 0
 
+    def bf16_plan(M, N, K, conv=None):
+        # CAPMI_GEMM_BF16_IO (2, ABI 25): the launcher's own plan (gemm.hip bf16_io_plan)
+        p = GemmProblem()
+        p.M, p.N, p.K, p.ksplit = M, N, K, 1
+        p.A = p.B = p.C = 256
+        p.lda, p.ldb, p.ldc, p.alpha = K, K, N, 1.0
+        amode = 0
+        if conv is not None:
+            n, h, cin, k, s = conv
+            p.cN, p.cH, p.cW, p.cCin, p.cKH, p.cKW = n, h, h, cin, k, k
+            p.cStride, p.cPad, p.cHo, p.cWo = s, k // 2, h // s, h // s
+            amode = 2
+        v = [c_int(0) for _ in range(5)]
+        rc = lib.capmi_gemm_sk_plan(ctypes.byref(p), amode, 0, 3, 2, *[ctypes.byref(x) for x in v])
+        return rc, tuple(x.value for x in v)
+
+    # config 5 at batch 64: layer3's 1x1 c3 (K = 256) takes the one-stage 128x64 form; layer3's 3x3 (196 tiles of
+    # 128x128) the two-stage 128x128; layer4's 3x3 (100 tiles: at most half of the 256 CUs) 128x64, two stages
+    rc, (bm, bn, sk, stages, nt) = bf16_plan(12544, 1024, 256)
+    assert rc == 0 and (bm, bn, sk, stages, nt) == (128, 64, 0, 1, 256)
+    assert bf16_plan(12544, 256, 2304, conv=(64, 14, 256, 3, 1))[1][:4] == (128, 128, 0, 2)
+    assert bf16_plan(3136, 512, 4608, conv=(64, 7, 512, 3, 1))[1][:4] == (128, 64, 0, 2)
+    assert bf16_plan(3136, 512, 100)[0] == 1001  # K % 64 != 0
+
 
 def test_device_tensors_required():
     from capmi import kernels as K
