@@ -482,7 +482,10 @@ gemm_x3_kernel(const GemmArgs args) {
   }
 
   // stream-K over (tile, k-tile) units with XCD groups and the hybrid schedule: gemm_nt.hip's
-  // hand-off protocol (sc1 write-through parking, drained, agent-scope flag; sc1 loads)
+  // hand-off protocol (sc1 write-through parking, drained, agent-scope flag; sc1 loads). The sc1 form
+  // without fences (gemm_args.h) needs one workgroup per CU: the BN = 64 tile (72 KB of LDS, <= 168
+  // VGPRs) fits two per CU, so it keeps the agent-scope release / acquire
+  constexpr bool kFencedX = kSkFenced1 || BN == 64;
   const capmi_gemm_problem& P = args.p[0];
   const int nkt = args.sk_nkt, tiles_n = args.tiles_n[0];
   const long long ngrp = args.sk_groups, grp = blockIdx.x % ngrp;
@@ -529,13 +532,13 @@ gemm_x3_kernel(const GemmArgs args) {
           __builtin_amdgcn_raw_buffer_store_b128(v, rs, ((j * 4 + q) * XNT + tid) * 16, 0, kSc1x);
         }
       }
-      sk_publish<kSkFenced1>(flags + blockIdx.x, tid);
+      sk_publish<kFencedX>(flags + blockIdx.x, tid);
       continue;
     }
     if (ks > 0) {
       for (long long w2 = w - 1;; --w2) {
         const long long b2 = w2 * ngrp + grp;
-        sk_consume<kSkFenced1>(flags + b2, flags + gridDim.x, tid);
+        sk_consume<kFencedX>(flags + b2, flags + gridDim.x, tid);
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(args.sk_part + b2 * PART, 0, PART * 4, 0x00020000);
         if constexpr (X3_M16) {
 #pragma unroll

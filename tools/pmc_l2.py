@@ -1,4 +1,4 @@
-"""L2 hit rate and memory-side reads per conv GEMM launch from the tools/r05_probe25.sh passes
+"""L2 hit rate and memory-side reads per conv GEMM launch from the tools/pmc_l2.sh passes
 (gpurun_out/l2/<case>/.../*.db: TCC_HIT_sum, TCC_MISS_sum, TCC_EA0_RDREQ_sum). Memory-side read bytes =
 TCC_EA0_RDREQ x 64 B x 2 (MI355X_MICROARCH.md: on gfx950 each 128-B request of a wide read is tallied at 64 B)."""
 import glob
