@@ -141,3 +141,41 @@ def test_bf16_elementwise():
         K.adaptive_avgpool_bf16(m.to(DEV), 2, Hh, Hh, 64, O, O, o)
         want = F.adaptive_avg_pool2d(m.float().permute(0, 3, 1, 2), (O, O)).permute(0, 2, 3, 1)
         torch.testing.assert_close(o.cpu(), want, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("H,Cin,Cout,k,s,name", [
+    (7, 512, 512, 3, 1, "gemm_bf16_kernel<128, 64, 2, false, 2>"),    # layer4 3x3: 100 tiles of 128x128, K = 4608
+    (14, 512, 512, 3, 2, "gemm_bf16_kernel<128, 64, 2, false, 2>"),   # layer4.0's stride-2 3x3
+    (7, 2048, 512, 1, 1, "gemm_bf16_kernel<128, 64, 0, false, 2>"),   # layer4 c1 (K = 2048, dense rows)
+])
+def test_bf16io_layer4_exact_shapes(H, Cin, Cout, k, s, name):
+    """layer4's convs at batch 64 run the 128x64 two-stage form on grids of 128x128 tiles that fill
+    at most half the CUs (round 5, gemm.hip bf16_io_plan) -- checked element-wise at their exact shapes, the
+    instantiation asserted through the launcher's own plan. fp64 reference on the device (im2col + GEMM)."""
+    from capmi import kernels as K
+    from capmi._lib import CAPMI_A_CONV_NHWC, CAPMI_A_KMAJOR
+    N, pad = 64, k // 2
+    Ho = (H + 2 * pad - k) // s + 1
+    x = _rand((N, H, H, Cin), 31, 2.0).to(DEV)
+    w = _rand((Cout, k, k, Cin), 32, 0.05).to(DEV).contiguous()
+    rows, Kd = N * Ho * Ho, k * k * Cin
+    out = torch.full((N, Ho, Ho, Cout), float("nan"), device=DEV, dtype=BF)
+    stats = torch.empty(K.stat_tiles(rows) * Cout * 2, device=DEV)
+    geo = dict(N=N, H=H, W=H, Cin=Cin, KH=k, KW=k, stride=s, pad=pad, Ho=Ho, Wo=Ho)
+    if k == 1 and s == 1:  # the runner's 1x1 form: dense rows (capmi.resnet.EncoderRunner._conv_bf16)
+        prob, mode = K.problem_bf16(rows, Cout, Kd, x, Cin, w, Kd, out, Cout, stats=stats), CAPMI_A_KMAJOR
+    else:
+        prob, mode = K.problem_bf16(rows, Cout, Kd, x, 0, w, Kd, out, Cout, stats=stats, conv=geo), CAPMI_A_CONV_NHWC
+    assert K.gemm_bf16_kernel_name(prob, mode) == name
+    K.gemm_bf16(prob, mode, K.gemm_workspace(DEV), K.TILE_AUTO)
+    torch.cuda.synchronize()
+    assert K.last_launch_name() == name
+
+    def im2col_gemm(u, v):  # (N, H, H, Cin) x (Cout, k, k, Cin) -> (rows, Cout), fp64 on the device
+        cols = F.unfold(u.permute(0, 3, 1, 2), k, padding=pad, stride=s)            # (N, Cin k k, Ho Wo)
+        wm = v.permute(0, 3, 1, 2).reshape(Cout, Kd)                                 # (ci, kh, kw) order
+        return (wm @ cols).permute(0, 2, 1).reshape(rows, Cout)
+    ref = im2col_gemm(x.double(), w.double()).cpu()
+    mag = im2col_gemm(x.double().abs(), w.double().abs()).cpu()
+    _check_out(out.reshape(rows, Cout), ref, mag)
+    _check_stats(stats, out, rows, Cout)

@@ -16,6 +16,8 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--only", choices=["enc", "dec"], default=None,
+                    help="after the warm-up, only replay that graph --steps times (a rocprofv3 trace of one part)")
     a = ap.parse_args()
     from capmi.data import synthetic_batch
     from capmi.optim import Adam
@@ -50,6 +52,12 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) * 1e3 / n
 
+    if a.only:
+        step.flush()
+        torch.cuda.synchronize()
+        g = step._pg[0]["g_" + a.only]
+        print(f"{a.only} graph alone {clock(g.replay, a.steps):.3f} ms")
+        return
     t_step = clock(lambda: step(imgs, caps, lens), a.steps)
     step.flush()
     torch.cuda.synchronize()
