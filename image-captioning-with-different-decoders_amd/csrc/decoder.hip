@@ -101,6 +101,11 @@ extern "C" int capmi_mean_rows(const float* enc, int B, int P, int E, float* out
 // score: e[b][p] = relu(att_enc[b][p][:] + ad[b][:]) . wf + bf      grid (P/PCH, B)
 // --------------------------------------------------------------------------------------
 constexpr int PCH = 28;  // slots per workgroup (7 per wave); 196 -> 7 chunks
+// the per-timestep score forward and context backward (round 6): 13 slots per workgroup -- the bench's 49 distinct
+// rows in 4 chunks, 256 workgroups at B = 64 instead of 128 (half the CUs idle, each reading twice the enc rows):
+// per call in a graph (tools/dec_kernels.py) att_score_fwd 5.15 -> 3.91 us, att_ctx_bwd 10.96 -> 10.26 us; every
+// row's dot product is one wave's in the same lane order, so the results are bit-identical
+constexpr int PCH_T = 13;
 
 __global__ void __launch_bounds__(256) att_score_fwd_kernel(
     const float* __restrict__ att_enc, const float* __restrict__ dec_part, int S, long long dec_slab,
@@ -108,7 +113,7 @@ __global__ void __launch_bounds__(256) att_score_fwd_kernel(
     int B, int P, int A, float* __restrict__ e, float* __restrict__ att_dec_out) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* ad = smem;  // [A]
-  const int b = blockIdx.y, p0 = blockIdx.x * PCH;
+  const int b = blockIdx.y, p0 = blockIdx.x * PCH_T;
   for (int a = threadIdx.x; a < A; a += blockDim.x) {
     const float v = slab_sum(dec_part + (long long)b * A + a, S, dec_slab, bias_da ? bias_da[a] : 0.f);
     ad[a] = v;
@@ -117,10 +122,10 @@ __global__ void __launch_bounds__(256) att_score_fwd_kernel(
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const float b0 = bf ? bf[0] : 0.f;
-  // a wave owns rows p0+wid, p0+wid+4, ... (PCH/4 of them): all their loads are issued before
-  // any reduction, and the PCH/4 wave sums run interleaved
-  constexpr int R = PCH / 4;
-  const int pend = min(P, p0 + PCH);
+  // a wave owns rows p0+wid, p0+wid+4, ... (ceil(PCH_T/4) of them): all their loads are issued before
+  // any reduction, and the wave sums run interleaved
+  constexpr int R = (PCH_T + 3) / 4;
+  const int pend = min(P, p0 + PCH_T);
   float acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -154,7 +159,7 @@ extern "C" int capmi_att_score_fwd(const float* att_enc, const float* dec_part, 
   CAPMI_REQUIRE(att_enc && dec_part && wf && e && B > 0 && P > 0 && A > 0 && S >= 1, CAPMI_EINVAL);
   CAPMI_REQUIRE(A % 4 == 0 && A <= 16384, CAPMI_ERANGE);
   CAPMI_REQUIRE(aligned16(att_enc) && aligned16(wf), CAPMI_EALIGN);
-  hipLaunchKernelGGL(att_score_fwd_kernel, dim3(cdiv(P, PCH), B), dim3(256), A * sizeof(float),
+  hipLaunchKernelGGL(att_score_fwd_kernel, dim3(cdiv(P, PCH_T), B), dim3(256), A * sizeof(float),
                      as_stream(stream), att_enc, dec_part, S, dec_slab, bias_da, wf, bf, B, P, A, e,
                      att_dec_out);
   CAPMI_LAUNCH_CHECK();
@@ -535,7 +540,7 @@ __global__ void __launch_bounds__(256) att_ctx_bwd_kernel(
     float* __restrict__ dgp, float* __restrict__ dalpha, float* __restrict__ dawe_out) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* dawe = smem;  // [E]
-  const int b = blockIdx.y, p0 = blockIdx.x * PCH;
+  const int b = blockIdx.y, p0 = blockIdx.x * PCH_T;
   for (int c = threadIdx.x * 4; c < E; c += 1024) {
     const long long o = (long long)b * E + c;
     const float4 d = slab_sum(reinterpret_cast<const float4*>(part + slab + o), S - 1, slab / 4,
@@ -559,7 +564,7 @@ __global__ void __launch_bounds__(256) att_ctx_bwd_kernel(
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int p = p0 + wid; p < min(P, p0 + PCH); p += 4) {
+  for (int p = p0 + wid; p < min(P, p0 + PCH_T); p += 4) {
     const float* row = enc + ((long long)b * P + p) * E;
     float acc = 0.f;
 #pragma unroll 8
@@ -632,7 +637,7 @@ extern "C" int capmi_att_ctx_bwd(const float* part, int S, long long slab, const
                     (!awe || aligned16(awe)) && (!dgp || aligned16(dgp)),
                 CAPMI_EALIGN);
   CAPMI_REQUIRE(!dgp || (gate && awe), CAPMI_EINVAL);
-  hipLaunchKernelGGL(att_ctx_bwd_kernel, dim3(cdiv(P, PCH), B), dim3(256), E * sizeof(float),
+  hipLaunchKernelGGL(att_ctx_bwd_kernel, dim3(cdiv(P, PCH_T), B), dim3(256), E * sizeof(float),
                      as_stream(stream), part, S, slab, gate, awe, enc, B, P, E, dgp, dalpha, dawe_out);
   CAPMI_LAUNCH_CHECK();
   return 0;

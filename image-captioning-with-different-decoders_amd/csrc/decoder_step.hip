@@ -16,8 +16,11 @@
 //   * W_hh h moves from the step's h-GEMM into the input GEMM (a second K segment), the score
 //     is recomputed by every workgroup of the context kernel (no separate score launch), and the
 //     score backward runs in the last workgroup of each row's context backward.
-// MFMA: v_mfma_f32_16x16x4_f32 (fp32 products and accumulation, the reference precision).
-#include "common.h"
+// MFMA (round 6): the fp32-accurate "x3" arithmetic of the other decoder GEMMs (CAPMI_GEMM_SPLIT3; gemm_x3.hip) --
+// each fp32 fragment read from LDS is split exactly into three bf16 terms in registers, six products per 16 x 16 x 32
+// block on v_mfma_f32_16x16x32_bf16 with fp32 accumulation (2.7x fewer MFMA cycles than v_mfma_f32_16x16x4_f32,
+// whose fp32 products rounds 1-5 used here; error at or below the fp32 kernel's: tests/test_gpu_dstep.py).
+#include "gemm_args.h"
 
 namespace {
 
@@ -109,21 +112,43 @@ __global__ void __launch_bounds__(256 * DS_KG) dstep_gemm_kernel(const DsArgs a)
       if (t + 256 * i < NW4)
         *reinterpret_cast<float4*>(&Ws[((t + 256 * i) >> 3) * DS_LD + ((t + 256 * i) & 7) * 4]) = st.rw[i];
   };
-  // lane (q = lane/16, r = lane%16) reads k 16g + 4q .. +3 of its row: MFMA e of the group
-  // contracts k = 16g + 4q + e over q (the same pairing for A and W)
+  // lane (q = lane/16, r = lane%16) reads k 8q .. 8q+7 of its row (the 16 x 16 x 32 bf16 operand layout; the same
+  // k for A and W), splits the eight values into their three bf16 terms and runs the six products, smallest first
+  typedef __bf16 bf16x8_d __attribute__((ext_vector_type(8)));
+  typedef unsigned u32x4_d __attribute__((ext_vector_type(4)));
+  auto split8 = [](const float4 v0, const float4 v1, bf16x8_d (&t)[3]) {
+    const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    u32x4_d w0, w1, w2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      unsigned wq[3];
+      split3_pair(v[2 * q], v[2 * q + 1], wq);
+      w0[q] = wq[0];
+      w1[q] = wq[1];
+      w2[q] = wq[2];
+    }
+    t[0] = __builtin_bit_cast(bf16x8_d, w0);
+    t[1] = __builtin_bit_cast(bf16x8_d, w1);
+    t[2] = __builtin_bit_cast(bf16x8_d, w2);
+  };
   auto compute = [&]() {
+    const int ko = 8 * (lane >> 4);
+    bf16x8_d av[3];
+    {
+      const float* ar_ = &As[(16 * w + (lane & 15)) * DS_LD + ko];
+      split8(*reinterpret_cast<const float4*>(ar_), *reinterpret_cast<const float4*>(ar_ + 4), av);
+    }
 #pragma unroll
-    for (int g = 0; g < DS_BK / 16; ++g) {
-      const int ko = 16 * g + 4 * (lane >> 4);
-      const float4 av = *reinterpret_cast<const float4*>(&As[(16 * w + (lane & 15)) * DS_LD + ko]);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const float4 bv = *reinterpret_cast<const float4*>(&Ws[(16 * j + (lane & 15)) * DS_LD + ko]);
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc[j], 0, 0, 0);
-      }
+    for (int j = 0; j < NJ; ++j) {
+      bf16x8_d bv[3];
+      const float* wr_ = &Ws[(16 * j + (lane & 15)) * DS_LD + ko];
+      split8(*reinterpret_cast<const float4*>(wr_), *reinterpret_cast<const float4*>(wr_ + 4), bv);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], bv[1], acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[2], acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2], bv[0], acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[1], acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1], bv[0], acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0], bv[0], acc[j], 0, 0, 0);
     }
   };
   // every k-tile of the group is requested before the first is multiplied: one memory round
