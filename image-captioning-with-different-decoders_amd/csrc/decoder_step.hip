@@ -29,6 +29,9 @@ constexpr int DS_ROWS = 64;  // rows (batch) per tile
 constexpr int DS_BK = 32;    // k per k-tile
 constexpr int DS_LD = 36;    // LDS row stride in floats: 16-lane ds_read_b128 groups hit 64 banks
 constexpr int kSc1d = 16;    // write-through / coherent cache policy of the parked partials
+#ifndef DSTEP_SC1
+#define DSTEP_SC1 1
+#endif
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_d(const void* p, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
@@ -199,17 +202,21 @@ __global__ void __launch_bounds__(256 * DS_KG) dstep_gemm_kernel(const DsArgs a)
     }
     __syncthreads();
     if (tid == 0) {
-      // acq_rel at agent scope: this split's parked partials (stored above, drained) are released
-      // before the count moves, and the last arriver acquires every other split's (the SC1 cache
-      // policy of the buffer ops stays as the performance hint, not the ordering guarantee)
-      const int old = __hip_atomic_fetch_add(a.count + tile, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      // DSTEP_SC1 (round 6): the hand-off form of MI355X_MICROARCH.md's "Valid forms besides Guideline 16", table
+      // row 1: every partial byte stored and loaded with 16-B sc1 buffer ops, every storing wave
+      // drained (vmcnt(0)) before the barrier above, ONE lane's relaxed agent-scope add for the workgroup, the
+      // workgroup whose add returns S - 1 learns it is last and its other waves load after the barrier below; one
+      // workgroup per CU (16 waves of 84-86 VGPRs: 5 waves per SIMD fit, a second workgroup's 4 do not).
+      // DSTEP_SC1=0: acq_rel at agent scope (an L2 write-back per workgroup) and an acquire in the last arriver
+      const int old = __hip_atomic_fetch_add(a.count + tile, 1, DSTEP_SC1 ? __ATOMIC_RELAXED : __ATOMIC_ACQ_REL,
+                                             __HIP_MEMORY_SCOPE_AGENT);
       const int last = old == S - 1;
       if (last) __hip_atomic_store(a.count + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       last_flag = last;
     }
     __syncthreads();
     if (!last_flag || grp != 0) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every wave of the last arriver reads the others' partials
+    if (!DSTEP_SC1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the fenced form's acquire)
     const auto rt = rsrc_d(a.part + tb, (unsigned)(S * DS_ROWS * NT * 4));
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
