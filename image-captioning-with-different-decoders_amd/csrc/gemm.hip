@@ -721,7 +721,16 @@ Bf16Plan bf16_io_plan(const capmi_gemm_problem& p, int tile, bool have_ws) {
     return e && e[0] == '1';
   }();
   r.sk = !st1 && bf16_sk && !sk_off() && have_ws && p.K / 64 >= 4 && (double)r.total / (double)(rounds * slots) < 0.9;
-  r.stages = st1 ? 1 : 2;
+  // (round 6) data-parallel: the LDS-DMA ring (gemm_bf16.hip), four k-tiles deep at one workgroup per CU when the grid
+  // is one round of tiles (layer3's 196-tile and layer4's 200-tile grids: l3 3x3 28.7 -> 23.4 us, l3 c1 15.8 -> 12.5,
+  // l4 c1 17.5 -> 14.7), else two deep at two workgroups per CU (l2 3x3 25.3 -> 21.4, l1 3x3 35.6 -> 31.4, ds3 27.4 ->
+  // 23.3, l4 c3 15.2 -> 13.1); CAPMI_BF16_STAGES = 2 / 4 forces one depth (A/B)
+  static const int bf16_stages = [] {
+    const char* e = getenv("CAPMI_BF16_STAGES");
+    const int v = e ? atoi(e) : 0;
+    return v == 2 || v == 4 ? v : 0;
+  }();
+  r.stages = st1 ? 1 : r.sk ? 2 : bf16_stages ? bf16_stages : r.total <= cu_count() ? 4 : 2;
   return r;
 }
 }  // namespace
@@ -810,7 +819,7 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
                       (amode == CAPMI_A_KMAJOR || amode == CAPMI_A_CONV_NHWC) && prob->K > 0 && prob->K % 64 == 0,
                   CAPMI_EINVAL);
     const Bf16Plan pl = bf16_io_plan(*prob, tile, true);
-    if (threads) *threads = 256;
+    if (threads) *threads = pl.stages >= 2 && !pl.sk && pl.bn == 128 ? 512 : 256;  // (gemm_bf16.hip: bf16_threads)
     if (bm) *bm = 128;
     if (bn) *bn = pl.bn;
     if (stream_k) *stream_k = pl.sk ? 1 : 0;

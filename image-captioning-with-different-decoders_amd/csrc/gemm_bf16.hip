@@ -48,23 +48,51 @@ __device__ __forceinline__ unsigned pack_bf(float lo, float hi) {
   return (unsigned)bf16_bits(lo) | ((unsigned)bf16_bits(hi) << 16);
 }
 
-// ST = LDS stages: 2 (two register stages ahead, two workgroups per CU) or 1 (round 5, 128x64 data-parallel only:
-// one LDS stage, one register stage ahead, four workgroups per CU -- the short-k 1x1 convs, where a tile's few
-// k-tiles leave no steady state to pipeline and more resident tiles hide the load latency instead)
+// s_barrier once this wave has at most N vector-memory operations (the later k-tiles' DMA) outstanding
+template <int N>
+__device__ __forceinline__ void vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// ST = LDS stages.
+//  * ST = 1 (round 5, 128x64 data-parallel only): one LDS stage, one register stage ahead, four workgroups per CU --
+//    the short-k 1x1 convs, where a tile's few k-tiles leave no steady state to pipeline and more resident tiles hide
+//    the load latency instead.
+//  * ST = 2 with stream-K (opt-in, CAPMI_BF16_SK=1): two register stages ahead, LDS double buffer, two workgroups per CU.
+//  * ST = 2 or 4 data-parallel (round 6): an LDS-DMA ring of ST k-tiles, ST - 1 in flight. The operands go straight
+//    from the buffer loads into LDS (buffer_load_dwordx4 ... lds: no staging registers, no ds_write), rows of 64 bf16
+//    without padding: lane l of a wave-instruction fills 16-B slot l % 8 of row l / 8 of a 1 KiB block, and that
+//    slot holds logical k-chunk (l % 8) ^ ((row / 2) % 8) (the swizzle is on the source address), so each 16-lane
+//    group of the 32x32x16 ds_read_b128 (lane: row l % 32, chunk 2 g + l / 32) covers 64 distinct banks. One barrier
+//    per k-tile, behind a counted vmcnt that leaves the later stages' DMA in flight. On 128-column tiles 512 threads
+//    (waves 2 x 4, wave tile 64 x 32), so a SIMD holds two waves of a workgroup: 75 VGPRs instead of the register
+//    form's 212, two workgroups per CU at ST = 2 (64 KiB of LDS each), one at ST = 4 (128 KiB).
+// Otherwise 256 threads (waves 2 x 2, wave tile 64 x BN / 2).
+constexpr bool bf16_dma(int ST, bool SK) { return ST >= 2 && !SK; }
+constexpr int bf16_threads(int BN, int ST, bool SK) { return bf16_dma(ST, SK) && BN == 128 ? 512 : 256; }
+constexpr int bf16_waves(int BM, int BN, int ST, bool SK) {  // waves per SIMD the LDS leaves room for
+  return ST == 1 ? 4 : !bf16_dma(ST, SK) ? 2 : (160 * 1024 / (ST * (BM + BN) * 128)) * bf16_threads(BN, ST, SK) / 256;
+}
+
 template <int BM, int BN, int AMODE, bool SK, int ST>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ST == 1 ? 4 : 2)))
+__global__ void __launch_bounds__((bf16_threads(BN, ST, SK))) __attribute__((amdgpu_waves_per_eu(bf16_waves(BM, BN, ST, SK))))
 gemm_bf16_kernel(const GemmArgs args) {
-  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
-  constexpr int NA = BM * BKH / 8 / 256, NB = BN * BKH / 8 / 256;
-  static_assert(NA >= 1 && NB >= 1 && WM == 64, "tile");
-  __shared__ __attribute__((aligned(16))) __bf16 lds_tile[ST * (BM + BN) * SBH];
-  __bf16* const As = lds_tile;                  // [ST][BM * SBH]
-  __bf16* const Bs = lds_tile + ST * BM * SBH;  // [ST][BN * SBH]
+  constexpr int NT = bf16_threads(BN, ST, SK), WGN = NT / 128;  // waves along N (2 along M)
+  constexpr int WM = BM / 2, WN = BN / WGN, TM = WM / 32, TN = WN / 32;
+  constexpr int NA = BM * BKH / 8 / NT, NB = BN * BKH / 8 / NT;
+  static_assert(NA >= 1 && NB >= 1 && WM == 64 && TN >= 1, "tile");
+  constexpr bool DMA = bf16_dma(ST, SK);
+  static_assert(!DMA || NA <= 4, "DMA offsets");
+  constexpr int SB = DMA ? BKH : SBH;  // LDS row stride (elements)
+  __shared__ __attribute__((aligned(1024))) __bf16 lds_tile[ST * (BM + BN) * SB];
+  __bf16* const As = lds_tile;                 // [ST][BM * SB]
+  __bf16* const Bs = lds_tile + ST * BM * SB;  // [ST][BN * SB]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm0 = (wid >> 1) * WM, wn0 = (wid & 1) * WN;
+  const int wm0 = (wid / WGN) * WM, wn0 = (wid % WGN) * WN;
   const int lr = lane & 31, lh = lane >> 5;
-  const int kc = (tid & 7) * 8;  // k offset of this thread's 16-B chunk inside a k-tile
+  // k offset of this thread's 16-B chunk inside a k-tile (its rows are (tid >> 3) + NT / 8 i: DMA swizzle (tid >> 4) % 8)
+  const int kc = DMA ? (((tid & 7) ^ ((tid >> 4) & 7)) * 8) : (tid & 7) * 8;
 
   f32x16 acc[TM][TN];
 
@@ -91,7 +119,7 @@ gemm_bf16_kernel(const GemmArgs args) {
     t_hi = k_hi;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int row = m0 + ((tid + i * 256) >> 3);
+      const int row = m0 + ((tid + i * NT) >> 3);
       a_ok[i] = row < M;
       if (AMODE == 0) {
         a_off[i] = a_ok[i] ? (unsigned)(((long long)row * P.lda + kc) * 2) : kOOB;
@@ -108,7 +136,7 @@ gemm_bf16_kernel(const GemmArgs args) {
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int n = n0 + ((tid + i * 256) >> 3);
+      const int n = n0 + ((tid + i * NT) >> 3);
       b_off[i] = n < N ? (unsigned)(((long long)n * P.ldb + kc) * 2) : kOOB;
     }
     if (AMODE == 2) {
@@ -147,29 +175,76 @@ gemm_bf16_kernel(const GemmArgs args) {
     for (int i = 0; i < NB; ++i)
       st.rb[i] = __builtin_amdgcn_raw_buffer_load_b128(rb, kok && !(BF16_SKIP & 4) ? b_off[i] + (unsigned)k * 2 : kOOB, 0, 0);
   };
-  // the first k-tiles of a tile into the register stages
+  // DMA ring: k-tile kt of the current tile into LDS stage buf, NA + NB wave-instructions per wave whatever kt is
+  // (past the k range every lane reads zeros), so the per-k-tile vmcnt count is a constant
+  const int wdu = __builtin_amdgcn_readfirstlane(wid);  // wave-uniform: the LDS-DMA bases in SGPRs
+  auto issue = [&](int kt, int buf) {
+    const int k = t_lo + kt * BKH;
+    const bool kok = k < t_hi && !(BF16_SKIP & 4);
+    unsigned offa[4];
+    if (AMODE == 0) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) offa[i] = kok ? a_off[i] + (unsigned)k * 2 : kOOB;
+    } else {
+      const int cH = P0.cH, cW = P0.cW, cCin = P0.cCin;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int ih = a_ih0[i] + c_kh, iw = a_iw0[i] + c_kw;
+        const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)cH && (unsigned)iw < (unsigned)cW;
+        offa[i] = ok ? ((a_off[i] + (unsigned)(ih * cW + iw)) * (unsigned)cCin + (unsigned)(c_ci + kc)) * 2u : kOOB;
+      }
+      c_ci += BKH;
+      if (c_ci >= cCin) {
+        c_ci = 0;
+        if (++c_kw == P0.cKW) {
+          c_kw = 0;
+          ++c_kh;
+        }
+      }
+    }
+    // row block wid + NT / 64 i: 8 rows x 128 B = 512 elements
+    __bf16* const ab = lds_tile + buf * BM * SB + wdu * 512;
+    __bf16* const bb = lds_tile + ST * BM * SB + buf * BN * SB + wdu * 512;
+    // (the DMA builtin takes offsets from local arrays of literal size: an element of the captured b_off[NB] as
+    // its argument loses the host launch stub)
+    unsigned offb[4];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) offb[i] = kok ? b_off[i] + (unsigned)k * 2 : kOOB;
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(ab + i * NT * 8), 16,
+                                               offa[i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (__attribute__((address_space(3))) void*)(bb + i * NT * 8), 16,
+                                               offb[i], 0, 0, 0);
+  };
+  // the first k-tiles of a tile into the register stages (the DMA ring issues its own in the k-loop)
   auto prefetch = [&](const capmi_gemm_problem& P, int m0, int n0, int k_lo, int k_hi) {
     begin_tile(P, m0, n0, k_lo, k_hi);
+    if (DMA) return;
     load_tile(s0, 0);
     if (ST == 2) load_tile(s1, 1);
   };
   auto store_tile = [&](const Stage& st, int buf) {
 #pragma unroll
-    for (int i = 0; i < NA; ++i) *reinterpret_cast<u32x4_t*>(&As[buf * BM * SBH + ((tid + i * 256) >> 3) * SBH + kc]) = st.ra[i];
+    for (int i = 0; i < NA; ++i) *reinterpret_cast<u32x4_t*>(&As[buf * BM * SB + ((tid + i * NT) >> 3) * SB + kc]) = st.ra[i];
 #pragma unroll
     for (int i = 0; i < NB; ++i)
-      *reinterpret_cast<u32x4_t*>(&Bs[buf * BN * SBH + ((tid + i * 256) >> 3) * SBH + kc]) = st.rb[i];
+      *reinterpret_cast<u32x4_t*>(&Bs[buf * BN * SB + ((tid + i * NT) >> 3) * SB + kc]) = st.rb[i];
   };
+  const int dsw = (lr >> 1) & 7;  // DMA ring: the swizzle of this lane's read rows (wm0 / wn0 + lr + 32 i)
   auto compute = [&](int buf) {
-    const __bf16* Ah = &As[buf * BM * SBH + (wm0 + lr) * SBH + 8 * lh];
-    const __bf16* Bh = &Bs[buf * BN * SBH + (wn0 + lr) * SBH + 8 * lh];
+    const __bf16* Ah = &As[buf * BM * SB + (wm0 + lr) * SB + (DMA ? 0 : 8 * lh)];
+    const __bf16* Bh = &Bs[buf * BN * SB + (wn0 + lr) * SB + (DMA ? 0 : 8 * lh)];
 #pragma unroll
     for (int g = 0; g < BKH / 16; ++g) {
       bf16x8_t a[TM], b[TN];
+      const int ko = DMA ? ((2 * g + lh) ^ dsw) * 8 : 16 * g;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const bf16x8_t*>(Ah + 32 * i * SBH + 16 * g);
+      for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const bf16x8_t*>(Ah + 32 * i * SB + ko);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const bf16x8_t*>(Bh + 32 * j * SBH + 16 * g);
+      for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const bf16x8_t*>(Bh + 32 * j * SB + ko);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -196,6 +271,20 @@ gemm_bf16_kernel(const GemmArgs args) {
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     const int nkt = (t_hi - t_lo) / BKH;
     if (nkt <= 0) return;
+    if constexpr (DMA) {  // LDS-DMA ring: k-tiles kt + 1 .. kt + ST - 2 stay in flight across the barrier
+#pragma unroll
+      for (int s = 0; s < ST - 1; ++s) issue(s, s);
+      for (int kt = 0; kt < nkt; ++kt) {
+        // this wave's DMA of k-tile kt done, every wave's (barrier); every wave past k-tile kt - 1's reads, so its
+        // stage takes k-tile kt + ST - 1
+        vm_barrier<(ST - 2) * (NA + NB)>();
+        issue(kt + ST - 1, (kt + ST - 1) % ST);
+        compute(kt % ST);
+      }
+      // the DMAs past the last k-tile drained and every wave's reads done before the epilogue stages C in LDS
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      return;
+    }
     if (ST == 1) {  // one LDS stage, one register stage ahead
       for (int kt = 0; kt < nkt; ++kt) {
         store_tile(s0, 0);
@@ -231,7 +320,7 @@ gemm_bf16_kernel(const GemmArgs args) {
       // per 2-B store (l3 c2 32.3 -> 30.3 us, l3 c3 19.9 -> 19.5)
       constexpr int ES = BN + 8;
       __bf16* E = lds_tile;
-      static_assert(BM * ES <= ST * (BM + BN) * SBH, "staging tile fits the LDS tile");
+      static_assert(BM * ES <= ST * (BM + BN) * SB, "staging tile fits the LDS tile");
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         csum[j] = 0.f;
@@ -252,8 +341,8 @@ gemm_bf16_kernel(const GemmArgs args) {
       const auto rc = rsrc_of(C, (unsigned)((long long)M * ldc * 2));
       constexpr int CPR = BN / 8;  // 16-B chunks per row
 #pragma unroll
-      for (int q = 0; q < BM * CPR / 256; ++q) {
-        const int e = q * 256 + tid, row = e / CPR, ch = e % CPR;
+      for (int q = 0; q < BM * CPR / NT; ++q) {
+        const int e = q * NT + tid, row = e / CPR, ch = e % CPR;
         const u32x4_t v = *reinterpret_cast<const u32x4_t*>(E + row * ES + ch * 8);
         if (!(BF16_SKIP & 1))
           __builtin_amdgcn_raw_buffer_store_b128(v, rc, (unsigned)(((long long)(m0 + row) * ldc + n0 + ch * 8) * 2), 0, 0);
@@ -347,7 +436,7 @@ gemm_bf16_kernel(const GemmArgs args) {
             v.y = __float_as_uint(acc[i][j][4 * q + 1]);
             v.z = __float_as_uint(acc[i][j][4 * q + 2]);
             v.w = __float_as_uint(acc[i][j][4 * q + 3]);
-            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (((i * TN + j) * 4 + q) * 256 + tid) * 16, 0, kSc1h);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (((i * TN + j) * 4 + q) * NT + tid) * 16, 0, kSc1h);
           }
       sk_publish(flags + blockIdx.x, tid);
       continue;
@@ -363,7 +452,7 @@ gemm_bf16_kernel(const GemmArgs args) {
           for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs, (((i * TN + j) * 4 + q) * 256 + tid) * 16, 0, kSc1h);
+              const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs, (((i * TN + j) * 4 + q) * NT + tid) * 16, 0, kSc1h);
               acc[i][j][4 * q + 0] += __uint_as_float(v.x);
               acc[i][j][4 * q + 1] += __uint_as_float(v.y);
               acc[i][j][4 * q + 2] += __uint_as_float(v.z);
@@ -376,21 +465,22 @@ gemm_bf16_kernel(const GemmArgs args) {
   }
 }
 
+template <int BM, int BN>
+void launch_bf16_sk(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
+  const dim3 g(blocks), b(bf16_threads(BN, 2, true));
+  if (amode == 2)
+    CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 2, true, 2>), g, b, 0, s, a);
+  else
+    CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 0, true, 2>), g, b, 0, s, a);
+}
+
 template <int BM, int BN, int ST>
-void launch_bf16(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
-  const dim3 g(blocks), b(256);
-  const bool sk = a.sk_workers > 0;
-  if (amode == 2) {
-    if (sk)
-      CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 2, true, ST>), g, b, 0, s, a);
-    else
-      CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 2, false, ST>), g, b, 0, s, a);
-  } else {
-    if (sk)
-      CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 0, true, ST>), g, b, 0, s, a);
-    else
-      CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 0, false, ST>), g, b, 0, s, a);
-  }
+void launch_bf16_dma(const GemmArgs& a, int amode, int blocks, hipStream_t s) {
+  const dim3 g(blocks), b(bf16_threads(BN, ST, false));
+  if (amode == 2)
+    CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 2, false, ST>), g, b, 0, s, a);
+  else
+    CAPMI_KLAUNCH((gemm_bf16_kernel<BM, BN, 0, false, ST>), g, b, 0, s, a);
 }
 
 template <int BM, int BN>
@@ -507,15 +597,30 @@ unsigned grid_for(long long n) { return (unsigned)std::min<long long>(std::max<l
 }  // namespace
 
 int gemm_bf16_launch(const GemmArgs& a, int amode, int bm, int bn, int blocks, hipStream_t s, int stages) {
+  if (bm != 128 || (bn != 64 && bn != 128)) return CAPMI_EINVAL;
+  const bool sk = a.sk_workers > 0;
   if (stages == 1) {  // (data-parallel 128x64 only)
-    if (bm != 128 || bn != 64 || a.sk_workers > 0) return CAPMI_EINVAL;
+    if (bn != 64 || sk) return CAPMI_EINVAL;
     launch_bf16_st1<128, 64>(a, amode, blocks, s);
-  } else if (bm == 128 && bn == 128)
-    launch_bf16<128, 128, 2>(a, amode, blocks, s);
-  else if (bm == 128 && bn == 64)
-    launch_bf16<128, 64, 2>(a, amode, blocks, s);
-  else
+  } else if (sk) {  // (two register stages)
+    if (stages != 2) return CAPMI_EINVAL;
+    if (bn == 128)
+      launch_bf16_sk<128, 128>(a, amode, blocks, s);
+    else
+      launch_bf16_sk<128, 64>(a, amode, blocks, s);
+  } else if (stages == 2) {  // the data-parallel DMA ring
+    if (bn == 128)
+      launch_bf16_dma<128, 128, 2>(a, amode, blocks, s);
+    else
+      launch_bf16_dma<128, 64, 2>(a, amode, blocks, s);
+  } else if (stages == 4) {
+    if (bn == 128)
+      launch_bf16_dma<128, 128, 4>(a, amode, blocks, s);
+    else
+      launch_bf16_dma<128, 64, 4>(a, amode, blocks, s);
+  } else {
     return CAPMI_EINVAL;
+  }
   CAPMI_LAUNCH_CHECK();
   return 0;
 }

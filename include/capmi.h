@@ -188,8 +188,9 @@ int capmi_gemm_sk_ex(const capmi_gemm_problem* problem, int amode, int bmode, in
  * time. Any out pointer may be NULL. */
 int capmi_gemm_sk_plan(const capmi_gemm_problem* problem, int amode, int bmode, int tile, int flags, int* bm,
                        int* bn, int* stream_k, int* generic, int* threads);
-/* (ABI 25) for CAPMI_GEMM_BF16_IO the plan is the launcher's own (generic = the LDS stages, 1 or 2; stream_k as
- * if a workspace were passed). The name of the last GEMM kernel instantiation this host thread launched (demangled,
+/* (ABI 25) for CAPMI_GEMM_BF16_IO the plan is the launcher's own (generic = the LDS stages: 1 the one-stage short-k
+ * form, 2 or 4 the data-parallel LDS-DMA ring, 2 with stream_k the register-staged stream-K form; stream_k as if a
+ * workspace were passed; threads 512 for the 128-column DMA ring). The name of the last GEMM kernel instantiation this host thread launched (demangled,
  * without return type and parameters, as rocprofv3 lists it) into out[n]: what a plan query's name must equal.
  * Needs the HIP runtime's code-object registry (a GPU process). */
 int capmi_last_launch_name(char* out, int n);

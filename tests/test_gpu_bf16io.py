@@ -40,9 +40,11 @@ def _check_stats(stats, out, rows, C):
 
 
 @pytest.mark.parametrize("N,H,Cin,Cout,k,s,tile", [
-    (64, 14, 256, 256, 3, 1, 3),   # layer3 conv2 at batch 64: stream-K, 128x128
-    (2, 14, 256, 256, 3, 1, 3),    # small grid: data-parallel
+    (64, 14, 256, 256, 3, 1, 3),   # layer3 conv2 at batch 64: 196 tiles, the four-deep DMA ring on 512 threads
+    (2, 14, 256, 256, 3, 1, 3),    # small grid
     (2, 56, 64, 64, 3, 1, 3),      # layer1 conv2: N = 64 -> 128x64
+    (12, 56, 64, 64, 3, 1, 3),     # 294 tiles of 128x64: the two-deep DMA ring on 256 threads
+    (48, 28, 64, 128, 3, 1, 3),    # 294 tiles of 128x128: the two-deep DMA ring on 512 threads
     (1, 28, 128, 128, 3, 2, 3),    # stride-2 3x3 (first block of layer3), M % 128 != 0
     (2, 14, 128, 256, 1, 2, 3),    # stride-2 1x1 downsample
     (3, 7, 512, 192, 1, 1, 2),     # forced 128x64, N not a multiple of 64
@@ -79,7 +81,8 @@ def test_bf16io_conv(N, H, Cin, Cout, k, s, tile):
 # K <= 256 under AUTO: the one-stage 128x64 form (round 5) -- the l3 c3 shape, a partial last row tile, N not a
 # multiple of 64 (general epilogue), layer1's K = 64
 @pytest.mark.parametrize("M,N,Kd,tile", [(12544, 256, 1024, 3), (1000, 512, 256, 3), (300, 64, 128, 3),
-                                         (12544, 1024, 256, 3), (500, 200, 192, 3), (2000, 256, 64, 3)])
+                                         (12544, 1024, 256, 3), (500, 200, 192, 3), (2000, 256, 64, 3),
+                                         (40000, 128, 512, 3), (3000, 320, 576, 3)])
 def test_bf16io_dense(M, N, Kd, tile):
     from capmi import kernels as K
     from capmi._lib import CAPMI_A_KMAJOR
@@ -144,14 +147,15 @@ def test_bf16_elementwise():
 
 
 @pytest.mark.parametrize("H,Cin,Cout,k,s,name", [
-    (7, 512, 512, 3, 1, "gemm_bf16_kernel<128, 64, 2, false, 2>"),    # layer4 3x3: 100 tiles of 128x128, K = 4608
-    (14, 512, 512, 3, 2, "gemm_bf16_kernel<128, 64, 2, false, 2>"),   # layer4.0's stride-2 3x3
-    (7, 2048, 512, 1, 1, "gemm_bf16_kernel<128, 64, 0, false, 2>"),   # layer4 c1 (K = 2048, dense rows)
+    (7, 512, 512, 3, 1, "gemm_bf16_kernel<128, 64, 2, false, 4>"),    # layer4 3x3: 100 tiles of 128x128, K = 4608
+    (14, 512, 512, 3, 2, "gemm_bf16_kernel<128, 64, 2, false, 4>"),   # layer4.0's stride-2 3x3
+    (7, 2048, 512, 1, 1, "gemm_bf16_kernel<128, 64, 0, false, 4>"),   # layer4 c1 (K = 2048, dense rows)
 ])
 def test_bf16io_layer4_exact_shapes(H, Cin, Cout, k, s, name):
-    """layer4's convs at batch 64 run the 128x64 two-stage form on grids of 128x128 tiles that fill
-    at most half the CUs (round 5, gemm.hip bf16_io_plan) -- checked element-wise at their exact shapes, the
-    instantiation asserted through the launcher's own plan. fp64 reference on the device (im2col + GEMM)."""
+    """layer4's convs at batch 64 run 128x64 tiles on grids of 128x128 tiles that fill at most half
+    the CUs (round 5), since round 6 on the four-deep DMA ring (gemm.hip bf16_io_plan) -- checked element-wise at their
+    exact shapes, the instantiation asserted through the launcher's own plan. fp64 reference on the device (im2col +
+    GEMM)."""
     from capmi import kernels as K
     from capmi._lib import CAPMI_A_CONV_NHWC, CAPMI_A_KMAJOR
     N, pad = 64, k // 2
