@@ -1,6 +1,6 @@
 """Where the pipelined step's time goes: the bench's 'attention' step (pipelined HIP graphs, B = 64) timed whole,
 then its encoder graph and its decoder graph (decoder step + clamp / Adam) each replayed alone on the chip.
-python tools/pipe_parts.py [--steps 20]
+python tools/pipe_parts.py [--steps 20] [--bert]  (--bert: config 5, bf16 encoder + 768-d synthetic word features)
 The step is max(encoder, decoder) when the two streams share the chip perfectly; what it costs above that is
 the interference of the decoder's kernels with the encoder's persistent grids."""
 import argparse
@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--only", choices=["enc", "dec"], default=None,
                     help="after the warm-up, only replay that graph --steps times (a rocprofv3 trace of one part)")
+    ap.add_argument("--bert", action="store_true", help="BASELINE config 5 (bench.py --config bert_attention)")
     a = ap.parse_args()
     from capmi.data import synthetic_batch
     from capmi.optim import Adam
@@ -28,12 +29,16 @@ def main():
     dev = torch.device("cuda")
     torch.manual_seed(0)
     enc = EncoderAttention().to(dev).train()
-    enc.set_compute_precision("fp32-x3")
+    enc.set_compute_precision("bf16" if a.bert else "fp32-x3")
     prm = AttentionDecoderParams()
     prm.vocab = synthetic_vocab(8100)
-    prm.embed_size = 512
+    prm.embed_size = 768 if a.bert else 512
+    prm.use_bert = a.bert
     dec = AttentionDecoder(dev, prm)
-    dec.set_compute_precision("fp32-x3")
+    if a.bert:
+        from capmi.data import SyntheticBertEmbedder
+        dec.bert_embedder = SyntheticBertEmbedder(8100, 768, device=dev)
+    dec.set_compute_precision("bf16" if a.bert else "fp32-x3")
     dec = dec.to(dev).train()
     dec.fine_tune_embeddings(False)
     opt = Adam(filter(lambda q: q.requires_grad, dec.parameters()), lr=1e-4)
