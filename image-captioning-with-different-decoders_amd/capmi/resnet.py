@@ -602,6 +602,13 @@ _FT_WGRAD_X3W = os.environ.get("CAPMI_FT_WGRAD_X3W", "1") != "0"
 # capmi_weight_x3_batch launch per step, from the second step on (the first records what the step uses);
 # CAPMI_FT_WPREP_BATCH=0: the per-conv packs and splits (A/B)
 _FT_WPREP_BATCH = os.environ.get("CAPMI_FT_WPREP_BATCH", "1") != "0"
+# round 6 (opt-in): the weight gradients on a second HIP stream beside the data-gradient chain (they are off its
+# critical path: nothing in the chain reads them), their inputs double-buffered by block parity so the chain waits
+# only for the weight gradients of two blocks back. CAPMI_FT_WGRAD_SIDE=1: the side stream at the high end of the
+# priority range (the chain on the caller's stream); "lo": at the low end. Off by default: measured slower (DESIGN
+# 4.23) -- the chain's stream-K data gradients hand partials between co-resident workgroups, and a weight gradient
+# holding CUs beside them leaves owners spinning for producers that have no CU yet
+_FT_WGRAD_SIDE = os.environ.get("CAPMI_FT_WGRAD_SIDE", "0")
 
 
 class FineTuneRunner:
@@ -630,6 +637,10 @@ class FineTuneRunner:
         self._wx3 = None
         self._wx3_n = 0  # jobs in the device array (fixed when it is built)
         self._wx3_fwd = {}  # cache key -> the forward planes buffer the array refreshes
+        # weight gradients beside the data-gradient chain (_FT_WGRAD_SIDE); None: one stream
+        self.wgrad_side = _FT_WGRAD_SIDE != "0"
+        self._side = None
+        self._side_ws = None
 
     # ------------------------------------------------------------------ forward
     def _bn_save(self, ws, bn, rows):
@@ -748,8 +759,9 @@ class FineTuneRunner:
             return CAPMI_GEMM_SPLIT3
         return 0
 
-    def _gemm(self, prob, amode, bmode, tile=K.TILE_AUTO):
-        K.gemm_sk(prob, amode, self.r._ws["sk"], tile, bmode, flags=self._flags(prob, amode, bmode))
+    def _gemm(self, prob, amode, bmode, tile=K.TILE_AUTO, ws=None):
+        K.gemm_sk(prob, amode, self.r._ws["sk"] if ws is None else ws, tile, bmode,
+                  flags=self._flags(prob, amode, bmode))
 
     @torch.no_grad()
     def backward(self, dfeat, grads, hook=None, on_layer=None):
@@ -770,9 +782,24 @@ class FineTuneRunner:
         blocks = stt["blocks"]
         big = max(b["H"] * b["W"] * max(b["Cin"], b["Cout"], b["wd"]) for b in blocks) * N
         dA = [gp("dA0", big, dev), gp("dA1", big, dev)]
-        dmid = gp("dmid", big, dev)
-        dy3 = gp("dy3", big, dev)
-        dyd = gp("dyd", big, dev)
+        # two streams (weight gradients beside the chain) only without the timing hook: the bench's roofline pass
+        # times each GEMM alone on the chip
+        two = self.wgrad_side and hook is None and dev.type == "cuda"
+        main = torch.cuda.current_stream(dev) if two else None
+        if two and self._side is None:
+            lo, hi = torch.cuda.Stream.priority_range()
+            self._side = torch.cuda.Stream(device=dev, priority=lo if _FT_WGRAD_SIDE == "lo" else hi)
+            self._side_ws = K.gemm_workspace(dev)
+        side_done = []  # per block (in backward order): event after its weight gradients on the side stream
+        joined = 0  # side_done[:joined] are behind a join of the chain (no wait needed; across graph segments none is
+        # allowed: an event recorded in one capture cannot be waited on in another)
+        # the chain's buffers the weight gradients read (dy3, dmid = da2, da1, dyd): one set per block parity with
+        # two streams, so block j's chain only waits for the weight gradients of block j - 2
+        npar = 2 if two else 1
+        dmid_p = [gp(f"dmid{i}", big, dev) for i in range(npar)]
+        dy3_p = [gp(f"dy3{i}", big, dev) for i in range(npar)]
+        dyd_p = [gp(f"dyd{i}", big, dev) for i in range(npar)]
+        da1_p = [gp(f"da1{i}", big, dev) for i in range(npar)] if two else dy3_p  # (one stream: da1 reuses dy3)
         wmax = max(b["wd"] * 9 * b["wd"] for b in blocks)
         dwp = gp("dw_packed", wmax, dev)
         wdg = gp("w_dgrad", wmax, dev)
@@ -788,18 +815,19 @@ class FineTuneRunner:
         def G(p):
             return grads.get(id(p))
 
-        def run(tag, flops, prob, amode, bmode, tile=K.TILE_AUTO):
+        def run(tag, flops, prob, amode, bmode, tile=K.TILE_AUTO, ws=None):
             if amode == AMM and self.r.x3 and _FT_WGRAD_X3W and K.gemm_x3w_ok(prob, bmode):
-                launch = lambda: K.gemm_x3w(prob, bmode, self.r._ws["sk"])  # noqa: E731
+                wsk = self.r._ws["sk"] if ws is None else ws
+                launch = lambda: K.gemm_x3w(prob, bmode, wsk)  # noqa: E731
                 if hook is None:
                     launch()
                 else:
                     hook(tag, flops, launch, K.gemm_x3w_kernel_name(prob, bmode))
                 return
             if hook is None:
-                self._gemm(prob, amode, bmode, tile)
+                self._gemm(prob, amode, bmode, tile, ws)
             else:
-                hook(tag, flops, lambda: self._gemm(prob, amode, bmode, tile),
+                hook(tag, flops, lambda: self._gemm(prob, amode, bmode, tile, ws),
                      K.gemm_sk_kernel_name(prob, amode, bmode, tile=tile, flags=self._flags(prob, amode, bmode)))
 
         x3d = self.r.x3 and _FT_DGRAD_X3 and _FT_DGRAD_X3D
@@ -870,11 +898,27 @@ class FineTuneRunner:
             else:
                 hook(tag, flops, launch, name)
 
+        def wgrad(fn):
+            """A weight gradient (and what finishes it): on the side stream after everything the chain has
+            launched so far (its inputs), else inline."""
+            if not two:
+                fn()
+                return
+            self._side.wait_stream(main)
+            with torch.cuda.stream(self._side):
+                fn()
+
         K.adaptive_avgpool_bwd_nhwc(dfeat.contiguous(), N, stt["H"], stt["W"], stt["C"], stt["OH"], stt["OW"],
                                     dA[0])
         cur = 0
+        wsw = self._side_ws if two else None
         for bi in range(len(blocks) - 1, -1, -1):
             b = blocks[bi]
+            j = len(blocks) - 1 - bi  # blocks done before this one
+            par = j % npar
+            if two and j >= 2 and j - 2 >= joined:  # this block's buffers were read by block j - 2's weight gradients
+                main.wait_event(side_done[j - 2])
+            dmid, dy3, dyd, da1buf = dmid_p[par], dy3_p[par], dyd_p[par], da1_p[par]
             blk, tag = b["blk"], b["tag"]
             H, W, H2, W2, s = b["H"], b["W"], b["H2"], b["W2"], b["stride"]
             Cin, wd, Cout = b["Cin"], b["wd"], b["Cout"]
@@ -899,9 +943,9 @@ class FineTuneRunner:
             c3 = blk.conv3
             geo3 = dict(N=N, H=H2, W=W2, Cin=wd, KH=1, KW=1, stride=1, pad=0, Ho=H2, Wo=W2)
             if G(c3.weight) is not None:
-                run(tag + ".conv3.wgrad", 2.0 * r3 * Cout * wd,
-                    K.problem(Cout, wd, r3, dy3, Cout, b["y2"], 0, G(c3.weight), wd, conv=geo3, in_scale=s2,
-                              in_shift=b2), AMM, BCONV)
+                wgrad(lambda: run(tag + ".conv3.wgrad", 2.0 * r3 * Cout * wd,
+                                  K.problem(Cout, wd, r3, dy3, Cout, b["y2"], 0, G(c3.weight), wd, conv=geo3,
+                                            in_scale=s2, in_shift=b2), AMM, BCONV, ws=wsw))
             da2 = dmid[:r3 * wd]
             if _FT_DGRAD1_KROWS:
                 run(tag + ".conv3.dgrad", 2.0 * r3 * Cout * wd,
@@ -918,11 +962,13 @@ class FineTuneRunner:
             c2 = blk.conv2
             geo2 = dict(N=N, H=H, W=W, Cin=wd, KH=3, KW=3, stride=s, pad=1, Ho=H2, Wo=W2)
             if G(c2.weight) is not None:
-                run(tag + ".conv2.wgrad", 2.0 * r3 * wd * 9 * wd,
-                    K.problem(wd, 9 * wd, r3, da2, wd, b["y1"], 0, dwp, 9 * wd, conv=geo2, in_scale=s1,
-                              in_shift=b1), AMM, BCONV)
-                K.conv_weight_unpack(dwp, tuple(c2.weight.shape), G(c2.weight))
-            da1 = dy3[:r1 * wd]  # dy3 is consumed
+                def c2w():
+                    run(tag + ".conv2.wgrad", 2.0 * r3 * wd * 9 * wd,
+                        K.problem(wd, 9 * wd, r3, da2, wd, b["y1"], 0, dwp, 9 * wd, conv=geo2, in_scale=s1,
+                                  in_shift=b1), AMM, BCONV, ws=wsw)
+                    K.conv_weight_unpack(dwp, tuple(c2.weight.shape), G(c2.weight))
+                wgrad(c2w)
+            da1 = da1buf[:r1 * wd]  # (one stream: dy3, consumed)
             if s == 1:
                 geod = dict(N=N, H=H, W=W, Cin=wd, KH=3, KW=3, stride=1, pad=1, Ho=H, Wo=W)
                 run_dgrad(tag + ".conv2.dgrad", 2.0 * r3 * wd * 9 * wd,
@@ -950,8 +996,8 @@ class FineTuneRunner:
             # ---- conv1 (1x1) on the block input x
             c1 = blk.conv1
             if G(c1.weight) is not None:
-                run(tag + ".conv1.wgrad", 2.0 * r1 * wd * Cin,
-                    K.problem(wd, Cin, r1, da1, wd, b["x"], Cin, G(c1.weight), Cin), AMM, BKR)
+                wgrad(lambda: run(tag + ".conv1.wgrad", 2.0 * r1 * wd * Cin,
+                                  K.problem(wd, Cin, r1, da1, wd, b["x"], Cin, G(c1.weight), Cin), AMM, BKR, ws=wsw))
             if need_dx:
                 if _FT_DGRAD1_KROWS:
                     run(tag + ".conv1.dgrad", 2.0 * r1 * wd * Cin,
@@ -966,8 +1012,9 @@ class FineTuneRunner:
                 cd = ds[0]
                 geodn = dict(N=N, H=H, W=W, Cin=Cin, KH=1, KW=1, stride=s, pad=0, Ho=H2, Wo=W2)
                 if G(cd.weight) is not None:
-                    run(tag + ".downsample.wgrad", 2.0 * r3 * Cout * Cin,
-                        K.problem(Cout, Cin, r3, dyd, Cout, b["x"], 0, G(cd.weight), Cin, conv=geodn), AMM, BCONV)
+                    wgrad(lambda: run(tag + ".downsample.wgrad", 2.0 * r3 * Cout * Cin,
+                                      K.problem(Cout, Cin, r3, dyd, Cout, b["x"], 0, G(cd.weight), Cin, conv=geodn),
+                                      AMM, BCONV, ws=wsw))
                 if need_dx:
                     # dX[n, s*i, s*j, :] += dYd[n, i, j, :] W_d  (rows (n, i, j) -> strided NHWC rows)
                     rm = dict(c_r1=W2, c_s2=s * W * Cin) if s > 1 else {}
@@ -980,8 +1027,16 @@ class FineTuneRunner:
                                   K.problem(r3, Cin, Cout, dyd, Cout, wt, Cout, dx, s * Cin, beta=1.0, **rm), wt,
                                   w1=cd.weight.detach())
             cur ^= 1
+            if two:
+                side_done.append(torch.cuda.Event())
+                side_done[-1].record(self._side)
             if on_layer is not None and (bi == 0 or blocks[bi - 1]["li"] != b["li"]):
+                if two:  # the stage's weight gradients are final once the side stream's work so far is
+                    main.wait_stream(self._side)
+                    joined = len(side_done)
                 on_layer(b["li"])
+        if two:  # join: the caller's stream sees every gradient (and a graph capture ends joined)
+            main.wait_stream(self._side)
         self.state = None
         if _FT_WPREP_BATCH and self._wx3 is None and self.r.x3:
             self._build_wx3(stt)
