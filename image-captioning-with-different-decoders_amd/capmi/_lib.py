@@ -23,7 +23,7 @@ CAPMI_B_NMAJOR_W, CAPMI_B_KROWS, CAPMI_B_CONV_NHWC = 0, 1, 2
 CAPMI_TILE_128, CAPMI_TILE_64, CAPMI_TILE_128x64, CAPMI_TILE_AUTO, CAPMI_TILE_128_W8 = 0, 1, 2, 3, 4
 CAPMI_MAX_GROUP = 4
 CAPMI_COLSUM_GROUPS = 64
-ABI_VERSION = 25
+ABI_VERSION = 26
 CAPMI_BNB_RELU_Y, CAPMI_BNB_RELU_OUT = 0, 1
 CAPMI_BNB_MAX_SLABS = 256
 CAPMI_GEMM_BF16 = 1

@@ -27,7 +27,7 @@ import torch
 
 from . import kernels as K
 from ._lib import CAPMI_A_KMAJOR as AK, CAPMI_A_MMAJOR as AMM, CAPMI_B_KROWS as BKR
-from ._lib import CAPMI_B_NMAJOR_W as BW, CAPMI_GEMM_SPLIT3
+from ._lib import CAPMI_B_NMAJOR_W as BW, CAPMI_GEMM_BF16, CAPMI_GEMM_SPLIT3
 from ._lib import CAPMI_DSTEP_GATE_BWD, CAPMI_DSTEP_LSTM_BWD, CAPMI_DSTEP_LSTM_FWD, CAPMI_DSTEP_STORE2
 
 E_DIM = 2048
@@ -47,9 +47,10 @@ def _dsplit(M, N, nt, K_, target=None):
     return max(1, min(kt, max(-(-kt // 16), round(target / tiles))))
 
 
-# round 6: the hoisted weight gradients dW = dY^T X (rows = timesteps x batch) in the x3 arithmetic on gemm_x3w, the
-# encoder fine-tune's weight-gradient kernel (both fp32 operands split in-kernel, 256 x 128 tiles, k-split slabs),
-# where its planner takes the problem (CAPMI_DEC_WGRAD_X3W=0: the split-staging stream-K kernel, A/B)
+# round 6: the hoisted weight gradients dW = dY^T X (rows = timesteps x batch) on gemm_x3w, the encoder fine-tune's
+# weight-gradient kernel (both fp32 operands split in-kernel, 256 x 128 tiles, k-split slabs) -- in the x3
+# arithmetic, or with one bf16 term per operand in the bf16 configuration (gemm_w16) -- where its planner takes the
+# problem (CAPMI_DEC_WGRAD_X3W=0: the split-staging stream-K kernel, A/B)
 DEC_WGRAD_X3W = os.environ.get("CAPMI_DEC_WGRAD_X3W", "1") != "0"
 
 # workgroups a per-timestep GEMM launch aims for (CAPMI_DEC_WGS, A/B measurement: fewer, longer
@@ -177,9 +178,11 @@ class DecoderCore:
         few output tiles (dW_enc_att: 128 tiles of 128x64 over K = B*P) still fills the chip.
         gf: operand staging flags (0 fp32 MFMA, CAPMI_GEMM_SPLIT3, CAPMI_GEMM_BF16)."""
         prob = K.problem(M, N, Kd, A, lda, B, ldb, out, ld_out, bias=bias, **kw)
-        if DEC_WGRAD_X3W and amode == AMM and gf == CAPMI_GEMM_SPLIT3 and K.gemm_x3w_ok(prob, bmode):
-            K.gemm_x3w(prob, bmode, ws.sk)
-            return
+        if DEC_WGRAD_X3W and amode == AMM and gf in (CAPMI_GEMM_SPLIT3, CAPMI_GEMM_BF16):
+            bf16 = gf == CAPMI_GEMM_BF16  # (the bf16 configuration: gemm_w16, one bf16 term per operand)
+            if K.gemm_x3w_ok(prob, bmode, bf16):
+                K.gemm_x3w(prob, bmode, ws.sk, bf16)
+                return
         K.gemm_sk(prob, amode, ws.sk, K.TILE_AUTO, bmode, flags=gf)
 
     # ------------------------------------------------------------------ fused recurrence

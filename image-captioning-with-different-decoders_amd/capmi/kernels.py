@@ -9,7 +9,8 @@ import weakref
 import torch
 
 from ._lib import DstepEpi, DstepSeg
-from ._lib import (CAPMI_A_CONV_NHWC, CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_GEMM_BF16_IO, CAPMI_GEMM_X3, CAPMI_GEMM_X3P,
+from ._lib import (CAPMI_A_CONV_NHWC, CAPMI_A_KMAJOR, CAPMI_A_MMAJOR, CAPMI_B_NMAJOR_W, CAPMI_BNB_MAX_SLABS, CAPMI_GEMM_BF16,
+                   CAPMI_GEMM_BF16_IO, CAPMI_GEMM_X3, CAPMI_GEMM_X3P,
                    CAPMI_GEMM_SPLIT3, CAPMI_GEMM_X3C, CAPMI_GEMM_X3D, CAPMI_GEMM_X3S, CAPMI_GEMM_X3W,
                    CAPMI_COLSUM_GROUPS, CAPMI_TILE_128, CAPMI_TILE_64,
                    CAPMI_TILE_128x64, CAPMI_TILE_AUTO, GemmProblem, call, lib)
@@ -219,26 +220,30 @@ def gemm_x3c_kernel_name(prob):
     return f"gemm_x3c_kernel<{'true' if prob.in_scale else 'false'}>"
 
 
-def gemm_x3w(prob, bmode, workspace):
+def gemm_x3w(prob, bmode, workspace, bf16=False):
     """CAPMI_GEMM_X3W: the conv weight gradient dW = dY^T . B (A = dY fp32 k rows, CAPMI_A_MMAJOR; B fp32 k
     rows, CAPMI_B_KROWS, or the NHWC conv input's im2col, CAPMI_B_CONV_NHWC, with the optional BN prologue);
-    k-split partial slabs in the stream-K workspace."""
+    k-split partial slabs in the stream-K workspace. bf16: one bf16 term per operand (| CAPMI_GEMM_BF16, ABI 26)."""
     _cuda(workspace, dtype=torch.int32)
-    call("capmi_gemm_sk_ex", ctypes.byref(prob), CAPMI_A_MMAJOR, bmode, CAPMI_TILE_AUTO, CAPMI_GEMM_X3W,
+    call("capmi_gemm_sk_ex", ctypes.byref(prob), CAPMI_A_MMAJOR, bmode, CAPMI_TILE_AUTO, _x3w_flags(bf16),
          ptr(workspace), workspace.numel() * 4, stream())
 
 
-def gemm_x3w_kernel_name(prob, bmode):
+def _x3w_flags(bf16):
+    return CAPMI_GEMM_X3W | (CAPMI_GEMM_BF16 if bf16 else 0)
+
+
+def gemm_x3w_kernel_name(prob, bmode, bf16=False):
     v = [ctypes.c_int(0) for _ in range(5)]
-    call("capmi_gemm_sk_plan", ctypes.byref(prob), CAPMI_A_MMAJOR, bmode, CAPMI_TILE_AUTO, CAPMI_GEMM_X3W,
+    call("capmi_gemm_sk_plan", ctypes.byref(prob), CAPMI_A_MMAJOR, bmode, CAPMI_TILE_AUTO, _x3w_flags(bf16),
          *[ctypes.byref(x) for x in v])
-    return f"gemm_x3w_kernel<{bmode}, {'true' if v[2].value else 'false'}>"
+    return f"{'gemm_w16_kernel' if bf16 else 'gemm_x3w_kernel'}<{bmode}, {'true' if v[2].value else 'false'}>"
 
 
-def gemm_x3w_ok(prob, bmode):
+def gemm_x3w_ok(prob, bmode, bf16=False):
     """True when CAPMI_GEMM_X3W takes this weight-gradient problem (its planner accepts it)."""
     v = [ctypes.c_int(0) for _ in range(5)]
-    return lib.capmi_gemm_sk_plan(ctypes.byref(prob), CAPMI_A_MMAJOR, bmode, CAPMI_TILE_AUTO, CAPMI_GEMM_X3W,
+    return lib.capmi_gemm_sk_plan(ctypes.byref(prob), CAPMI_A_MMAJOR, bmode, CAPMI_TILE_AUTO, _x3w_flags(bf16),
                                   *[ctypes.byref(x) for x in v]) == 0
 
 

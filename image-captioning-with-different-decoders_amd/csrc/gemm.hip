@@ -768,7 +768,7 @@ extern "C" int capmi_gemm_sk_plan(const capmi_gemm_problem* prob, int amode, int
     if (generic) *generic = 32;
     return 0;
   }
-  if (flags == CAPMI_GEMM_X3W) {
+  if (flags == CAPMI_GEMM_X3W || flags == (CAPMI_GEMM_X3W | CAPMI_GEMM_BF16)) {
     GemmArgs a;
     int S = 1;
     long long tiles = 0;
@@ -1166,7 +1166,8 @@ int x3w_plan(const capmi_gemm_problem* prob, int amode, int bmode, long long ws_
   return 0;
 }
 
-int gemm_x3w(const capmi_gemm_problem* prob, int amode, int bmode, void* workspace, long long ws_bytes, hipStream_t s) {
+int gemm_x3w(const capmi_gemm_problem* prob, int amode, int bmode, void* workspace, long long ws_bytes, hipStream_t s,
+             int terms) {
   const int cus = cu_count();
   const long long part_floats =
       workspace != nullptr && ws_bytes > sk_flag_bytes(cus) ? (ws_bytes - sk_flag_bytes(cus)) / 4 : 0;
@@ -1177,7 +1178,7 @@ int gemm_x3w(const capmi_gemm_problem* prob, int amode, int bmode, void* workspa
   if (rc) return rc;
   CAPMI_REQUIRE(workspace == nullptr || aligned16(workspace), CAPMI_EINVAL);
   if (S > 1) a.sk_part = reinterpret_cast<float*>(static_cast<char*>(workspace) + sk_flag_bytes(cus));
-  int e = gemm_x3w_launch(a, bmode, (int)(tiles * S), s);
+  int e = gemm_x3w_launch(a, bmode, (int)(tiles * S), s, terms);
   if (e || S == 1) return e;
   const int ldp = a.tiles_n[0] * 128;
   return capmi_splitk_reduce(a.sk_part, S, (long long)prob->M * ldp, prob->M, prob->N, ldp, nullptr, prob->C,
@@ -1290,7 +1291,9 @@ extern "C" int capmi_gemm_sk_ex(const capmi_gemm_problem* prob, int amode, int b
   if (flags == CAPMI_GEMM_X3P) return gemm_x3p(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3D) return gemm_x3d(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
   if (flags == CAPMI_GEMM_X3S) return gemm_x3s(prob, amode, bmode, as_stream(stream));
-  if (flags == CAPMI_GEMM_X3W) return gemm_x3w(prob, amode, bmode, workspace, ws_bytes, as_stream(stream));
+  if (flags == CAPMI_GEMM_X3W) return gemm_x3w(prob, amode, bmode, workspace, ws_bytes, as_stream(stream), 3);
+  if (flags == (CAPMI_GEMM_X3W | CAPMI_GEMM_BF16))  // (round 6, ABI 26) one bf16 term per operand: gemm_w16_kernel
+    return gemm_x3w(prob, amode, bmode, workspace, ws_bytes, as_stream(stream), 1);
   if (flags == CAPMI_GEMM_X3C) return gemm_x3c(prob, amode, bmode, as_stream(stream));
   int terms = flag_terms(flags);
   CAPMI_REQUIRE(terms >= 0, CAPMI_EINVAL);

@@ -135,7 +135,7 @@ int gemm_x3d_launch(const GemmArgs& a, int amode, int blocks, hipStream_t s);
 int gemm_x3s_launch(const capmi_gemm_problem& p, long long lda, int tiles, int grid, hipStream_t s);
 // conv weight gradients (gemm_x3w.hip): A = dY fp32 k rows, B = fp32 k rows (bmode 1) or the NHWC conv input's
 // implicit im2col (bmode 2), both split in-kernel; grid = tiles x S k-splits (a.kchunk[0] k-tiles each)
-int gemm_x3w_launch(const GemmArgs& a, int bmode, int blocks, hipStream_t s);
+int gemm_x3w_launch(const GemmArgs& a, int bmode, int blocks, hipStream_t s, int terms);  // terms 3 (x3) or 1 (bf16)
 // direct 3x3 conv (gemm_x3c.hip): N = 64, stride 1, pad 1, Cin % 32 == 0, W <= gemm_x3c_max_width(); one
 // workgroup per 256-pixel tile
 int gemm_x3c_launch(const capmi_gemm_problem& p, int tiles, hipStream_t s);

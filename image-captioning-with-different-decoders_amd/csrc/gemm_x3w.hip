@@ -17,6 +17,9 @@
 // batch 64): the k range is split S ways so the grid fills the CUs, and the S partial slabs are summed in a
 // fixed order afterwards (deterministic). It replaces the split-staging nts kernel's weight gradients (round-3
 // VERDICT: 0.26 of the x3 bound, 244 MB per launch against 28 MB).
+// gemm_w16_kernel (round 6, CAPMI_GEMM_X3W | CAPMI_GEMM_BF16): the same kernel with one term per operand -- each
+// fp32 value rounded to bf16 (RNE, the CAPMI_GEMM_BF16 operand contract) and one product per block -- for the
+// bf16 configuration's decoder weight gradients (capmi/decoder_core.py).
 #include "gemm_args.h"
 
 namespace {
@@ -51,10 +54,10 @@ __device__ __forceinline__ s16x4_w tr_read(const unsigned char* plane, int rowb,
 }
 
 // BMODE: CAPMI_B_KROWS (1, B dense k rows) or CAPMI_B_CONV_NHWC (2, implicit im2col of the conv input);
-// SK: k-split into partial slabs (the grid's S > 1)
-template <int BMODE, bool SK>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
-gemm_x3w_kernel(const GemmArgs args) {
+// SK: k-split into partial slabs (the grid's S > 1); TERMS: 3 (x3) or 1 (bf16 operands)
+template <int BMODE, bool SK, int TERMS>
+__device__ __forceinline__ void wgrad_body(const GemmArgs& args) {
+  static_assert(TERMS == 3 || TERMS == 1, "terms");
   __shared__ __attribute__((aligned(1024))) unsigned char lds[2 * WBUF];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -161,11 +164,11 @@ gemm_x3w_kernel(const GemmArgs args) {
       if (pc < 4) {
         const int r = a_r0 + 8 * pc;
         const int o = r * WA_ROWB + (((a_c4 >> 1) ^ wsw(r)) << 4) + (a_c4 & 1) * 8;
-        unsigned lo[3], hi[3];
+        unsigned lo[3], hi[3];  // (TERMS = 1: only term 0 = RNE(x) is stored; the rest is dead code)
         split3_pair(ra4[pc].x, ra4[pc].y, lo);
         split3_pair(ra4[pc].z, ra4[pc].w, hi);
 #pragma unroll
-        for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(base + p * WA_PLANE + o) = make_uint2(lo[p], hi[p]);
+        for (int p = 0; p < TERMS; ++p) *reinterpret_cast<uint2*>(base + p * WA_PLANE + o) = make_uint2(lo[p], hi[p]);
         return;
       }
       const int i = pc - 4;
@@ -186,7 +189,7 @@ gemm_x3w_kernel(const GemmArgs args) {
       split3_pair(v.x, v.y, lo);
       split3_pair(v.z, v.w, hi);
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
+      for (int p = 0; p < TERMS; ++p)
         *reinterpret_cast<uint2*>(base + WA_BYTES + p * WB_PLANE + o) = make_uint2(lo[p], hi[p]);
     };
     // transposed fragment reads: lane l of group g = l / 16 takes k-rows 8g + (l & 15) / 4 (+ 4), columns
@@ -202,21 +205,21 @@ gemm_x3w_kernel(const GemmArgs args) {
         const s16x4_w hi = tr_read(plane, rowb, g8 + 4 + q, col);
         return __builtin_bit_cast(bf16x8_w, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       };
-      bf16x8_w b[4][3];
+      bf16x8_w b[4][TERMS];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) b[j][p] = frag(B_ + p * WB_PLANE, WB_ROWB, wn0 + 16 * j + c4);
+        for (int p = 0; p < TERMS; ++p) b[j][p] = frag(B_ + p * WB_PLANE, WB_ROWB, wn0 + 16 * j + c4);
       // A fragments one 16-row block at a time (12 VGPRs live instead of 48)
-      bf16x8_w a[3];
+      bf16x8_w a[TERMS];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) a[p] = frag(A_ + p * WA_PLANE, WA_ROWB, wm0 + c4);
+      for (int p = 0; p < TERMS; ++p) a[p] = frag(A_ + p * WA_PLANE, WA_ROWB, wm0 + c4);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        bf16x8_w an[3];
+        bf16x8_w an[TERMS];
         if (i + 1 < 4) {
 #pragma unroll
-          for (int p = 0; p < 3; ++p) an[p] = frag(A_ + p * WA_PLANE, WA_ROWB, wm0 + 16 * (i + 1) + c4);
+          for (int p = 0; p < TERMS; ++p) an[p] = frag(A_ + p * WA_PLANE, WA_ROWB, wm0 + 16 * (i + 1) + c4);
         }
         __builtin_amdgcn_sched_barrier(0);
         // pieces i (and 2 + i for i >= 2: the input's two) of tile kt + 1 -> LDS, then their tile kt + 2 loads
@@ -224,28 +227,32 @@ gemm_x3w_kernel(const GemmArgs args) {
         if (i >= 2) store_piece(buf ^ 1, 2 + i);
         load_piece(kt + 2, i);
         if (i >= 2) load_piece(kt + 2, 2 + i);
-        // per accumulator the six products smallest terms first (gemm_x3p.hip's order)
+        // per accumulator the six products smallest terms first (gemm_x3p.hip's order); one term: a0 b0
+        if constexpr (TERMS == 3) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][1], acc4[i][j], 0, 0, 0);
-          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][2], acc4[i][j], 0, 0, 0);
-          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[j][0], acc4[i][j], 0, 0, 0);
+          for (int j = 0; j < 4; ++j) {
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][1], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][2], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[j][0], acc4[i][j], 0, 0, 0);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][1], acc4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][0], acc4[i][j], 0, 0, 0);
+          }
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][1], acc4[i][j], 0, 0, 0);
-          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][0], acc4[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j)
           acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][0], acc4[i][j], 0, 0, 0);
-        }
 #pragma unroll
-        for (int r = 0; r < 24; ++r) {  // one MFMA, then up to two VALU (the piece's split)
+        for (int r = 0; r < (TERMS == 3 ? 24 : 4); ++r) {  // one MFMA, then up to two VALU (the piece's split)
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
         if (i + 1 < 4) {
 #pragma unroll
-          for (int p = 0; p < 3; ++p) a[p] = an[p];
+          for (int p = 0; p < TERMS; ++p) a[p] = an[p];
         }
       }
       __syncthreads();
@@ -364,12 +371,34 @@ gemm_x3w_kernel(const GemmArgs args) {
     }
 }
 
+template <int BMODE, bool SK>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) gemm_x3w_kernel(const GemmArgs args) {
+  wgrad_body<BMODE, SK, 3>(args);
+}
+
+template <int BMODE, bool SK>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) gemm_w16_kernel(const GemmArgs args) {
+  wgrad_body<BMODE, SK, 1>(args);
+}
+
 }  // namespace
 
-int gemm_x3w_launch(const GemmArgs& a, int bmode, int blocks, hipStream_t s) {
+int gemm_x3w_launch(const GemmArgs& a, int bmode, int blocks, hipStream_t s, int terms) {
   const dim3 g(blocks), b(WNT);
   const bool sk = a.kchunk[0] * WBK < a.p[0].K;  // k split over several workgroups: partial slabs
-  if (bmode == 2) {
+  if (terms == 1) {
+    if (bmode == 2) {
+      if (sk)
+        CAPMI_KLAUNCH((gemm_w16_kernel<2, true>), g, b, 0, s, a);
+      else
+        CAPMI_KLAUNCH((gemm_w16_kernel<2, false>), g, b, 0, s, a);
+    } else {
+      if (sk)
+        CAPMI_KLAUNCH((gemm_w16_kernel<1, true>), g, b, 0, s, a);
+      else
+        CAPMI_KLAUNCH((gemm_w16_kernel<1, false>), g, b, 0, s, a);
+    }
+  } else if (bmode == 2) {
     if (sk)
       CAPMI_KLAUNCH((gemm_x3w_kernel<2, true>), g, b, 0, s, a);
     else

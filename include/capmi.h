@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CAPMI_ABI_VERSION 25
+#define CAPMI_ABI_VERSION 26
 
 #define CAPMI_OK 0
 #define CAPMI_EINVAL 1001   /* bad shape / argument */
@@ -154,7 +154,9 @@ int capmi_gemm_sk(const capmi_gemm_problem* problem, int amode, int bmode, int t
  * read back transposed (ds_read_b64_tr_b16); 256x128 tiles, 512 threads, one workgroup per CU. With alpha 1
  * and beta 0 the pixel range is split over several workgroups whose partial slabs go to the workspace (as
  * capmi_gemm_sk's) and are summed in a fixed order (capmi_splitk_reduce); capmi_gemm_sk_plan reports the
- * split count in `generic`. */
+ * split count in `generic`. (ABI 26) CAPMI_GEMM_X3W | CAPMI_GEMM_BF16: the same kernel with one term per operand --
+ * each fp32 value rounded to bf16 (RNE), one product, fp32 accumulation: the CAPMI_GEMM_BF16 operand contract for
+ * weight gradients (gemm_w16_kernel). */
 #define CAPMI_GEMM_X3W 128
 /* CAPMI_GEMM_X3C (alone, ABI 23): DIRECT 3x3 convolution in the CAPMI_GEMM_X3 arithmetic for short-channel
  * layers (layer1's 3x3): CAPMI_A_CONV_NHWC with KH = KW = 3, stride 1, pad 1, Cin % 32 == 0, W <= 64, the
