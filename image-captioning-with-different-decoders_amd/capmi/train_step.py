@@ -7,15 +7,15 @@
 
 Launch modes:
   * eager: every call launches the ~530 kernels of the step from Python;
-  * pipelined (``pipeline=True``): call k runs the encoder of batch k on a low-priority stream
-    while the decoder step of batch k-1 runs on a high-priority one. The encoder is frozen and
+  * pipelined (``pipeline=True``): call k runs the encoder of batch k on a high-priority stream
+    while the decoder step of batch k-1 runs on a low-priority one (round 6; before, the other way round). The encoder is frozen and
     reads no decoder state, so the result is bit-identical to the sequential order; the
     decoder's latency-bound per-timestep kernels leave most CUs idle, which the encoder's
     GEMMs fill. Each call returns the loss of the previous batch (None on the first);
     ``flush()`` runs the last decoder step and returns its loss;
   * pipelined graphs (``pipeline=True, graph=True``): as pipelined, but each stream replays a
-    captured graph (encoder forward per feature slot on the low-priority stream, decoder step +
-    update per slot on the high-priority one), which removes the launch gaps of ~530 short kernels;
+    captured graph (encoder forward per feature slot on the high-priority stream, decoder step +
+    update per slot on the low-priority one), which removes the launch gaps of ~530 short kernels;
   * graph (``graph=True``): the step is captured once into a HIP graph (torch.cuda.CUDAGraph)
     and replayed; inputs are copied into static buffers first. Everything that changes from
     step to step lives on the device (Adam's step count, the dropout seed counter), so a
@@ -106,7 +106,9 @@ class AttentionTrainStep:
             self.graph_mode = False
             self._pg = None
             lo, hi = torch.cuda.Stream.priority_range()
-            pe, pd = {"swap": (hi, lo), "equal": (lo, lo)}.get(os.environ.get("CAPMI_PIPE_PRIO", ""), (lo, hi))
+            # encoder high / decoder low since round 6 (same box, three interleaved rounds: config 2 6300 -> 6321,
+            # config 5 13137 -> 13254 img/s); CAPMI_PIPE_PRIO=dec: decoder high (the earlier default), equal: one level
+            pe, pd = {"dec": (lo, hi), "equal": (lo, lo)}.get(os.environ.get("CAPMI_PIPE_PRIO", ""), (hi, lo))
             self.s_enc = torch.cuda.Stream(device=dev, priority=pe)
             self.s_dec = torch.cuda.Stream(device=dev, priority=pd)
             self._feats = [None, None]
