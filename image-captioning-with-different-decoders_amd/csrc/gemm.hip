@@ -700,14 +700,17 @@ struct Bf16Plan {
   long long total;
 };
 Bf16Plan bf16_io_plan(const capmi_gemm_problem& p, int tile, bool have_ws) {
-  // AUTO on a short k (K <= 128, and K = 256 on 64 columns: the bf16 config's layer1/2 1x1 c3 convs, layer1's K = 64
-  // convs and downsample, layer1's c1): 128x64 tiles, one LDS
-  // stage, four workgroups per CU, data-parallel (round 5: l3 c3 20.0 -> 17.1 us, l2 c3 24.7 -> 18.4, l1 c3 33.3 ->
-  // 24.3; at K = 512 a tie and above it slower: the two-stage 128x128 form stays)
-  // (round 6) at K = 256 with N >= 128 the DMA ring below is faster (l3 c3 17.3 -> 16.0 us, ds2 29.3 -> 28.1); at
-  // K <= 128 and on 64-column K = 256 grids the one-stage form stays (l1 c3 25.4 / 29.7, ds1 24.4 / 28.5, l1 c1 22.1 /
-  // 25.6 us one-stage / ring)
-  const bool st1 = tile == CAPMI_TILE_AUTO && (p.K <= 128 || (p.K <= 256 && p.N <= 64));
+  // AUTO on a short k (K <= 256: the bf16 config's 1x1 c3 convs, layer1's K = 64 convs and downsample, the c1 of
+  // layer1): 128x64 tiles, one LDS stage, four workgroups per CU, data-parallel (round 5: l3 c3 20.0 -> 17.1 us, l2 c3
+  // 24.7 -> 18.4, l1 c3 33.3 -> 24.3; at K = 512 a tie and above it slower). Round 6: alone, the K = 256 convs on 128+
+  // columns run faster on the DMA ring below (l3 c3 17.3 -> 16.0 us, ds2 29.3 -> 28.1), but in the pipelined config-5
+  // step the one-stage form stays ahead (13330 -> 13365 img/s, three interleaved rounds, same box); CAPMI_BF16_ST1_K = k
+  // moves the bound (A/B)
+  static const int st1_k = [] {
+    const char* e = getenv("CAPMI_BF16_ST1_K");
+    return e ? atoi(e) : 256;
+  }();
+  const bool st1 = tile == CAPMI_TILE_AUTO && p.K <= st1_k;
   // AUTO on a grid of 128x128 tiles that fills at most half the CUs (layer4's 3136-row convs: 100 tiles):
   // 128x64 tiles, twice the workgroups (round 5: l4 3x3 53.2 -> 40.8 us, l4 c1 25.8 -> 18.9; the 400-tile
   // layer4 c3 / downsample and layer3's 196-tile grids stay at 128x128, where 128x64 measured slower)

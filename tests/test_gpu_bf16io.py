@@ -78,9 +78,8 @@ def test_bf16io_conv(N, H, Cin, Cout, k, s, tile):
     assert torch.equal(out.view(torch.int16), out2.view(torch.int16))
 
 
-# short k under AUTO: the one-stage 128x64 form (round 5; K <= 128, or K = 256 on 64 columns) or, at K = 256 on wider
-# grids, the DMA ring (round 6) -- the l3 c3 shape, a partial last row tile, N not a multiple of 64 (general
-# epilogue), layer1's K = 64
+# K <= 256 under AUTO: the one-stage 128x64 form (round 5) -- the l3 c3 shape, a partial last row tile, N not a
+# multiple of 64 (general epilogue), layer1's K = 64; K = 512 / 576 / 1024: the DMA ring
 @pytest.mark.parametrize("M,N,Kd,tile", [(12544, 256, 1024, 3), (1000, 512, 256, 3), (300, 64, 128, 3),
                                          (12544, 1024, 256, 3), (500, 200, 192, 3), (2000, 256, 64, 3),
                                          (40000, 128, 512, 3), (3000, 320, 576, 3)])

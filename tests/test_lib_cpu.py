@@ -174,14 +174,15 @@ def test_gemm_sk_plan_on_host():
         rc = lib.capmi_gemm_sk_plan(ctypes.byref(p), amode, 0, 3, 2, *[ctypes.byref(x) for x in v])
         return rc, tuple(x.value for x in v)
 
-    # config 5 at batch 64: layer2's 1x1 c3 (K = 128) and layer1's c1 (K = 256, N = 64) take the one-stage 128x64
-    # form, layer3's c3 (K = 256, N = 1024: 784 tiles) the two-deep DMA ring; layer3's 3x3 (196 tiles of
+    # config 5 at batch 64: the K <= 256 1x1s (layer2's c3, layer1's c1, layer3's c3) take the one-stage 128x64
+    # form; layer3's 3x3 (196 tiles of
     # 128x128: one round on 256 CUs) the four-deep DMA ring on 512 threads; layer2's 3x3 (392 tiles) the two-deep
     # ring; layer4's 3x3 (100 tiles: at most half of the CUs) 128x64 tiles (200), four deep on 256 threads
     rc, (bm, bn, sk, stages, nt) = bf16_plan(50176, 512, 128)
     assert rc == 0 and (bm, bn, sk, stages, nt) == (128, 64, 0, 1, 256)
     assert bf16_plan(200704, 64, 256)[1] == (128, 64, 0, 1, 256)
-    assert bf16_plan(12544, 1024, 256)[1] == (128, 128, 0, 2, 512)
+    assert bf16_plan(12544, 1024, 256)[1] == (128, 64, 0, 1, 256)
+    assert bf16_plan(12544, 256, 1024)[1] == (128, 128, 0, 4, 512)
     assert bf16_plan(12544, 256, 2304, conv=(64, 14, 256, 3, 1))[1] == (128, 128, 0, 4, 512)
     assert bf16_plan(50176, 128, 1152, conv=(64, 28, 128, 3, 1))[1] == (128, 128, 0, 2, 512)
     assert bf16_plan(3136, 512, 4608, conv=(64, 7, 512, 3, 1))[1] == (128, 64, 0, 4, 256)
