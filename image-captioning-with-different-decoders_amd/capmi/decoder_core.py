@@ -69,7 +69,7 @@ def _split(M, N, K_, tile, target=None, min_k=128):
 
 
 class DecoderDims:
-    def __init__(self, B, T, L, P, A, D, M, V, E=E_DIM):
+    def __init__(self, B, T, L, P, A, D, M, V, E=E_DIM, gemm_flags=0):
         self.B, self.T, self.L, self.P, self.A, self.D, self.M, self.V, self.E = B, T, L, P, A, D, M, V, E
         self.X = M + E
         for name, v in (("A", A), ("D", D), ("M", M), ("E", E)):
@@ -83,13 +83,16 @@ class DecoderDims:
         self.s_dx = _split(B, E, 4 * D, K.TILE_64)
         self.s_dh = (_split(B, D, 4 * D, K.TILE_64, DEC_WGS * 3 // 8), _split(B, D, E, K.TILE_64, DEC_WGS * 3 // 8),
                      _split(B, D, A, K.TILE_64, DEC_WGS // 4))
-        # decoder_step.hip (CAPMI_DEC_FUSED, opt-in): "1" the attention forward (score + softmax +
-        # context + gate) and backward (gate split + context + softmax + score) as one launch each,
-        # reading the split-K GEMM partials; "2" also the last-arriver GEMMs with the LSTM cell in
-        # their epilogue (three launches per timestep each way). "0" (default) the five-launch path:
-        # measured on one box "1" is 0.9 % faster run alone but 1.1 % slower in the
-        # pipelined step, "2" 3.5 % slower
-        mode = os.environ.get("CAPMI_DEC_FUSED", "0")
+        # decoder_step.hip (CAPMI_DEC_FUSED): "1" (default since round 6) the attention forward (score +
+        # softmax + context + gate) and backward (gate split + context + softmax + score) as one launch
+        # each, reading the split-K GEMM partials; "2" also the last-arriver GEMMs with the LSTM cell in
+        # their epilogue (three launches per timestep each way); "0" the five-launch path. Measured
+        # (DESIGN.md 4.5): through round 5 "1" was 0.9 % faster alone but 1.1 % slower in the pipelined
+        # step; with the encoder stream at high priority (round 6) it is ahead in the pipelined step
+        # too on every interleaved round (config 2 6214 -> 6245, config 4 2151 -> 2157 img/s, same box), but
+        # not with the bf16 GEMMs (config 5 13096 -> 12767): default "1" except for CAPMI_GEMM_BF16; "2" stays
+        # 5 % slower
+        mode = os.environ.get("CAPMI_DEC_FUSED", "0" if gemm_flags == CAPMI_GEMM_BF16 else "1")
         self.fused_att = mode != "0" and P <= 56 and E + P + 4100 <= 16384
         self.fused = (mode == "2" and self.fused_att and A % 32 == 0 and D % 32 == 0 and E % 64 == 0
                       and M % 4 == 0)
@@ -286,7 +289,7 @@ class DecoderCore:
         D = p["decode_step.weight_hh"].shape[1]
         M = p["embedding.weight"].shape[1] if emb_dense is None else emb_dense.shape[2]
         V = p["fc.weight"].shape[0]
-        dm = DecoderDims(B, T, L, P, A, D, M, V, E)
+        dm = DecoderDims(B, T, L, P, A, D, M, V, E, gemm_flags=gf)
         ws = self.workspace(dm, enc.device)
         X = dm.X
         bt = [sum(1 for l in decode_lengths if l > t) for t in range(T)]
